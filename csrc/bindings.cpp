@@ -1,0 +1,313 @@
+// Python bindings for the MI355X K-FAC kernels (module
+// distributed_kfac_pytorch_amd._C).  This is the only translation unit that
+// includes torch; it validates tensors, picks the current HIP stream and
+// calls the raw launchers in the *.hip files.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
+
+#include <hip/hip_runtime.h>
+#include <vector>
+
+#include "common.h"
+
+namespace kfac {
+// pack.hip
+void triu_pack(int dtype, const void* src, int64_t ld, int64_t n, void* dst,
+               hipStream_t s);
+void triu_unpack(int dtype, const void* packed, int64_t n, void* dst,
+                 int64_t ld, float scale, hipStream_t s);
+void scale_copy(int dtype, const void* src, void* dst, int64_t n, float scale,
+                hipStream_t s);
+// syrk.hip
+int64_t syrk_workspace_splits(int64_t N, int64_t D);
+void syrk(int in_dtype, const void* x, int64_t N, int64_t K, int64_t ldx,
+          bool bias, float* C, int64_t D, int64_t ldc, float alpha,
+          float beta, int splits, hipStream_t s);
+// im2col.hip
+void im2col_nhwc(int dtype, const void* x, int64_t B, int64_t H, int64_t W,
+                 int64_t C, int64_t sB, int64_t sH, int64_t sW, int kh, int kw,
+                 int sh, int sw, int ph, int pw, int64_t OH, int64_t OW,
+                 void* out, int64_t ldo, int out_dtype, hipStream_t s);
+void im2col_nchw(int dtype, const void* x, int64_t B, int64_t C, int64_t H,
+                 int64_t W, int64_t sB, int64_t sC, int64_t sH, int64_t sW,
+                 int kh, int kw, int sh, int sw, int ph, int pw, int64_t OH,
+                 int64_t OW, void* out, int64_t ldo, int out_dtype,
+                 hipStream_t s);
+// precond.hip
+void eigen_scale(float* v, int64_t rows, int64_t cols, int64_t ldv,
+                 const float* dgda, const float* dg, const float* da,
+                 float damping, hipStream_t s);
+void kl_dot_accumulate(const float* p, int64_t rows, int64_t cols, int64_t ldp,
+                       const void* wgrad, int wdtype, int64_t ldw,
+                       const void* bgrad, int bdtype, double* acc,
+                       hipStream_t s);
+void kl_scale_finalize(const double* acc, float* scale_out, float kl_clip,
+                       float lr, hipStream_t s);
+void apply_grad(const float* p, int64_t rows, int64_t cols, int64_t ldp,
+                void* wgrad, int wdtype, int64_t ldw, void* bgrad, int bdtype,
+                const float* scale, hipStream_t s);
+void fill_identity_lerp(float* C, int64_t n, int64_t ldc, hipStream_t s);
+// eigh_jacobi.hip
+int jacobi_max_n();
+void jacobi_eigh_batched(const float* A, int64_t n, int64_t batch,
+                         int64_t strideA, float* evals, float* evecs,
+                         int64_t strideV, int max_sweeps, float tol,
+                         hipStream_t s);
+}  // namespace kfac
+
+namespace {
+
+hipStream_t cur_stream() {
+  return c10::hip::getCurrentHIPStream().stream();
+}
+
+int dtype_tag(const at::Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kFloat: return kfac::kF32;
+    case at::kBFloat16: return kfac::kBF16;
+    case at::kDouble: return kfac::kF64;
+    case at::kHalf: return kfac::kF16;
+    default:
+      TORCH_CHECK(false, "kfac native: unsupported dtype ", t.scalar_type());
+  }
+  return -1;
+}
+
+void check_cuda(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), "kfac native: ", name, " must be a GPU tensor");
+}
+
+// ---------------------------------------------------------------- pack
+void triu_pack(const at::Tensor& src, at::Tensor& dst) {
+  check_cuda(src, "src");
+  check_cuda(dst, "dst");
+  TORCH_CHECK(src.dim() == 2 && src.size(0) == src.size(1), "square src");
+  TORCH_CHECK(src.stride(1) == 1, "src rows must be contiguous");
+  TORCH_CHECK(dst.is_contiguous() && dst.scalar_type() == src.scalar_type());
+  const int64_t n = src.size(0);
+  TORCH_CHECK(dst.numel() == n * (n + 1) / 2, "dst size");
+  c10::hip::HIPGuard g(src.device());
+  kfac::triu_pack(dtype_tag(src), src.data_ptr(), src.stride(0), n,
+                  dst.data_ptr(), cur_stream());
+}
+
+void triu_unpack(at::Tensor& dst, const at::Tensor& packed, double scale) {
+  check_cuda(dst, "dst");
+  check_cuda(packed, "packed");
+  TORCH_CHECK(dst.dim() == 2 && dst.size(0) == dst.size(1), "square dst");
+  TORCH_CHECK(dst.stride(1) == 1, "dst rows must be contiguous");
+  TORCH_CHECK(packed.is_contiguous() &&
+              packed.scalar_type() == dst.scalar_type());
+  const int64_t n = dst.size(0);
+  TORCH_CHECK(packed.numel() == n * (n + 1) / 2, "packed size");
+  c10::hip::HIPGuard g(dst.device());
+  kfac::triu_unpack(dtype_tag(dst), packed.data_ptr(), n, dst.data_ptr(),
+                    dst.stride(0), (float)scale, cur_stream());
+}
+
+void scale_copy(at::Tensor& dst, const at::Tensor& src, double scale) {
+  check_cuda(dst, "dst");
+  check_cuda(src, "src");
+  TORCH_CHECK(dst.is_contiguous() && src.is_contiguous());
+  TORCH_CHECK(dst.numel() == src.numel());
+  TORCH_CHECK(dst.scalar_type() == src.scalar_type());
+  c10::hip::HIPGuard g(dst.device());
+  kfac::scale_copy(dtype_tag(dst), src.data_ptr(), dst.data_ptr(),
+                   dst.numel(), (float)scale, cur_stream());
+}
+
+// ---------------------------------------------------------------- syrk
+// C[D,D] = beta*C + alpha * Xt^T Xt, Xt = [X | 1] when bias.
+void syrk(const at::Tensor& x, at::Tensor& C, bool bias, double alpha,
+          double beta, int64_t splits) {
+  check_cuda(x, "x");
+  check_cuda(C, "C");
+  TORCH_CHECK(x.dim() == 2, "x must be 2D [N, K]");
+  TORCH_CHECK(x.stride(1) == 1, "x rows must be contiguous (stride(1)==1)");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 ||
+                  x.scalar_type() == at::kFloat,
+              "syrk input must be bf16 or fp32");
+  TORCH_CHECK(C.scalar_type() == at::kFloat, "syrk output must be fp32");
+  TORCH_CHECK(C.dim() == 2 && C.size(0) == C.size(1) && C.stride(1) == 1);
+  const int64_t N = x.size(0), K = x.size(1);
+  const int64_t D = K + (bias ? 1 : 0);
+  TORCH_CHECK(C.size(0) == D, "C must be [K+bias, K+bias]");
+  const int64_t ldx = N > 1 ? x.stride(0) : K;
+  c10::hip::HIPGuard g(x.device());
+  int sp = splits > 0 ? (int)splits : (int)kfac::syrk_workspace_splits(N, D);
+  kfac::syrk(dtype_tag(x), x.data_ptr(), N, K, ldx, bias,
+             C.data_ptr<float>(), D, C.stride(0), (float)alpha, (float)beta,
+             sp, cur_stream());
+}
+
+// --------------------------------------------------------------- im2col
+// x: [B, C, H, W] logical (any strides; NHWC fast path when channels_last).
+// out: [B*OH*OW, ldo] rows; columns in (kh, kw, c) order for the NHWC path
+// ("natural" order) and (c, kh, kw) order for the NCHW path (reference
+// order, kfac/layers/modules.py:210-237).
+void im2col(const at::Tensor& x, at::Tensor& out, int64_t kh, int64_t kw,
+            int64_t sh, int64_t sw, int64_t ph, int64_t pw, bool natural) {
+  check_cuda(x, "x");
+  check_cuda(out, "out");
+  TORCH_CHECK(x.dim() == 4, "x must be [B, C, H, W]");
+  TORCH_CHECK(out.dim() == 2 && out.stride(1) == 1);
+  const int64_t B = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int64_t OH = (H + 2 * ph - kh) / sh + 1;
+  const int64_t OW = (W + 2 * pw - kw) / sw + 1;
+  TORCH_CHECK(out.size(0) == B * OH * OW, "out rows");
+  TORCH_CHECK(out.size(1) >= C * kh * kw, "out cols");
+  c10::hip::HIPGuard g(x.device());
+  if (natural) {
+    TORCH_CHECK(x.stride(1) == 1, "natural im2col needs channels_last input");
+    kfac::im2col_nhwc(dtype_tag(x), x.data_ptr(), B, H, W, C, x.stride(0),
+                      x.stride(2), x.stride(3), (int)kh, (int)kw, (int)sh,
+                      (int)sw, (int)ph, (int)pw, OH, OW, out.data_ptr(),
+                      out.stride(0), dtype_tag(out), cur_stream());
+  } else {
+    kfac::im2col_nchw(dtype_tag(x), x.data_ptr(), B, C, H, W, x.stride(0),
+                      x.stride(1), x.stride(2), x.stride(3), (int)kh, (int)kw,
+                      (int)sh, (int)sw, (int)ph, (int)pw, OH, OW,
+                      out.data_ptr(), out.stride(0), dtype_tag(out),
+                      cur_stream());
+  }
+}
+
+// ------------------------------------------------------------ precondition
+void eigen_scale(at::Tensor& v, const c10::optional<at::Tensor>& dgda,
+                 const c10::optional<at::Tensor>& dg,
+                 const c10::optional<at::Tensor>& da, double damping) {
+  check_cuda(v, "v");
+  TORCH_CHECK(v.scalar_type() == at::kFloat && v.dim() == 2 &&
+              v.stride(1) == 1);
+  c10::hip::HIPGuard g(v.device());
+  if (dgda.has_value()) {
+    TORCH_CHECK(dgda->is_contiguous() && dgda->sizes() == v.sizes() &&
+                dgda->scalar_type() == at::kFloat);
+    kfac::eigen_scale(v.data_ptr<float>(), v.size(0), v.size(1), v.stride(0),
+                      dgda->data_ptr<float>(), nullptr, nullptr, 0.f,
+                      cur_stream());
+  } else {
+    TORCH_CHECK(dg.has_value() && da.has_value());
+    TORCH_CHECK(dg->is_contiguous() && da->is_contiguous());
+    TORCH_CHECK(dg->numel() == v.size(0) && da->numel() == v.size(1));
+    kfac::eigen_scale(v.data_ptr<float>(), v.size(0), v.size(1), v.stride(0),
+                      nullptr, dg->data_ptr<float>(), da->data_ptr<float>(),
+                      (float)damping, cur_stream());
+  }
+}
+
+// acc[0] += sum(P[:, :in] * Wg) + sum(P[:, in] * bg)   (double accumulator)
+void kl_dot(const at::Tensor& p, const at::Tensor& wgrad,
+            const c10::optional<at::Tensor>& bgrad, at::Tensor& acc) {
+  check_cuda(p, "p");
+  TORCH_CHECK(p.scalar_type() == at::kFloat && p.dim() == 2 &&
+              p.stride(1) == 1);
+  TORCH_CHECK(acc.scalar_type() == at::kDouble && acc.numel() >= 1);
+  const int64_t rows = p.size(0);
+  const int64_t wcols = p.size(1) - (bgrad.has_value() ? 1 : 0);
+  TORCH_CHECK(wgrad.numel() == rows * wcols, "weight grad size");
+  TORCH_CHECK(wgrad.is_contiguous(), "weight grad must be contiguous");
+  c10::hip::HIPGuard g(p.device());
+  const void* bptr = nullptr;
+  int bdt = kfac::kF32;
+  if (bgrad.has_value()) {
+    TORCH_CHECK(bgrad->is_contiguous() && bgrad->numel() == rows);
+    bptr = bgrad->data_ptr();
+    bdt = dtype_tag(*bgrad);
+  }
+  kfac::kl_dot_accumulate(p.data_ptr<float>(), rows, p.size(1), p.stride(0),
+                          wgrad.data_ptr(), dtype_tag(wgrad), wcols, bptr, bdt,
+                          acc.data_ptr<double>(), cur_stream());
+}
+
+void kl_finalize(const at::Tensor& acc, at::Tensor& scale, double kl_clip,
+                 double lr) {
+  TORCH_CHECK(acc.scalar_type() == at::kDouble);
+  TORCH_CHECK(scale.scalar_type() == at::kFloat);
+  c10::hip::HIPGuard g(acc.device());
+  kfac::kl_scale_finalize(acc.data_ptr<double>(), scale.data_ptr<float>(),
+                          (float)kl_clip, (float)lr, cur_stream());
+}
+
+// wgrad = scale * P[:, :in], bgrad = scale * P[:, in]  (scale on device or
+// None for 1)
+void apply_grad(const at::Tensor& p, at::Tensor& wgrad,
+                c10::optional<at::Tensor> bgrad,
+                const c10::optional<at::Tensor>& scale) {
+  check_cuda(p, "p");
+  TORCH_CHECK(p.scalar_type() == at::kFloat && p.dim() == 2 &&
+              p.stride(1) == 1);
+  const int64_t rows = p.size(0);
+  const int64_t wcols = p.size(1) - (bgrad.has_value() ? 1 : 0);
+  TORCH_CHECK(wgrad.numel() == rows * wcols && wgrad.is_contiguous());
+  c10::hip::HIPGuard g(p.device());
+  void* bptr = nullptr;
+  int bdt = kfac::kF32;
+  if (bgrad.has_value()) {
+    TORCH_CHECK(bgrad->is_contiguous() && bgrad->numel() == rows);
+    bptr = bgrad->data_ptr();
+    bdt = dtype_tag(*bgrad);
+  }
+  const float* sptr = nullptr;
+  if (scale.has_value()) {
+    TORCH_CHECK(scale->scalar_type() == at::kFloat);
+    sptr = scale->data_ptr<float>();
+  }
+  kfac::apply_grad(p.data_ptr<float>(), rows, p.size(1), p.stride(0),
+                   wgrad.data_ptr(), dtype_tag(wgrad), wcols, bptr, bdt, sptr,
+                   cur_stream());
+}
+
+void fill_identity(at::Tensor& C) {
+  check_cuda(C, "C");
+  TORCH_CHECK(C.scalar_type() == at::kFloat && C.dim() == 2 &&
+              C.size(0) == C.size(1) && C.stride(1) == 1);
+  c10::hip::HIPGuard g(C.device());
+  kfac::fill_identity_lerp(C.data_ptr<float>(), C.size(0), C.stride(0),
+                           cur_stream());
+}
+
+// ------------------------------------------------------------ eigensolver
+// A: [batch, n, n] fp32 symmetric.  Returns (evals [batch, n] ascending,
+// evecs [batch, n, n] with eigenvectors in COLUMNS, like torch.linalg.eigh).
+std::vector<at::Tensor> jacobi_eigh(const at::Tensor& A, int64_t max_sweeps,
+                                    double tol) {
+  check_cuda(A, "A");
+  TORCH_CHECK(A.scalar_type() == at::kFloat && A.dim() == 3 &&
+              A.size(1) == A.size(2) && A.is_contiguous());
+  const int64_t batch = A.size(0), n = A.size(1);
+  TORCH_CHECK(n <= kfac::jacobi_max_n(), "jacobi_eigh supports n <= ",
+              kfac::jacobi_max_n());
+  auto evals = at::empty({batch, n}, A.options());
+  auto evecs = at::empty({batch, n, n}, A.options());
+  c10::hip::HIPGuard g(A.device());
+  if (batch > 0 && n > 0) {
+    kfac::jacobi_eigh_batched(A.data_ptr<float>(), n, batch, n * n,
+                              evals.data_ptr<float>(),
+                              evecs.data_ptr<float>(), n * n,
+                              (int)max_sweeps, (float)tol, cur_stream());
+  }
+  return {evals, evecs};
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "MI355X (gfx950) HIP kernels for distributed K-FAC";
+  m.def("triu_pack", &triu_pack);
+  m.def("triu_unpack", &triu_unpack);
+  m.def("scale_copy", &scale_copy);
+  m.def("syrk", &syrk, py::arg("x"), py::arg("C"), py::arg("bias"),
+        py::arg("alpha"), py::arg("beta"), py::arg("splits") = 0);
+  m.def("syrk_default_splits", &kfac::syrk_workspace_splits);
+  m.def("im2col", &im2col);
+  m.def("eigen_scale", &eigen_scale);
+  m.def("kl_dot", &kl_dot);
+  m.def("kl_finalize", &kl_finalize);
+  m.def("apply_grad", &apply_grad);
+  m.def("fill_identity", &fill_identity);
+  m.def("jacobi_eigh", &jacobi_eigh);
+  m.def("jacobi_max_n", &kfac::jacobi_max_n);
+  m.attr("arch") = "gfx950";
+}

@@ -1,0 +1,190 @@
+// K-HIP-2 (stage 1): convolution patch extraction for the K-FAC A factor.
+//
+// Reference: Conv2dModuleHelper._extract_patches (kfac/layers/modules.py:
+// 210-237) = pad + unfold x2 + transpose + contiguous, in (c, kh, kw) column
+// order and fp32/whatever the activation dtype is.  Here:
+//   * NHWC (channels_last) input -> rows (b, oy, ox), columns in the
+//     "natural" (kh, kw, c) order.  Every (ky, kx) tap is a contiguous copy of
+//     C channels, so the kernel moves 16-byte vectors end to end.  The K-FAC
+//     layer keeps its A factor in this order and views the channels_last
+//     weight gradient, whose physical layout is [out][kh][kw][c], with the
+//     same column order -- no permutation anywhere on the hot path.
+//   * NCHW input -> reference (c, kh, kw) order.
+// Zero padding and stride are honoured; dilation / groups are rejected by
+// the Python side (the reference silently ignores them).
+#include "common.h"
+
+namespace kfac {
+
+namespace {
+
+template <typename TI, typename TO>
+__device__ __forceinline__ TO cvt(TI v) {
+  return (TO)(float)v;
+}
+template <>
+__device__ __forceinline__ float cvt<float, float>(float v) { return v; }
+template <>
+__device__ __forceinline__ bf16_t cvt<bf16_t, bf16_t>(bf16_t v) { return v; }
+
+// scalar path: one thread per output element, c fastest (coalesced both ways)
+template <typename TI, typename TO>
+__global__ void __launch_bounds__(256)
+im2col_nhwc_kernel(const TI* __restrict__ x, int64_t H, int64_t W, int64_t C,
+                   int64_t sB, int64_t sH, int64_t sW, int kh, int kw, int sh,
+                   int sw, int ph, int pw, int64_t OH, int64_t OW,
+                   TO* __restrict__ out, int64_t ldo, int64_t total) {
+  const int64_t KC = (int64_t)kh * kw * C;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += stride) {
+    const int64_t row = e / KC;
+    const int64_t col = e - row * KC;
+    const int64_t tap = col / C;
+    const int64_t c = col - tap * C;
+    const int ky = (int)(tap / kw), kx = (int)(tap - (int64_t)(tap / kw) * kw);
+    const int64_t b = row / (OH * OW);
+    const int64_t rem = row - b * OH * OW;
+    const int64_t oy = rem / OW, ox = rem - (rem / OW) * OW;
+    const int64_t iy = oy * sh - ph + ky, ix = ox * sw - pw + kx;
+    TO v = cvt<float, TO>(0.f);
+    if (iy >= 0 && iy < H && ix >= 0 && ix < W)
+      v = cvt<TI, TO>(x[b * sB + iy * sH + ix * sW + c]);
+    out[row * ldo + col] = v;
+  }
+}
+
+// vector path (same dtype in/out, C*sizeof % 16 == 0, aligned): one thread
+// per 16-byte chunk of channels.
+template <typename T>
+__global__ void __launch_bounds__(256)
+im2col_nhwc_vec_kernel(const T* __restrict__ x, int64_t H, int64_t W,
+                       int64_t C, int64_t sB, int64_t sH, int64_t sW, int kh,
+                       int kw, int sh, int sw, int ph, int pw, int64_t OH,
+                       int64_t OW, T* __restrict__ out, int64_t ldo,
+                       int64_t total_chunks) {
+  constexpr int V = 16 / sizeof(T);
+  const int64_t CC = C / V;             // chunks per tap
+  const int64_t KCC = (int64_t)kh * kw * CC;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+       e < total_chunks; e += stride) {
+    const int64_t row = e / KCC;
+    const int64_t colc = e - row * KCC;
+    const int64_t tap = colc / CC;
+    const int64_t cc = colc - tap * CC;
+    const int ky = (int)(tap / kw), kx = (int)(tap - (int64_t)(tap / kw) * kw);
+    const int64_t b = row / (OH * OW);
+    const int64_t rem = row - b * OH * OW;
+    const int64_t oy = rem / OW, ox = rem - (rem / OW) * OW;
+    const int64_t iy = oy * sh - ph + ky, ix = ox * sw - pw + kx;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (iy >= 0 && iy < H && ix >= 0 && ix < W)
+      v = *reinterpret_cast<const uint4*>(x + b * sB + iy * sH + ix * sW +
+                                          cc * V);
+    *reinterpret_cast<uint4*>(out + row * ldo + tap * C + cc * V) = v;
+  }
+}
+
+// NCHW -> reference (c, kh, kw) order; one thread per output element.
+template <typename TI, typename TO>
+__global__ void __launch_bounds__(256)
+im2col_nchw_kernel(const TI* __restrict__ x, int64_t C, int64_t H, int64_t W,
+                   int64_t sB, int64_t sC, int64_t sH, int64_t sW, int kh,
+                   int kw, int sh, int sw, int ph, int pw, int64_t OH,
+                   int64_t OW, TO* __restrict__ out, int64_t ldo,
+                   int64_t total) {
+  const int64_t KK = (int64_t)kh * kw;
+  const int64_t KC = KK * C;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += stride) {
+    const int64_t row = e / KC;
+    const int64_t col = e - row * KC;
+    const int64_t c = col / KK;
+    const int64_t tap = col - c * KK;
+    const int ky = (int)(tap / kw), kx = (int)(tap - (int64_t)(tap / kw) * kw);
+    const int64_t b = row / (OH * OW);
+    const int64_t rem = row - b * OH * OW;
+    const int64_t oy = rem / OW, ox = rem - (rem / OW) * OW;
+    const int64_t iy = oy * sh - ph + ky, ix = ox * sw - pw + kx;
+    TO v = cvt<float, TO>(0.f);
+    if (iy >= 0 && iy < H && ix >= 0 && ix < W)
+      v = cvt<TI, TO>(x[b * sB + c * sC + iy * sH + ix * sW]);
+    out[row * ldo + col] = v;
+  }
+}
+
+inline unsigned grid_for(int64_t n) {
+  int64_t g = ceil_div(n, 256);
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  return (unsigned)g;
+}
+
+template <typename TI, typename TO>
+void nhwc_dispatch(const void* x, int64_t B, int64_t H, int64_t W, int64_t C,
+                   int64_t sB, int64_t sH, int64_t sW, int kh, int kw, int sh,
+                   int sw, int ph, int pw, int64_t OH, int64_t OW, void* out,
+                   int64_t ldo, hipStream_t s) {
+  const int64_t rows = B * OH * OW;
+  if constexpr (std::is_same<TI, TO>::value) {
+    constexpr int V = 16 / sizeof(TI);
+    const bool ok =
+        (C % V == 0) && (sB % V == 0) && (sH % V == 0) && (sW % V == 0) &&
+        (ldo % V == 0) &&
+        ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(out)) &
+         15) == 0;
+    if (ok) {
+      const int64_t chunks = rows * kh * kw * (C / V);
+      im2col_nhwc_vec_kernel<TI><<<grid_for(chunks), 256, 0, s>>>(
+          (const TI*)x, H, W, C, sB, sH, sW, kh, kw, sh, sw, ph, pw, OH, OW,
+          (TI*)out, ldo, chunks);
+      return;
+    }
+  }
+  const int64_t total = rows * kh * kw * C;
+  im2col_nhwc_kernel<TI, TO><<<grid_for(total), 256, 0, s>>>(
+      (const TI*)x, H, W, C, sB, sH, sW, kh, kw, sh, sw, ph, pw, OH, OW,
+      (TO*)out, ldo, total);
+}
+
+}  // namespace
+
+void im2col_nhwc(int dtype, const void* x, int64_t B, int64_t H, int64_t W,
+                 int64_t C, int64_t sB, int64_t sH, int64_t sW, int kh, int kw,
+                 int sh, int sw, int ph, int pw, int64_t OH, int64_t OW,
+                 void* out, int64_t ldo, int out_dtype, hipStream_t s) {
+  if (B * OH * OW == 0) return;
+#define KFAC_NHWC(TI, TO) \
+  nhwc_dispatch<TI, TO>(x, B, H, W, C, sB, sH, sW, kh, kw, sh, sw, ph, pw, OH, OW, out, ldo, s)
+  if (dtype == kBF16 && out_dtype == kBF16) KFAC_NHWC(bf16_t, bf16_t);
+  else if (dtype == kF32 && out_dtype == kF32) KFAC_NHWC(float, float);
+  else if (dtype == kF32 && out_dtype == kBF16) KFAC_NHWC(float, bf16_t);
+  else if (dtype == kBF16 && out_dtype == kF32) KFAC_NHWC(bf16_t, float);
+  else if (dtype == kF16 && out_dtype == kBF16) KFAC_NHWC(__half, bf16_t);
+  else if (dtype == kF16 && out_dtype == kF32) KFAC_NHWC(__half, float);
+#undef KFAC_NHWC
+}
+
+void im2col_nchw(int dtype, const void* x, int64_t B, int64_t C, int64_t H,
+                 int64_t W, int64_t sB, int64_t sC, int64_t sH, int64_t sW,
+                 int kh, int kw, int sh, int sw, int ph, int pw, int64_t OH,
+                 int64_t OW, void* out, int64_t ldo, int out_dtype,
+                 hipStream_t s) {
+  const int64_t total = B * OH * OW * C * kh * kw;
+  if (total == 0) return;
+#define KFAC_NCHW(TI, TO)                                                     \
+  im2col_nchw_kernel<TI, TO><<<grid_for(total), 256, 0, s>>>(                 \
+      (const TI*)x, C, H, W, sB, sC, sH, sW, kh, kw, sh, sw, ph, pw, OH, OW,  \
+      (TO*)out, ldo, total)
+  if (dtype == kBF16 && out_dtype == kBF16) KFAC_NCHW(bf16_t, bf16_t);
+  else if (dtype == kF32 && out_dtype == kF32) KFAC_NCHW(float, float);
+  else if (dtype == kF32 && out_dtype == kBF16) KFAC_NCHW(float, bf16_t);
+  else if (dtype == kBF16 && out_dtype == kF32) KFAC_NCHW(bf16_t, float);
+  else if (dtype == kF16 && out_dtype == kBF16) KFAC_NCHW(__half, bf16_t);
+  else if (dtype == kF16 && out_dtype == kF32) KFAC_NCHW(__half, float);
+#undef KFAC_NCHW
+}
+
+}  // namespace kfac

@@ -1,0 +1,239 @@
+"""Eigendecomposition K-FAC layer (reference ``kfac/layers/eigen.py:19-384``).
+
+Preconditioning with the eigenbases QA, QG of the factors:
+
+    V1 = QG^T [Wg | bg] QA
+    V2 = V1 * dgda            (prediv: dgda = 1 / (dG (x) dA + damping))
+       | V1 / (dG (x) dA + damping)
+    P  = QG V2 QA^T
+
+MI355X implementation: ``[Wg | bg] QA`` is formed as ``Wg QA[:-1] + bg (x)
+QA[-1]`` (a GEMM on a row-slice of QA plus a rank-1 update) so the
+concatenated gradient is never materialised; the four GEMMs run on hipBLASLt
+into persistent fp32 buffers (``torch.mm(out=)``); the eigenvalue scaling is
+a native in-place kernel.  Eigendecompositions are normally computed in
+batches across layers by the preconditioner (``ops.linalg.eigh_many``) and
+installed with ``set_a_eig`` / ``set_g_eig``; ``compute_a_inv`` /
+``compute_g_inv`` remain for single-layer use.
+"""
+from __future__ import annotations
+
+from typing import Any
+
+import torch
+import torch.distributed as dist
+
+from distributed_kfac_pytorch_amd.layers.base import _nbytes
+from distributed_kfac_pytorch_amd.layers.base import _resolve
+from distributed_kfac_pytorch_amd.layers.base import KFACBaseLayer
+from distributed_kfac_pytorch_amd.ops import linalg
+from distributed_kfac_pytorch_amd.ops import precondition as pops
+from distributed_kfac_pytorch_amd.parallel.comm import FutureType
+from distributed_kfac_pytorch_amd.parallel.comm import get_rank
+
+
+class KFACEigenLayer(KFACBaseLayer):
+    """K-FAC layer preconditioning through factor eigendecompositions."""
+
+    def __init__(self, module: Any, *, prediv_eigenvalues: bool = False, **kwargs: Any) -> None:
+        """Init KFACEigenLayer.
+
+        Args:
+            module (ModuleHelper): module helper.
+            prediv_eigenvalues (bool): precompute ``1/(dG (x) dA + damping)``
+                on the eigendecomposition worker (needs A and G colocated).
+            **kwargs: ``KFACBaseLayer`` arguments.
+        """
+        super().__init__(module, **kwargs)
+        self.prediv_eigenvalues = prediv_eigenvalues
+        self._qa: torch.Tensor | FutureType | None = None
+        self._qg: torch.Tensor | FutureType | None = None
+        self._da: torch.Tensor | FutureType | None = None
+        self._dg: torch.Tensor | FutureType | None = None
+        self._dgda: torch.Tensor | FutureType | None = None
+        self._tmp1: torch.Tensor | None = None
+        self._tmp2: torch.Tensor | None = None
+
+    # ------------------------------------------------------------ properties
+    @property
+    def qa(self) -> torch.Tensor | None:
+        self._qa = _resolve(self._qa)
+        return self._qa
+
+    @qa.setter
+    def qa(self, v: torch.Tensor | FutureType | None) -> None:
+        self._qa = v
+
+    @property
+    def qg(self) -> torch.Tensor | None:
+        self._qg = _resolve(self._qg)
+        return self._qg
+
+    @qg.setter
+    def qg(self, v: torch.Tensor | FutureType | None) -> None:
+        self._qg = v
+
+    @property
+    def da(self) -> torch.Tensor | None:
+        self._da = _resolve(self._da)
+        return self._da
+
+    @da.setter
+    def da(self, v: torch.Tensor | FutureType | None) -> None:
+        self._da = v
+
+    @property
+    def dg(self) -> torch.Tensor | None:
+        self._dg = _resolve(self._dg)
+        return self._dg
+
+    @dg.setter
+    def dg(self, v: torch.Tensor | FutureType | None) -> None:
+        self._dg = v
+
+    @property
+    def dgda(self) -> torch.Tensor | None:
+        self._dgda = _resolve(self._dgda)
+        return self._dgda
+
+    @dgda.setter
+    def dgda(self, v: torch.Tensor | FutureType | None) -> None:
+        self._dgda = v
+
+    def memory_usage(self) -> dict[str, int]:
+        sizes = super().memory_usage()
+        sizes['a_inverses'] = _nbytes(self.qa) + _nbytes(self.da)
+        sizes['g_inverses'] = (
+            _nbytes(self.qg) + _nbytes(self.dg) + _nbytes(self.dgda)
+        )
+        return sizes
+
+    # ------------------------------------------------------------ broadcasts
+    def broadcast_a_inv(self, src: int, group: dist.ProcessGroup | None = None) -> None:
+        """Broadcast QA (and dA unless prediv) from the A inverse worker."""
+        if self.qa is None or (not self.prediv_eigenvalues and self.da is None):
+            if get_rank() == src:
+                raise RuntimeError(
+                    f'Attempt to broadcast A inv from src={src} but this rank '
+                    'has not computed A inv yet.',
+                )
+            d = self.module.a_factor_shape[0]
+            dev = self.module.device
+            self.qa = torch.empty(d, d, device=dev, dtype=self.inv_dtype)
+            self.da = torch.empty(d, device=dev, dtype=self.inv_dtype)
+        self.qa = self.tdc.broadcast(self.qa, src=src, group=group)
+        if not self.prediv_eigenvalues:
+            assert self.da is not None
+            self.da = self.tdc.broadcast(self.da, src=src, group=group)
+
+    def broadcast_g_inv(self, src: int, group: dist.ProcessGroup | None = None) -> None:
+        """Broadcast QG and dG (or dGdA with prediv) from the G worker."""
+        if (
+            self.qg is None
+            or (not self.prediv_eigenvalues and self.dg is None)
+            or (self.prediv_eigenvalues and self.dgda is None)
+        ):
+            if get_rank() == src:
+                raise RuntimeError(
+                    f'Attempt to broadcast G inv from src={src} but this rank '
+                    'has not computed G inv yet.',
+                )
+            g = self.module.g_factor_shape[0]
+            a = self.module.a_factor_shape[0]
+            dev = self.module.device
+            self.qg = torch.empty(g, g, device=dev, dtype=self.inv_dtype)
+            if not self.prediv_eigenvalues:
+                self.dg = torch.empty(g, device=dev, dtype=self.inv_dtype)
+            else:
+                self.dgda = torch.empty(g, a, device=dev, dtype=self.inv_dtype)
+        self.qg = self.tdc.broadcast(self.qg, src=src, group=group)
+        if not self.prediv_eigenvalues:
+            assert self.dg is not None
+            self.dg = self.tdc.broadcast(self.dg, src=src, group=group)
+        else:
+            assert self.dgda is not None
+            self.dgda = self.tdc.broadcast(self.dgda, src=src, group=group)
+
+    # ---------------------------------------------------------- decomposition
+    def _eig(self, factor: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+        if self.symmetric_factors:
+            return linalg.eigh(factor.to(torch.float32))
+        d, q = torch.linalg.eig(factor.to(torch.float32))
+        return d.real, q.real
+
+    def set_a_eig(self, d: torch.Tensor, q: torch.Tensor) -> None:
+        """Install an eigendecomposition of A (eigenvalues clamped at 0)."""
+        self.qa = q.to(self.inv_dtype)
+        self.da = torch.clamp(d.to(self.inv_dtype), min=0.0)
+
+    def set_g_eig(self, d: torch.Tensor, q: torch.Tensor, damping: float) -> None:
+        """Install an eigendecomposition of G (and dGdA with prediv)."""
+        self.qg = q.to(self.inv_dtype)
+        self.dg = torch.clamp(d.to(self.inv_dtype), min=0.0)
+        if self.prediv_eigenvalues:
+            assert self.da is not None and self.dg is not None
+            self.dgda = 1.0 / (torch.outer(self.dg, self.da) + damping)
+            self.dg = None
+            self.da = None
+
+    def compute_a_inv(self, damping: float = 0.001) -> None:
+        """Eigendecompose A (rank must be the A inverse worker)."""
+        if not isinstance(self.a_factor, torch.Tensor):
+            raise RuntimeError('Cannot eigendecompose A before A has been computed')
+        self.set_a_eig(*self._eig(self.a_factor))
+
+    def compute_g_inv(self, damping: float = 0.001) -> None:
+        """Eigendecompose G (and form dGdA if prediv)."""
+        if not isinstance(self.g_factor, torch.Tensor):
+            raise RuntimeError('Cannot eigendecompose G before G has been computed')
+        if self.prediv_eigenvalues and self.da is None:
+            raise RuntimeError('prediv_eigenvalues needs A eigenvalues first')
+        self.set_g_eig(*self._eig(self.g_factor), damping=damping)
+
+    # ----------------------------------------------------------- precondition
+    def _buf(self, name: str, shape: tuple[int, int], dtype: torch.dtype, device: torch.device) -> torch.Tensor:
+        t = getattr(self, name)
+        if t is None or tuple(t.shape) != shape or t.dtype != dtype or t.device != device:
+            t = torch.empty(shape, dtype=dtype, device=device)
+            setattr(self, name, t)
+        return t
+
+    def preconditioned_grad(self, damping: float = 0.001) -> None:
+        """Compute P = QG ((QG^T G QA) . S) QA^T into the grad buffer."""
+        qa, qg = self.qa, self.qg
+        if (
+            qa is None
+            or qg is None
+            or (not self.prediv_eigenvalues and self.da is None)
+            or (not self.prediv_eigenvalues and self.dg is None)
+            or (self.prediv_eigenvalues and self.dgda is None)
+        ):
+            raise RuntimeError(
+                'Eigendecompositions for both A and G have not been computed',
+            )
+        wg = self.module.weight_grad_matrix()
+        bias = self.module.has_bias()
+        dt = qa.dtype
+        g_rows, a_cols = qg.shape[0], qa.shape[0]
+        dev = qa.device
+        t1 = self._buf('_tmp1', (g_rows, a_cols), dt, dev)
+        t2 = self._buf('_tmp2', (g_rows, a_cols), dt, dev)
+        # t1 = [Wg | bg] QA  (no concatenation)
+        if bias:
+            torch.mm(wg.to(dt), qa[:-1], out=t1)
+            bg = self.module.get_bias_grad().reshape(-1).to(dt)
+            t1.addr_(bg, qa[-1])
+        else:
+            torch.mm(wg.to(dt), qa, out=t1)
+        torch.mm(qg.t(), t1, out=t2)  # V1
+        if self.prediv_eigenvalues:
+            pops.eigen_scale_(t2, dgda=self.dgda)
+        else:
+            pops.eigen_scale_(t2, dg=self.dg, da=self.da, damping=damping)
+        torch.mm(qg, t2, out=t1)
+        if dt == torch.float32:
+            out = self._grad_buffer(dev)
+            torch.mm(t1, qa.t(), out=out)
+        else:
+            out = (t1 @ qa.t()).to(torch.float32)
+        self.grad = out
