@@ -1,0 +1,227 @@
+"""Headline benchmark: ResNet-50 ImageNet-shaped training with distributed
+K-FAC (KAISA, grad_worker_fraction=0.5) on MI355X.
+
+Config (BASELINE.md / reference ``examples/torch_imagenet_resnet.py``):
+per-GPU batch 32 at 224x224, SGD momentum 0.9, label smoothing 0.1,
+K-FAC factor update every 10 steps, second-order update every 100 steps,
+damping 0.001, factor decay 0.95, KL clip 0.001, hybrid-opt (gwf 0.5),
+25 MB factor all-reduce buckets, eigen method with eigenvalue outer product.
+Data is synthetic (random images / labels of that shape, generated on the
+device), weights random-init.  bf16 autocast, channels_last.
+
+Single GPU:     python bench.py
+N GPUs:         python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+                    --master-addr 127.0.0.1 --master-port P bench.py --gpus N
+
+Prints ONE JSON line on rank 0.  ``value`` is whole-job images/s over the
+K timed steps (max step time over ranks).  With ``--baseline`` (default on)
+the same model is then timed without K-FAC and ``kfac_overhead_ms`` =
+ms/step(K-FAC) - ms/step(SGD) is reported alongside.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+import distributed_kfac_pytorch_amd as kfac  # noqa: E402
+from distributed_kfac_pytorch_amd import tracing  # noqa: E402
+from distributed_kfac_pytorch_amd.models.resnet import get_model  # noqa: E402
+
+BASELINE_IMG_S = None  # no published reference number
+
+
+def parse_args() -> argparse.Namespace:
+    p = argparse.ArgumentParser(description=__doc__)
+    p.add_argument('--gpus', type=int, default=1)
+    p.add_argument('--steps', type=int, default=100)
+    p.add_argument('--warmup', type=int, default=10)
+    p.add_argument('--model', default='resnet50')
+    p.add_argument('--batch-size', type=int, default=32, help='per GPU')
+    p.add_argument('--image-size', type=int, default=224)
+    p.add_argument('--kfac-factor-update-steps', type=int, default=10)
+    p.add_argument('--kfac-inv-update-steps', type=int, default=100)
+    p.add_argument('--kfac-damping', type=float, default=0.001)
+    p.add_argument('--kfac-factor-decay', type=float, default=0.95)
+    p.add_argument('--kfac-kl-clip', type=float, default=0.001)
+    p.add_argument('--kfac-grad-worker-fraction', type=float, default=0.5)
+    p.add_argument('--kfac-inv-method', action='store_true',
+                   help='use the damped-inverse method instead of eigen')
+    p.add_argument('--no-kfac', action='store_true')
+    p.add_argument('--baseline', type=int, default=1,
+                   help='also time plain SGD and report the K-FAC overhead')
+    p.add_argument('--no-channels-last', action='store_true')
+    p.add_argument('--fp32', action='store_true', help='disable bf16 autocast')
+    p.add_argument('--phase-timing', action='store_true')
+    p.add_argument('--lr', type=float, default=0.0125)
+    return p.parse_args()
+
+
+def setup() -> tuple[int, int, torch.device]:
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
+    if world > 1:
+        dist.init_process_group('nccl', device_id=dev)
+    return rank, world, dev
+
+
+def barrier_sync(world: int) -> None:
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def run(args: argparse.Namespace, use_kfac: bool, rank: int, world: int,
+        dev: torch.device) -> dict:
+    torch.manual_seed(1234 + rank)
+    model = get_model(args.model).to(dev)
+    cl = not args.no_channels_last
+    if cl:
+        model = model.to(memory_format=torch.channels_last)
+    if world > 1:
+        model = torch.nn.parallel.DistributedDataParallel(
+            model, device_ids=[dev.index], gradient_as_bucket_view=True,
+        )
+    lr = args.lr * world
+    opt = torch.optim.SGD(model.parameters(), lr=lr, momentum=0.9,
+                          weight_decay=5e-5)
+    precond = None
+    if use_kfac:
+        precond = kfac.KFACPreconditioner(
+            model,
+            factor_update_steps=args.kfac_factor_update_steps,
+            inv_update_steps=args.kfac_inv_update_steps,
+            damping=args.kfac_damping,
+            factor_decay=args.kfac_factor_decay,
+            kl_clip=args.kfac_kl_clip,
+            lr=lambda step: opt.param_groups[0]['lr'],
+            accumulation_steps=1,
+            allreduce_bucket_cap_mb=25,
+            colocate_factors=True,
+            compute_method='inverse' if args.kfac_inv_method else 'eigen',
+            grad_worker_fraction=args.kfac_grad_worker_fraction,
+        )
+    x = torch.randn(args.batch_size, 3, args.image_size, args.image_size,
+                    device=dev)
+    if cl:
+        x = x.contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 1000, (args.batch_size,), device=dev)
+    crit = torch.nn.CrossEntropyLoss(label_smoothing=0.1)
+    amp = not args.fp32
+
+    def step() -> None:
+        opt.zero_grad(set_to_none=False)
+        with torch.autocast('cuda', dtype=torch.bfloat16, enabled=amp):
+            loss = crit(model(x), y)
+        loss.backward()
+        if precond is not None:
+            precond.step()
+        opt.step()
+
+    for _ in range(args.warmup):
+        step()
+    timer = None
+    if args.phase_timing and precond is not None:
+        timer = tracing.enable_phase_timing(True)
+    barrier_sync(world)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier_sync(world)
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    out = {'seconds': elapsed, 'ms_per_step': elapsed / args.steps * 1e3}
+    if timer is not None:
+        out['phase_ms_per_step'] = {
+            k: v / args.steps for k, v in timer.summary().items()
+        }
+        out['phase_counts'] = timer.counts()
+        tracing.enable_phase_timing(False)
+    if precond is not None:
+        out['kfac_layers'] = len(precond._layers)
+        out['kfac_steps_end'] = precond.steps
+        mem = precond.memory_usage()
+        out['kfac_memory_mb'] = round(mem['total'] / 1e6, 1)
+    del model, opt, precond
+    torch.cuda.empty_cache()
+    return out
+
+
+def main() -> None:
+    args = parse_args()
+    rank, world, dev = setup()
+    if world != args.gpus and rank == 0:
+        print(f'[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}',
+              file=sys.stderr)
+    res = run(args, not args.no_kfac, rank, world, dev)
+    base = None
+    if args.baseline and not args.no_kfac:
+        base = run(args, False, rank, world, dev)
+    gb = args.batch_size * world
+    value = gb * args.steps / res['seconds']
+    line = {
+        'metric': 'images/sec (whole node), ResNet-50 ImageNet K-FAC training',
+        'value': round(value, 2),
+        'unit': 'images/s',
+        'n_gpus': world,
+        'steps': args.steps,
+        'warmup': args.warmup,
+        'ms_per_step': round(res['ms_per_step'], 3),
+        'higher_is_better': True,
+        'scaling': 'weak',
+        'vs_baseline': (round(value / BASELINE_IMG_S, 4)
+                        if BASELINE_IMG_S else None),
+        'dtype': 'fp32' if args.fp32 else 'bf16',
+        'data': 'synthetic (random 224x224 images / labels, random-init '
+                'weights)',
+        'config': {
+            'model': args.model,
+            'global_batch': gb,
+            'per_gpu_batch': args.batch_size,
+            'seq_len': None,
+            'image_size': args.image_size,
+            'parallelism': f'dp{world}',
+            'kfac': None if args.no_kfac else {
+                'method': 'inverse' if args.kfac_inv_method else 'eigen',
+                'factor_update_steps': args.kfac_factor_update_steps,
+                'inv_update_steps': args.kfac_inv_update_steps,
+                'grad_worker_fraction': args.kfac_grad_worker_fraction,
+                'damping': args.kfac_damping,
+                'kl_clip': args.kfac_kl_clip,
+            },
+            'channels_last': not args.no_channels_last,
+        },
+    }
+    if base is not None:
+        line['sgd_ms_per_step'] = round(base['ms_per_step'], 3)
+        line['sgd_images_per_sec'] = round(gb * args.steps / base['seconds'], 2)
+        line['kfac_overhead_ms'] = round(
+            res['ms_per_step'] - base['ms_per_step'], 3,
+        )
+    for k in ('phase_ms_per_step', 'phase_counts', 'kfac_layers',
+              'kfac_memory_mb', 'kfac_steps_end'):
+        if k in res:
+            line[k] = res[k]
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -3,8 +3,8 @@
 // includes torch; it validates tensors, picks the current HIP stream and
 // calls the raw launchers in the *.hip files.
 #include <torch/extension.h>
-#include <c10/hip/HIPStream.h>
-#include <c10/hip/HIPGuard.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 
 #include <hip/hip_runtime.h>
 #include <vector>
@@ -59,7 +59,7 @@ void jacobi_eigh_batched(const float* A, int64_t n, int64_t batch,
 namespace {
 
 hipStream_t cur_stream() {
-  return c10::hip::getCurrentHIPStream().stream();
+  return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
 }
 
 int dtype_tag(const at::Tensor& t) {
@@ -87,7 +87,7 @@ void triu_pack(const at::Tensor& src, at::Tensor& dst) {
   TORCH_CHECK(dst.is_contiguous() && dst.scalar_type() == src.scalar_type());
   const int64_t n = src.size(0);
   TORCH_CHECK(dst.numel() == n * (n + 1) / 2, "dst size");
-  c10::hip::HIPGuard g(src.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(src.device());
   kfac::triu_pack(dtype_tag(src), src.data_ptr(), src.stride(0), n,
                   dst.data_ptr(), cur_stream());
 }
@@ -101,7 +101,7 @@ void triu_unpack(at::Tensor& dst, const at::Tensor& packed, double scale) {
               packed.scalar_type() == dst.scalar_type());
   const int64_t n = dst.size(0);
   TORCH_CHECK(packed.numel() == n * (n + 1) / 2, "packed size");
-  c10::hip::HIPGuard g(dst.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(dst.device());
   kfac::triu_unpack(dtype_tag(dst), packed.data_ptr(), n, dst.data_ptr(),
                     dst.stride(0), (float)scale, cur_stream());
 }
@@ -112,7 +112,7 @@ void scale_copy(at::Tensor& dst, const at::Tensor& src, double scale) {
   TORCH_CHECK(dst.is_contiguous() && src.is_contiguous());
   TORCH_CHECK(dst.numel() == src.numel());
   TORCH_CHECK(dst.scalar_type() == src.scalar_type());
-  c10::hip::HIPGuard g(dst.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(dst.device());
   kfac::scale_copy(dtype_tag(dst), src.data_ptr(), dst.data_ptr(),
                    dst.numel(), (float)scale, cur_stream());
 }
@@ -134,7 +134,7 @@ void syrk(const at::Tensor& x, at::Tensor& C, bool bias, double alpha,
   const int64_t D = K + (bias ? 1 : 0);
   TORCH_CHECK(C.size(0) == D, "C must be [K+bias, K+bias]");
   const int64_t ldx = N > 1 ? x.stride(0) : K;
-  c10::hip::HIPGuard g(x.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   int sp = splits > 0 ? (int)splits : (int)kfac::syrk_workspace_splits(N, D);
   kfac::syrk(dtype_tag(x), x.data_ptr(), N, K, ldx, bias,
              C.data_ptr<float>(), D, C.stride(0), (float)alpha, (float)beta,
@@ -157,7 +157,7 @@ void im2col(const at::Tensor& x, at::Tensor& out, int64_t kh, int64_t kw,
   const int64_t OW = (W + 2 * pw - kw) / sw + 1;
   TORCH_CHECK(out.size(0) == B * OH * OW, "out rows");
   TORCH_CHECK(out.size(1) >= C * kh * kw, "out cols");
-  c10::hip::HIPGuard g(x.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   if (natural) {
     TORCH_CHECK(x.stride(1) == 1, "natural im2col needs channels_last input");
     kfac::im2col_nhwc(dtype_tag(x), x.data_ptr(), B, H, W, C, x.stride(0),
@@ -180,7 +180,7 @@ void eigen_scale(at::Tensor& v, const c10::optional<at::Tensor>& dgda,
   check_cuda(v, "v");
   TORCH_CHECK(v.scalar_type() == at::kFloat && v.dim() == 2 &&
               v.stride(1) == 1);
-  c10::hip::HIPGuard g(v.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(v.device());
   if (dgda.has_value()) {
     TORCH_CHECK(dgda->is_contiguous() && dgda->sizes() == v.sizes() &&
                 dgda->scalar_type() == at::kFloat);
@@ -208,7 +208,7 @@ void kl_dot(const at::Tensor& p, const at::Tensor& wgrad,
   const int64_t wcols = p.size(1) - (bgrad.has_value() ? 1 : 0);
   TORCH_CHECK(wgrad.numel() == rows * wcols, "weight grad size");
   TORCH_CHECK(wgrad.is_contiguous(), "weight grad must be contiguous");
-  c10::hip::HIPGuard g(p.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(p.device());
   const void* bptr = nullptr;
   int bdt = kfac::kF32;
   if (bgrad.has_value()) {
@@ -225,7 +225,7 @@ void kl_finalize(const at::Tensor& acc, at::Tensor& scale, double kl_clip,
                  double lr) {
   TORCH_CHECK(acc.scalar_type() == at::kDouble);
   TORCH_CHECK(scale.scalar_type() == at::kFloat);
-  c10::hip::HIPGuard g(acc.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(acc.device());
   kfac::kl_scale_finalize(acc.data_ptr<double>(), scale.data_ptr<float>(),
                           (float)kl_clip, (float)lr, cur_stream());
 }
@@ -241,7 +241,7 @@ void apply_grad(const at::Tensor& p, at::Tensor& wgrad,
   const int64_t rows = p.size(0);
   const int64_t wcols = p.size(1) - (bgrad.has_value() ? 1 : 0);
   TORCH_CHECK(wgrad.numel() == rows * wcols && wgrad.is_contiguous());
-  c10::hip::HIPGuard g(p.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(p.device());
   void* bptr = nullptr;
   int bdt = kfac::kF32;
   if (bgrad.has_value()) {
@@ -263,7 +263,7 @@ void fill_identity(at::Tensor& C) {
   check_cuda(C, "C");
   TORCH_CHECK(C.scalar_type() == at::kFloat && C.dim() == 2 &&
               C.size(0) == C.size(1) && C.stride(1) == 1);
-  c10::hip::HIPGuard g(C.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(C.device());
   kfac::fill_identity_lerp(C.data_ptr<float>(), C.size(0), C.stride(0),
                            cur_stream());
 }
@@ -281,7 +281,7 @@ std::vector<at::Tensor> jacobi_eigh(const at::Tensor& A, int64_t max_sweeps,
               kfac::jacobi_max_n());
   auto evals = at::empty({batch, n}, A.options());
   auto evecs = at::empty({batch, n, n}, A.options());
-  c10::hip::HIPGuard g(A.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(A.device());
   if (batch > 0 && n > 0) {
     kfac::jacobi_eigh_batched(A.data_ptr<float>(), n, batch, n * n,
                               evals.data_ptr<float>(),

@@ -130,6 +130,21 @@ Future = (AsyncTensor,)
 FutureType = Union[AsyncTensor]
 
 
+def _result_buffer(
+    tensor: torch.Tensor,
+    wire: torch.Tensor,
+    symmetric: bool,
+) -> torch.Tensor:
+    """Where a collective's result lands: the caller's tensor when it is
+    contiguous (in place), else the contiguous wire buffer, or a fresh
+    dense matrix for a triangle-packed wire."""
+    if tensor.is_contiguous():
+        return tensor
+    if symmetric:
+        return torch.empty_like(tensor, memory_format=torch.contiguous_format)
+    return wire
+
+
 def _scale_for(average: bool, group: dist.ProcessGroup | None) -> float:
     return 1.0 / get_world_size(group) if average else 1.0
 
@@ -272,7 +287,7 @@ class TorchDistributedCommunicator:
         else:
             wire = tensor.contiguous()
         work = dist.all_reduce(wire, group=group, async_op=True)
-        target = tensor if tensor.is_contiguous() else wire
+        target = _result_buffer(tensor, wire, symmetric)
 
         def _finish() -> torch.Tensor:
             if symmetric:
@@ -300,7 +315,7 @@ class TorchDistributedCommunicator:
         else:
             wire = tensor if tensor.is_contiguous() else tensor.contiguous()
         work = dist.broadcast(wire, src=src, group=group, async_op=True)
-        target = tensor if tensor.is_contiguous() else wire
+        target = _result_buffer(tensor, wire, symmetric)
 
         def _finish() -> torch.Tensor:
             if symmetric:

@@ -1,0 +1,98 @@
+"""End-to-end: the native GPU path reproduces the CPU reference math."""
+from __future__ import annotations
+
+import copy
+
+import pytest
+import torch
+
+import distributed_kfac_pytorch_amd as kfac
+
+pytestmark = pytest.mark.gpu
+
+
+def _net() -> torch.nn.Module:
+    torch.manual_seed(0)
+    return torch.nn.Sequential(
+        torch.nn.Conv2d(3, 16, 3, padding=1, stride=2),
+        torch.nn.ReLU(),
+        torch.nn.Conv2d(16, 16, 3, bias=False),
+        torch.nn.ReLU(),
+        torch.nn.Conv2d(16, 32, 1),
+        torch.nn.Flatten(),
+        torch.nn.Linear(32 * 5 * 5, 10),
+    )
+
+
+@pytest.mark.parametrize('method', ['eigen', 'inverse'])
+@pytest.mark.parametrize('channels_last', [False, True])
+@pytest.mark.parametrize('prediv', [True, False])
+def test_gpu_matches_cpu(cuda, method, channels_last, prediv):
+    cpu = _net()
+    gpu = copy.deepcopy(cpu).to(cuda)
+    if channels_last:
+        gpu = gpu.to(memory_format=torch.channels_last)
+    kw = dict(
+        factor_update_steps=1,
+        inv_update_steps=2,
+        compute_method=method,
+        compute_eigenvalue_outer_product=prediv,
+        lr=0.1,
+        kl_clip=0.001,
+    )
+    pc = kfac.KFACPreconditioner(cpu, **kw)
+    pg = kfac.KFACPreconditioner(gpu, **kw)
+    oc = torch.optim.SGD(cpu.parameters(), lr=0.1)
+    og = torch.optim.SGD(gpu.parameters(), lr=0.1)
+    torch.manual_seed(1)
+    for _ in range(4):
+        x = torch.randn(8, 3, 14, 14)
+        y = torch.randint(0, 10, (8,))
+        xg = x.to(cuda)
+        if channels_last:
+            xg = xg.contiguous(memory_format=torch.channels_last)
+        oc.zero_grad()
+        torch.nn.functional.cross_entropy(cpu(x), y).backward()
+        pc.step()
+        og.zero_grad()
+        torch.nn.functional.cross_entropy(gpu(xg), y.to(cuda)).backward()
+        pg.step()
+        for a, b in zip(cpu.parameters(), gpu.parameters()):
+            err = (a.grad - b.grad.cpu()).abs().max().item()
+            assert err <= 2e-3 * a.grad.abs().max().item() + 1e-7
+        oc.step()
+        og.step()
+    # checkpoints are interchangeable (reference order on both)
+    sc, sg = pc.state_dict(), pg.state_dict()
+    for name in sc['layers']:
+        for f in 'AG':
+            a = sc['layers'][name][f]
+            b = sg['layers'][name][f].cpu()
+            assert (a - b).abs().max().item() <= 1e-3 * a.abs().max().item()
+
+
+def test_bf16_autocast_resnet_smoke(cuda):
+    from distributed_kfac_pytorch_amd.models.resnet import resnet18
+
+    model = resnet18(num_classes=10).to(cuda).to(memory_format=torch.channels_last)
+    opt = torch.optim.SGD(model.parameters(), lr=0.01, momentum=0.9)
+    pre = kfac.KFACPreconditioner(
+        model,
+        factor_update_steps=1,
+        inv_update_steps=2,
+        grad_worker_fraction=0.5,
+    )
+    x = torch.randn(4, 3, 64, 64, device=cuda).contiguous(
+        memory_format=torch.channels_last,
+    )
+    y = torch.randint(0, 10, (4,), device=cuda)
+    for _ in range(3):
+        opt.zero_grad()
+        with torch.autocast('cuda', dtype=torch.bfloat16):
+            loss = torch.nn.functional.cross_entropy(model(x), y)
+        loss.backward()
+        pre.step()
+        opt.step()
+    assert torch.isfinite(loss).item()
+    for p in model.parameters():
+        assert torch.isfinite(p).all()

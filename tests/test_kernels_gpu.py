@@ -1,0 +1,163 @@
+"""Numerics of the gfx950 HIP kernels against plain PyTorch fp32/fp64 math."""
+from __future__ import annotations
+
+import pytest
+import torch
+
+from distributed_kfac_pytorch_amd.ops import _native
+from distributed_kfac_pytorch_amd.ops import comm_pack
+from distributed_kfac_pytorch_amd.ops import factors
+from distributed_kfac_pytorch_amd.ops import linalg
+from distributed_kfac_pytorch_amd.ops import precondition as pops
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref_cov(x: torch.Tensor, bias: bool) -> torch.Tensor:
+    x = x.double()
+    if bias:
+        x = torch.cat([x, torch.ones(x.shape[0], 1, dtype=x.dtype, device=x.device)], 1)
+    return x.t() @ x
+
+
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize(
+    'n,k,bias',
+    [
+        (64, 10, False),
+        (1000, 147, True),
+        (4096, 256, False),
+        (300, 129, True),
+        (37, 520, False),
+        (20000, 64, True),
+        (512, 1152, False),
+    ],
+)
+def test_syrk_matches_reference(cuda, dtype, n, k, bias):
+    torch.manual_seed(0)
+    x = torch.randn(n, k, device=cuda).to(dtype)
+    d = k + int(bias)
+    c0 = torch.randn(d, d, device=cuda)
+    c0 = c0 + c0.t()
+    for alpha, beta in ((1.0 / n, 0.0), (0.05 / n, 0.95)):
+        out = c0.clone()
+        factors.cov_accumulate_(out, x, bias=bias, alpha=alpha, beta=beta)
+        ref = beta * c0.double() + alpha * _ref_cov(x, bias)
+        err = (out.double() - ref).abs().max().item()
+        scale = ref.abs().max().item()
+        assert err <= 2e-5 * scale + 1e-6, (err, scale)
+        # exact symmetry
+        assert torch.equal(out, out.t())
+
+
+def test_syrk_strided_rows(cuda):
+    x = torch.randn(500, 200, device=cuda, dtype=torch.bfloat16)[:, :150]
+    out = torch.empty(151, 151, device=cuda)
+    factors.cov_accumulate_(out, x, bias=True, alpha=1.0, beta=0.0)
+    ref = _ref_cov(x, True)
+    assert (out.double() - ref).abs().max().item() < 1e-3 * ref.abs().max().item()
+
+
+def test_syrk_split_k_forced(cuda):
+    lib = _native.native()
+    x = torch.randn(5000, 96, device=cuda)
+    out = torch.zeros(96, 96, device=cuda)
+    for splits in (1, 3, 17):
+        lib.syrk(x, out, False, 1.0, 0.0, splits)
+        ref = _ref_cov(x, False)
+        assert (out.double() - ref).abs().max().item() < 1e-4 * ref.abs().max().item()
+        assert torch.equal(out, out.t())
+
+
+@pytest.mark.parametrize('natural', [True, False])
+@pytest.mark.parametrize(
+    'c,h,k,s,p',
+    [(3, 17, 7, 2, 3), (16, 9, 3, 1, 1), (64, 8, 3, 2, 1), (8, 10, 1, 2, 0), (5, 6, 3, 1, 0)],
+)
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+def test_im2col(cuda, natural, c, h, k, s, p, dtype):
+    x = torch.randn(2, c, h, h + 1, device=cuda).to(dtype)
+    if natural:
+        x = x.contiguous(memory_format=torch.channels_last)
+    got, spatial = factors.conv_patches(x, (k, k), (s, s), (p, p), natural=natural)
+    ref, spatial_ref = factors.conv_patches(
+        x.cpu().float(), (k, k), (s, s), (p, p), natural=natural,
+    )
+    assert spatial == spatial_ref
+    assert torch.equal(got.float().cpu(), ref.to(dtype).float())
+
+
+@pytest.mark.parametrize('n', [1, 7, 64, 129, 300])
+@pytest.mark.parametrize('dtype', [torch.float32, torch.float64])
+def test_triu_roundtrip(cuda, n, dtype):
+    a = torch.randn(n, n, device=cuda, dtype=dtype)
+    a = a + a.t()
+    packed = comm_pack.triu_pack(a)
+    idx = torch.triu_indices(n, n, device=cuda)
+    assert torch.equal(packed, a[idx[0], idx[1]])
+    out = torch.empty_like(a)
+    comm_pack.triu_unpack_(out, packed, 0.5)
+    assert torch.allclose(out, 0.5 * a)
+
+
+@pytest.mark.parametrize('n', [2, 10, 33, 64, 100, 128])
+def test_jacobi_eigh(cuda, n):
+    torch.manual_seed(n)
+    b = 5
+    x = torch.randn(b, n, 3 * n, device=cuda)
+    a = x @ x.transpose(1, 2) / n
+    evals, evecs = _native.native().jacobi_eigh(a.contiguous(), 15, 1e-7)
+    ref = torch.linalg.eigvalsh(a.double())
+    assert (evals.double() - ref).abs().max().item() < 1e-4 * ref.abs().max().item()
+    recon = evecs @ torch.diag_embed(evals) @ evecs.transpose(1, 2)
+    assert (recon - a).abs().max().item() < 1e-4 * a.abs().max().item()
+    eye = torch.eye(n, device=cuda).expand(b, n, n)
+    assert (evecs.transpose(1, 2) @ evecs - eye).abs().max().item() < 1e-4
+    # ascending
+    assert bool((evals[:, 1:] >= evals[:, :-1]).all())
+
+
+def test_eigh_many_mixed_sizes(cuda):
+    mats = []
+    for n in (3, 64, 64, 130, 200, 17):
+        x = torch.randn(n, 2 * n, device=cuda)
+        mats.append(x @ x.t() / n)
+    res = linalg.eigh_many(mats)
+    for m, (d, q) in zip(mats, res):
+        recon = q @ torch.diag(d) @ q.t()
+        assert (recon - m).abs().max().item() < 1e-4 * m.abs().max().item()
+
+
+def test_precondition_epilogues(cuda):
+    g, a = 48, 97
+    v = torch.randn(g, a, device=cuda)
+    dgda = torch.rand(g, a, device=cuda)
+    out = v.clone()
+    pops.eigen_scale_(out, dgda=dgda)
+    assert torch.allclose(out, v * dgda)
+    dg, da = torch.rand(g, device=cuda), torch.rand(a, device=cuda)
+    out = v.clone()
+    pops.eigen_scale_(out, dg=dg, da=da, damping=0.01)
+    assert torch.allclose(out, v / (torch.outer(dg, da) + 0.01), rtol=1e-5)
+
+    p = torch.randn(g, a + 1, device=cuda)
+    w = torch.randn(g, a, device=cuda)
+    bvec = torch.randn(g, device=cuda)
+    acc = torch.zeros(1, dtype=torch.float64, device=cuda)
+    pops.kl_dot_(p, w, bvec, acc)
+    ref = (p[:, :-1].double() * w.double()).sum() + (p[:, -1].double() * bvec.double()).sum()
+    assert abs(acc.item() - ref.item()) < 1e-6 * abs(ref.item()) + 1e-6
+    scale = torch.empty(1, device=cuda)
+    pops.kl_finalize(acc, scale, 0.001, 0.1)
+    vg = ref.item() * 0.01
+    assert abs(scale.item() - min(1.0, (0.001 / abs(vg)) ** 0.5)) < 1e-6
+    assert acc.item() == 0.0
+    pops.apply_grad_(p, w, bvec, scale)
+    assert torch.allclose(w, scale * p[:, :-1])
+    assert torch.allclose(bvec, scale * p[:, -1])
+
+
+def test_identity(cuda):
+    c = torch.randn(70, 70, device=cuda)
+    factors.identity_(c)
+    assert torch.equal(c, torch.eye(70, device=cuda))
