@@ -7,6 +7,8 @@
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 
 #include <hip/hip_runtime.h>
+#include <cstring>
+#include <tuple>
 #include <vector>
 
 #include "common.h"
@@ -54,7 +56,27 @@ void jacobi_eigh_batched(const float* A, int64_t n, int64_t batch,
                          int64_t strideA, float* evals, float* evecs,
                          int64_t strideV, int max_sweeps, float tol,
                          hipStream_t s);
+// multi.hip
+struct LayerDesc {
+  const float* p;
+  void* w;
+  void* b;
+  int64_t rows, cols, ldp, wcols;
+  int64_t block_start;
+  int32_t wdt, bdt;
+};
+int64_t multi_blocks_for(int64_t rows, int64_t cols);
+void kl_dot_multi(const LayerDesc* descs, int nlayers, int64_t total_blocks,
+                  double* acc, hipStream_t s);
+void kl_finalize_dev(double* acc, const float* params, float* scale,
+                     hipStream_t s);
+void apply_multi(const LayerDesc* descs, int nlayers, int64_t total_blocks,
+                 const float* scale, hipStream_t s);
 }  // namespace kfac
+
+// solver.cpp
+std::vector<at::Tensor> rocsolver_eigh(at::Tensor A, int64_t algo,
+                                       int64_t max_sweeps, double tol);
 
 namespace {
 
@@ -291,6 +313,84 @@ std::vector<at::Tensor> jacobi_eigh(const at::Tensor& A, int64_t max_sweeps,
   return {evals, evecs};
 }
 
+// ------------------------------------------------------- multi-tensor ops
+// Build the device descriptor table for a list of layers.  Returns
+// (table [uint8 on device], total_blocks).  The caller caches the table
+// while the tensors' storages are unchanged.
+std::tuple<at::Tensor, int64_t> build_layer_table(
+    const std::vector<at::Tensor>& ps, const std::vector<at::Tensor>& ws,
+    const std::vector<c10::optional<at::Tensor>>& bs) {
+  TORCH_CHECK(ps.size() == ws.size() && ps.size() == bs.size());
+  std::vector<kfac::LayerDesc> host(ps.size());
+  int64_t blocks = 0;
+  for (size_t i = 0; i < ps.size(); ++i) {
+    const auto& p = ps[i];
+    const auto& w = ws[i];
+    check_cuda(p, "p");
+    TORCH_CHECK(p.scalar_type() == at::kFloat && p.dim() == 2 &&
+                p.stride(1) == 1);
+    TORCH_CHECK(w.is_contiguous());
+    const bool hb = bs[i].has_value();
+    const int64_t rows = p.size(0), cols = p.size(1);
+    const int64_t wcols = cols - (hb ? 1 : 0);
+    TORCH_CHECK(w.numel() == rows * wcols, "layer ", i, ": weight grad size");
+    kfac::LayerDesc d{};
+    d.p = p.data_ptr<float>();
+    d.w = w.data_ptr();
+    d.wdt = dtype_tag(w);
+    d.b = nullptr;
+    d.bdt = d.wdt;
+    if (hb) {
+      TORCH_CHECK(bs[i]->is_contiguous() && bs[i]->numel() == rows);
+      d.b = bs[i]->data_ptr();
+      d.bdt = dtype_tag(*bs[i]);
+    }
+    d.rows = rows;
+    d.cols = cols;
+    d.ldp = p.stride(0);
+    d.wcols = wcols;
+    d.block_start = blocks;
+    blocks += kfac::multi_blocks_for(rows, cols);
+    host[i] = d;
+  }
+  const int64_t nbytes = (int64_t)(host.size() * sizeof(kfac::LayerDesc));
+  at::Tensor dev_t;
+  if (!ps.empty()) {
+    auto cpu = at::empty({std::max<int64_t>(nbytes, 1)},
+                         at::TensorOptions().dtype(at::kByte).pinned_memory(true));
+    std::memcpy(cpu.data_ptr(), host.data(), nbytes);
+    dev_t = cpu.to(ps[0].device(), /*non_blocking=*/true);
+  }
+  return {dev_t, blocks};
+}
+
+void kl_dot_multi(const at::Tensor& table, int64_t nlayers,
+                  int64_t total_blocks, at::Tensor& acc) {
+  TORCH_CHECK(acc.scalar_type() == at::kDouble);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(acc.device());
+  kfac::kl_dot_multi((const kfac::LayerDesc*)table.data_ptr(), (int)nlayers,
+                     total_blocks, acc.data_ptr<double>(), cur_stream());
+}
+
+void kl_finalize_dev(at::Tensor& acc, const at::Tensor& params,
+                     at::Tensor& scale) {
+  TORCH_CHECK(acc.scalar_type() == at::kDouble &&
+              params.scalar_type() == at::kFloat &&
+              scale.scalar_type() == at::kFloat);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(acc.device());
+  kfac::kl_finalize_dev(acc.data_ptr<double>(), params.data_ptr<float>(),
+                        scale.data_ptr<float>(), cur_stream());
+}
+
+void apply_multi(const at::Tensor& table, int64_t nlayers,
+                 int64_t total_blocks, const c10::optional<at::Tensor>& scale) {
+  c10::hip::HIPGuardMasqueradingAsCUDA g(table.device());
+  kfac::apply_multi((const kfac::LayerDesc*)table.data_ptr(), (int)nlayers,
+                    total_blocks,
+                    scale.has_value() ? scale->data_ptr<float>() : nullptr,
+                    cur_stream());
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -309,5 +409,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fill_identity", &fill_identity);
   m.def("jacobi_eigh", &jacobi_eigh);
   m.def("jacobi_max_n", &kfac::jacobi_max_n);
+  m.def("build_layer_table", &build_layer_table);
+  m.def("kl_dot_multi", &kl_dot_multi);
+  m.def("kl_finalize_dev", &kl_finalize_dev);
+  m.def("apply_multi", &apply_multi);
+  m.def("rocsolver_eigh", &rocsolver_eigh, py::arg("A"), py::arg("algo") = 0,
+        py::arg("max_sweeps") = 100, py::arg("tol") = 1e-7);
   m.attr("arch") = "gfx950";
 }

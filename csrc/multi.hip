@@ -1,0 +1,148 @@
+// K-HIP-7 (multi-tensor form): the KL-clip reduction and the scaled gradient
+// write for ALL layers of a step in one launch each.
+//
+// The reference does, per layer, two `.item()` host syncs plus a cat/split/
+// contiguous chain (base_preconditioner.py:409-433, layers/base.py:406-422).
+// ResNet-50 has 54 K-FAC layers: one launch per layer per op is ~110 small
+// launches per step on the critical path.  Here a step issues three:
+//   kl_dot_multi    acc += sum_l <P_l, [Wg_l | bg_l]>      (fp64 atomics)
+//   kl_finalize_dev scale = min(1, sqrt(kl_clip / |acc * lr^2|)), acc = 0
+//   apply_multi     [Wg_l | bg_l] = scale * P_l
+// Layers are described by a device-resident descriptor table; each block
+// finds its layer by binary search over the per-layer block prefix sums.
+// kl_clip and lr are read from a small device array so the launches can be
+// captured in a HIP graph and replayed with new hyperparameters.
+#include "common.h"
+
+namespace kfac {
+
+struct LayerDesc {
+  const float* p;   // preconditioned grad [rows, cols], row stride ldp
+  void* w;          // weight grad [rows, wcols] contiguous
+  void* b;          // bias grad [rows] or null
+  int64_t rows, cols, ldp, wcols;
+  int64_t block_start;  // first block of this layer
+  int32_t wdt, bdt;     // dtype tags
+};
+
+namespace {
+
+constexpr int MT = 256;
+constexpr int EPT = 8;  // elements per thread per block
+
+__device__ __forceinline__ float load_any(const void* base, int64_t i, int dt) {
+  if (dt == kF32) return ((const float*)base)[i];
+  if (dt == kBF16) return __bfloat162float(((const bf16_t*)base)[i]);
+  return __half2float(((const __half*)base)[i]);
+}
+
+__device__ __forceinline__ void store_any(void* base, int64_t i, int dt, float v) {
+  if (dt == kF32) ((float*)base)[i] = v;
+  else if (dt == kBF16) ((bf16_t*)base)[i] = __float2bfloat16(v);
+  else ((__half*)base)[i] = __float2half(v);
+}
+
+__device__ __forceinline__ int find_layer(const LayerDesc* d, int n, int64_t blk) {
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (d[mid].block_start <= blk) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+__global__ void __launch_bounds__(MT)
+kl_dot_multi_kernel(const LayerDesc* __restrict__ descs, int nlayers,
+                    double* __restrict__ acc) {
+  __shared__ double part[MT / 64];
+  const int li = find_layer(descs, nlayers, blockIdx.x);
+  const LayerDesc d = descs[li];
+  const int64_t total = d.rows * d.cols;
+  const int64_t base = (int64_t)(blockIdx.x - d.block_start) * MT * EPT;
+  double s = 0.0;
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) {
+    const int64_t e = base + k * MT + threadIdx.x;
+    if (e < total) {
+      const int64_t i = e / d.cols, j = e - (e / d.cols) * d.cols;
+      const float pv = d.p[i * d.ldp + j];
+      const float g = j < d.wcols ? load_any(d.w, i * d.wcols + j, d.wdt)
+                                  : load_any(d.b, i, d.bdt);
+      s += (double)pv * (double)g;
+    }
+  }
+  s = wave_reduce_sum(s);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+#pragma unroll
+    for (int w = 0; w < MT / 64; ++w) t += part[w];
+    if (t != 0.0) atomicAdd(acc, t);
+  }
+}
+
+// params: [0] kl_clip, [1] lr
+__global__ void kl_finalize_dev_kernel(double* __restrict__ acc,
+                                       const float* __restrict__ params,
+                                       float* __restrict__ scale) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    const double lr = params[1];
+    const double vg = acc[0] * lr * lr;
+    double sc = 1.0;
+    if (vg != 0.0) {
+      sc = sqrt((double)params[0] / fabs(vg));
+      if (sc > 1.0) sc = 1.0;
+    }
+    scale[0] = (float)sc;
+    acc[0] = 0.0;
+  }
+}
+
+__global__ void __launch_bounds__(MT)
+apply_multi_kernel(const LayerDesc* __restrict__ descs, int nlayers,
+                   const float* __restrict__ scale) {
+  const int li = find_layer(descs, nlayers, blockIdx.x);
+  const LayerDesc d = descs[li];
+  const float sc = scale != nullptr ? scale[0] : 1.f;
+  const int64_t total = d.rows * d.cols;
+  const int64_t base = (int64_t)(blockIdx.x - d.block_start) * MT * EPT;
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) {
+    const int64_t e = base + k * MT + threadIdx.x;
+    if (e < total) {
+      const int64_t i = e / d.cols, j = e - (e / d.cols) * d.cols;
+      const float v = sc * d.p[i * d.ldp + j];
+      if (j < d.wcols) store_any(d.w, i * d.wcols + j, d.wdt, v);
+      else store_any(d.b, i, d.bdt, v);
+    }
+  }
+}
+
+}  // namespace
+
+int64_t multi_blocks_for(int64_t rows, int64_t cols) {
+  return ceil_div(rows * cols, (int64_t)MT * EPT);
+}
+
+void kl_dot_multi(const LayerDesc* descs, int nlayers, int64_t total_blocks,
+                  double* acc, hipStream_t s) {
+  if (nlayers == 0 || total_blocks == 0) return;
+  kl_dot_multi_kernel<<<dim3((unsigned)total_blocks), dim3(MT), 0, s>>>(
+      descs, nlayers, acc);
+}
+
+void kl_finalize_dev(double* acc, const float* params, float* scale,
+                     hipStream_t s) {
+  kl_finalize_dev_kernel<<<1, 64, 0, s>>>(acc, params, scale);
+}
+
+void apply_multi(const LayerDesc* descs, int nlayers, int64_t total_blocks,
+                 const float* scale, hipStream_t s) {
+  if (nlayers == 0 || total_blocks == 0) return;
+  apply_multi_kernel<<<dim3((unsigned)total_blocks), dim3(MT), 0, s>>>(
+      descs, nlayers, scale);
+}
+
+}  // namespace kfac

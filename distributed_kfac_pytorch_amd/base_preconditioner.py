@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import logging
 import math
+import os
 import warnings
 from collections import defaultdict
 from typing import Any
@@ -43,6 +44,127 @@ from distributed_kfac_pytorch_amd.parallel.comm import (
 )
 
 logger = logging.getLogger(__name__)
+
+
+class StepGraphs:
+    """HIP-graph replay of the per-step precondition + apply phases.
+
+    Between second-order updates the precondition phase is a fixed chain of
+    ~6 launches per layer (4 hipBLASLt GEMMs, a rank-1 update, the eigenvalue
+    scaling) plus the three multi-tensor KL / apply launches -- ~330 small
+    launches per ResNet-50 step, host-launch bound from Python.  All operands
+    live in persistent buffers (factors' eigenbases are installed in place,
+    P / temporaries are per-layer buffers, gradients are the parameters'
+    ``.grad``), so the chain is captured once into a HIP graph and replayed.
+
+    Capture happens on the second consecutive eligible step with the same
+    buffer addresses and hyperparameters baked into kernels (damping without
+    prediv); any change falls back to eager execution and re-captures.
+    Eligible steps: GPU, native extension present, not an inverse-update step,
+    and no gradient broadcast inside the phase (COMM-OPT / single rank).
+    KL-clip and lr values are read by the kernels from a device buffer that
+    is refreshed before each replay, so LR schedules do not force re-capture.
+    """
+
+    def __init__(self) -> None:
+        self.graph: Any = None
+        self.key: tuple | None = None
+        self.pending_key: tuple | None = None
+        self.replays = 0
+        self.captures = 0
+
+    @staticmethod
+    def _ptr(t: Any) -> int:
+        return t.data_ptr() if isinstance(t, torch.Tensor) else 0
+
+    def _key(self, pre: 'BaseKFACPreconditioner', ordered: list) -> tuple | None:
+        parts: list = []
+        for name, layer in ordered:
+            if not pre._assignment.is_grad_worker(name):
+                return None
+            if not isinstance(layer, KFACEigenLayer):
+                parts.append(('inv', self._ptr(getattr(layer, 'a_inv', None)),
+                              self._ptr(getattr(layer, 'g_inv', None))))
+            else:
+                if layer.qa is None or layer.qa.dtype != torch.float32:
+                    return None
+                parts.append((self._ptr(layer.qa), self._ptr(layer.qg),
+                              self._ptr(layer.dgda), self._ptr(layer.da),
+                              self._ptr(layer.dg), layer.prediv_eigenvalues))
+            m = layer.module
+            w = m.module.weight.grad
+            if w is None or not w.is_cuda:
+                return None
+            b = m.module.bias.grad if m.has_bias() else None
+            parts.append((w.data_ptr(), self._ptr(b),
+                          self._ptr(layer._grad_buf),
+                          self._ptr(getattr(layer, '_tmp1', None)),
+                          self._ptr(getattr(layer, '_tmp2', None))))
+        needs_damping = any(
+            isinstance(l, KFACEigenLayer) and not l.prediv_eigenvalues
+            for _, l in ordered
+        )
+        return (tuple(parts), pre.damping if needs_damping else None,
+                pre.kl_clip is None)
+
+    def run(
+        self,
+        pre: 'BaseKFACPreconditioner',
+        ordered: list,
+        inverse_step: bool,
+    ) -> bool:
+        """Execute the phases through the graph; False = caller runs eager."""
+        from distributed_kfac_pytorch_amd.ops import _native
+
+        if inverse_step or not ordered or _native.native() is None:
+            self.pending_key = None
+            return False
+        if pre._assignment.broadcast_gradients():
+            return False
+        if not ordered[0][1].module.device.type == 'cuda':
+            return False
+        key = self._key(pre, ordered)
+        if key is None:
+            return False
+        layers = [l for _, l in ordered]
+        if pre._multi_apply is None:
+            pre._multi_apply = pops.MultiLayerApply()
+        kl = pre.kl_clip
+        if key == self.key and self.graph is not None:
+            if not pre._multi_apply.prepare(layers, kl, float(pre.lr), use_buffers=True):
+                return False
+            with tracing.phase('precondition+apply(graph)'):
+                self.graph.replay()
+            self.replays += 1
+            for l in layers:
+                l.grad = None
+            return True
+        if key != self.pending_key:
+            # first sighting of this configuration: run eagerly, capture next
+            self.pending_key = key
+            return False
+        # second consecutive sighting: capture, then replay once for this step
+        if not pre._multi_apply.prepare(layers, kl, float(pre.lr), use_buffers=True):
+            return False
+        damping = pre.damping
+        g = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            with torch.cuda.graph(g, stream=side):
+                for _, l in ordered:
+                    l.preconditioned_grad(damping=damping)
+                pre._multi_apply.launch(kl is not None)
+        torch.cuda.current_stream().wait_stream(side)
+        self.graph = g
+        self.key = key
+        self.pending_key = None
+        self.captures += 1
+        with tracing.phase('precondition+apply(graph)'):
+            g.replay()
+        for l in layers:
+            l.grad = None
+        return True
 
 
 class BaseKFACPreconditioner:
@@ -125,6 +247,10 @@ class BaseKFACPreconditioner:
         self._mini_steps: dict[str, int] = defaultdict(int)
         self._kl_acc: torch.Tensor | None = None
         self._kl_scale: torch.Tensor | None = None
+        self._multi_apply: Any = None
+        self._graphs: Any = None
+        if os.environ.get('KFAC_GRAPHS', '1') != '0':
+            self._graphs = StepGraphs()
         self._hook_handles: list[Any] = []
         for module in self._layers:
             self._hook_handles.append(
@@ -332,27 +458,53 @@ class BaseKFACPreconditioner:
                             )
             self._tdc.flush_allreduce_buckets()
 
-        with tracing.phase('precondition'):
-            damping = self.damping
-            bcast = self._assignment.broadcast_gradients()
-            for name, layer in ordered:
-                if self._assignment.is_grad_worker(name):
-                    layer.preconditioned_grad(damping=damping)
-                if bcast:
-                    layer.broadcast_grad(
-                        src=self._assignment.src_grad_worker(name),
-                        group=self._assignment.grad_receiver_group(name),
-                    )
-            self._tdc.flush_allreduce_buckets()
-
-        with tracing.phase('apply'):
-            kl = self.kl_clip
-            scale = None if kl is None else self._device_grad_scale(ordered, kl)
-            for _, layer in ordered:
-                layer.update_grad(scale=scale)
+        inverse_step = self.steps % self.inv_update_steps == 0
+        if self._graphs is None or not self._graphs.run(self, ordered, inverse_step):
+            with tracing.phase('precondition'):
+                self._precondition_all(ordered)
+            with tracing.phase('apply'):
+                self._apply_gradients(ordered, self.kl_clip)
 
         self._steps += 1
         self._mini_steps = defaultdict(int)
+
+    def _precondition_all(self, ordered: list[tuple[str, KFACBaseLayer]]) -> None:
+        """Precondition this rank's layers; broadcast results if needed."""
+        damping = self.damping
+        bcast = self._assignment.broadcast_gradients()
+        for name, layer in ordered:
+            if self._assignment.is_grad_worker(name):
+                layer.preconditioned_grad(damping=damping)
+            if bcast:
+                layer.broadcast_grad(
+                    src=self._assignment.src_grad_worker(name),
+                    group=self._assignment.grad_receiver_group(name),
+                )
+        self._tdc.flush_allreduce_buckets()
+
+    def _apply_gradients(
+        self,
+        ordered: list[tuple[str, KFACBaseLayer]],
+        kl: float | None,
+    ) -> None:
+        """KL-clip scale + in-place gradient write for every layer.
+
+        GPU fast path: three multi-tensor launches for the whole model
+        (``ops.precondition.MultiLayerApply``); otherwise per layer.
+        """
+        if not ordered:
+            return
+        if self._multi_apply is None:
+            self._multi_apply = pops.MultiLayerApply()
+        if self._multi_apply.run(
+            [layer for _, layer in ordered],
+            kl,
+            float(self.lr) if kl is not None else 0.0,
+        ):
+            return
+        scale = None if kl is None else self._device_grad_scale(ordered, kl)
+        for _, layer in ordered:
+            layer.update_grad(scale=scale)
 
     def _kl_buffers(self, device: torch.device) -> tuple[torch.Tensor, torch.Tensor]:
         if self._kl_acc is None or self._kl_acc.device != device:

@@ -161,20 +161,44 @@ class KFACEigenLayer(KFACBaseLayer):
         d, q = torch.linalg.eig(factor.to(torch.float32))
         return d.real, q.real
 
+    @staticmethod
+    def _install(old: Any, new: torch.Tensor) -> torch.Tensor:
+        """Copy ``new`` into the existing buffer when possible, so the
+        second-order state keeps a fixed address across inverse updates
+        (device tables and captured HIP graphs stay valid)."""
+        if (
+            isinstance(old, torch.Tensor)
+            and old.shape == new.shape
+            and old.dtype == new.dtype
+            and old.device == new.device
+            and old.is_contiguous()
+        ):
+            old.copy_(new)
+            return old
+        return new.contiguous()
+
     def set_a_eig(self, d: torch.Tensor, q: torch.Tensor) -> None:
         """Install an eigendecomposition of A (eigenvalues clamped at 0)."""
-        self.qa = q.to(self.inv_dtype)
-        self.da = torch.clamp(d.to(self.inv_dtype), min=0.0)
+        self.qa = self._install(self.qa, q.to(self.inv_dtype))
+        self._da_store = self._install(
+            getattr(self, '_da_store', None),
+            torch.clamp(d.to(self.inv_dtype), min=0.0),
+        )
+        self.da = self._da_store
 
     def set_g_eig(self, d: torch.Tensor, q: torch.Tensor, damping: float) -> None:
         """Install an eigendecomposition of G (and dGdA with prediv)."""
-        self.qg = q.to(self.inv_dtype)
-        self.dg = torch.clamp(d.to(self.inv_dtype), min=0.0)
+        self.qg = self._install(self.qg, q.to(self.inv_dtype))
+        dg = torch.clamp(d.to(self.inv_dtype), min=0.0)
         if self.prediv_eigenvalues:
-            assert self.da is not None and self.dg is not None
-            self.dgda = 1.0 / (torch.outer(self.dg, self.da) + damping)
+            assert self.da is not None
+            dgda = torch.outer(dg, self.da).add_(damping).reciprocal_()
+            self.dgda = self._install(self.dgda, dgda)
             self.dg = None
             self.da = None
+        else:
+            self._dg_store = self._install(getattr(self, '_dg_store', None), dg)
+            self.dg = self._dg_store
 
     def compute_a_inv(self, damping: float = 0.001) -> None:
         """Eigendecompose A (rank must be the A inverse worker)."""

@@ -1,20 +1,26 @@
 """Second-order linear algebra: batched symmetric eigensolver and SPD inverse.
 
 ``eigh_many(mats)`` decomposes a list of symmetric fp32 matrices of mixed
-sizes in as few launches as possible:
+sizes (all K-FAC factors a rank owns) with as little latency as possible:
 
-* n <= ``jacobi_max_n()`` (128): one batched launch per size of the
-  LDS-resident parallel Jacobi kernel (csrc/eigh_jacobi.hip), one matrix per
-  workgroup, no host synchronisation.
-* larger n: same-size matrices are stacked and sent through
-  ``torch.linalg.eigh`` as one batched call (rocSOLVER), so the per-call
-  latency and the host sync torch does to check ``info`` are paid once per
-  size bucket instead of once per factor.
+* matrices are bucketed by size; each bucket is ONE batched call;
+* n <= 64: the LDS-resident parallel Jacobi kernel (csrc/eigh_jacobi.hip),
+  one matrix per workgroup;
+* larger n: direct batched rocSOLVER ``syevd`` calls from C++
+  (csrc/solver.cpp) which, unlike ``torch.linalg.eigh``, never synchronise
+  the host;
+* the buckets run concurrently on a small pool of HIP streams (joined back
+  into the caller's stream with events), so latency-bound small/medium
+  decompositions overlap the bandwidth-bound large ones.
 
 Results match ``torch.linalg.eigh``: ascending eigenvalues, eigenvectors in
 columns.  Eigenvectors are unique only up to sign (and rotation inside
 degenerate eigenspaces); K-FAC only uses them through ``Q f(D) Q^T``, which
 is invariant to that freedom.
+
+Environment knobs: ``KFAC_EIGH`` = auto | torch | syevd | syevj | syevdj
+(force one algorithm for n > 64), ``KFAC_EIGH_STREAMS`` (default 4),
+``KFAC_JACOBI_SWEEPS`` / ``KFAC_JACOBI_TOL`` (small-n kernel).
 """
 from __future__ import annotations
 
@@ -28,11 +34,51 @@ from distributed_kfac_pytorch_amd.ops._native import use_native
 
 JACOBI_SWEEPS = int(os.environ.get('KFAC_JACOBI_SWEEPS', '15'))
 JACOBI_TOL = float(os.environ.get('KFAC_JACOBI_TOL', '1e-7'))
+_ALGOS = {'syevd': 0, 'syevj': 1, 'syevdj': 2}
+# n above which auto picks syevd over syevj (Jacobi sweeps are O(n^3) each)
+# largest n sent to the LDS Jacobi kernel (its hard limit is jacobi_max_n())
+JACOBI_MAX_N = int(os.environ.get('KFAC_JACOBI_MAX_N', '64'))
+
+_streams: list[torch.cuda.Stream] = []
 
 
 def jacobi_max_n() -> int:
     lib = native()
     return int(lib.jacobi_max_n()) if lib is not None else 0
+
+
+def _side_streams(device: torch.device) -> list[torch.cuda.Stream]:
+    n = int(os.environ.get('KFAC_EIGH_STREAMS', '4'))
+    global _streams
+    if len(_streams) < n or _streams[0].device != device:
+        _streams = [torch.cuda.Stream(device=device) for _ in range(n)]
+    return _streams[:n]
+
+
+def _algo_for(n: int) -> str:
+    mode = os.environ.get('KFAC_EIGH', 'auto')
+    if mode != 'auto':
+        return mode
+    # Measured on MI355X (tools/bench_eigh.py): batched syevd beats syevj /
+    # syevdj at every size >= 128 and matches torch's eigh accuracy; the
+    # native Jacobi kernel wins for n <= 64.
+    return 'syevd'
+
+
+def _gpu_bucket(stack: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    n = stack.shape[-1]
+    lib = native()
+    if n <= JACOBI_MAX_N:
+        return lib.jacobi_eigh(stack.contiguous(), JACOBI_SWEEPS, JACOBI_TOL)
+    algo = _algo_for(n)
+    if algo == 'torch':
+        return torch.linalg.eigh(stack)
+    evals, evecs = lib.rocsolver_eigh(stack.contiguous(), _ALGOS[algo], 100, 1e-7)
+    return evals, evecs
+
+
+def _bucket_cost(n: int, count: int) -> float:
+    return float(count) * float(n) ** 3
 
 
 def eigh_many(
@@ -43,24 +89,49 @@ def eigh_many(
     buckets: dict[tuple[int, torch.device], list[int]] = defaultdict(list)
     for i, m in enumerate(mats):
         buckets[(m.shape[0], m.device)].append(i)
-    jmax = None
-    for (n, dev), idxs in buckets.items():
+    gpu = [(k, v) for k, v in buckets.items() if k[1].type == 'cuda']
+    cpu = [(k, v) for k, v in buckets.items() if k[1].type != 'cuda']
+    for (n, _), idxs in cpu:
         stack = torch.stack([mats[i].to(torch.float32) for i in idxs])
-        if dev.type == 'cuda' and use_native(stack):
-            if jmax is None:
-                jmax = jacobi_max_n()
-            if n <= jmax:
-                evals, evecs = native().jacobi_eigh(
-                    stack.contiguous(),
-                    JACOBI_SWEEPS,
-                    JACOBI_TOL,
-                )
-            else:
-                evals, evecs = torch.linalg.eigh(stack)
-        else:
-            evals, evecs = torch.linalg.eigh(stack)
+        evals, evecs = torch.linalg.eigh(stack)
         for k, i in enumerate(idxs):
             out[i] = (evals[k], evecs[k])
+    if gpu:
+        dev = gpu[0][0][1]
+        stacks = {
+            key: torch.stack([mats[i].to(torch.float32) for i in idxs])
+            for key, idxs in gpu
+        }
+        if not use_native(*stacks.values()):
+            for key, idxs in gpu:
+                evals, evecs = torch.linalg.eigh(stacks[key])
+                for k, i in enumerate(idxs):
+                    out[i] = (evals[k], evecs[k])
+        else:
+            main = torch.cuda.current_stream(dev)
+            ready = torch.cuda.Event()
+            ready.record(main)
+            streams = _side_streams(dev)
+            # longest buckets first, round-robin over the side streams
+            order = sorted(gpu, key=lambda kv: -_bucket_cost(kv[0][0], len(kv[1])))
+            loads = [0.0] * len(streams)
+            results = {}
+            for key, idxs in order:
+                j = loads.index(min(loads))
+                loads[j] += _bucket_cost(key[0], len(idxs))
+                s = streams[j]
+                s.wait_event(ready)
+                with torch.cuda.stream(s):
+                    results[key] = _gpu_bucket(stacks[key])
+            for s in streams:
+                main.wait_stream(s)
+            for key, idxs in gpu:
+                evals, evecs = results[key]
+                for k, i in enumerate(idxs):
+                    out[i] = (evals[k], evecs[k])
+                # tensors produced on side streams are consumed on main
+                evals.record_stream(main)
+                evecs.record_stream(main)
     return [o for o in out if o is not None]
 
 

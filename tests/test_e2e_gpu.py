@@ -96,3 +96,37 @@ def test_bf16_autocast_resnet_smoke(cuda):
     assert torch.isfinite(loss).item()
     for p in model.parameters():
         assert torch.isfinite(p).all()
+
+
+@pytest.mark.parametrize('prediv', [True, False])
+@pytest.mark.parametrize('method', ['eigen', 'inverse'])
+def test_graph_replay_matches_eager(cuda, prediv, method):
+    """HIP-graph replay of precondition+apply == eager execution."""
+    base = _net().to(cuda).to(memory_format=torch.channels_last)
+    models = [copy.deepcopy(base), copy.deepcopy(base)]
+    pres = [
+        kfac.KFACPreconditioner(
+            m,
+            factor_update_steps=1,
+            inv_update_steps=4,
+            compute_method=method,
+            compute_eigenvalue_outer_product=prediv,
+            lr=lambda s: 0.1 / (1 + s),
+        )
+        for m in models
+    ]
+    pres[1]._graphs = None  # eager reference
+    opts = [torch.optim.SGD(m.parameters(), lr=0.05) for m in models]
+    torch.manual_seed(2)
+    for _ in range(10):
+        x = torch.randn(8, 3, 14, 14, device=cuda).contiguous(memory_format=torch.channels_last)
+        y = torch.randint(0, 10, (8,), device=cuda)
+        for m, p, o in zip(models, pres, opts):
+            o.zero_grad(set_to_none=False)
+            torch.nn.functional.cross_entropy(m(x), y).backward()
+            p.step()
+        for a, b in zip(models[0].parameters(), models[1].parameters()):
+            assert torch.allclose(a.grad, b.grad, rtol=1e-4, atol=1e-6)
+        for o in opts:
+            o.step()
+    assert pres[0]._graphs.replays > 0 and pres[0]._graphs.captures >= 1

@@ -1,10 +1,10 @@
 """Time the eigensolver paths on the ResNet-50 K-FAC factor size mix.
 
-For every distinct factor dimension n (with its multiplicity in ResNet-50):
-  * torch.linalg.eigh one matrix at a time
-  * torch.linalg.eigh batched over the same-size factors
-  * the native batched Jacobi kernel (n <= 128)
-Prints one JSON line per size and a total.
+Per distinct factor dimension n (with its multiplicity in ResNet-50): batched
+torch.linalg.eigh, batched rocSOLVER syevd / syevj / syevdj through the native
+extension, and the native Jacobi kernel for n <= 128.  Then the full
+``eigh_many`` over all 108 factors (multi-stream) for comparison with the
+sequential sum.  One JSON line per measurement.
 """
 from __future__ import annotations
 
@@ -33,29 +33,51 @@ def timed(fn, reps=2):
     return (time.perf_counter() - t) / reps * 1e3
 
 
+def make(n, cnt, dev):
+    x = torch.randn(cnt, n, 2 * n, device=dev)
+    return (x @ x.transpose(1, 2)) / (2 * n) + 1e-3 * torch.eye(n, device=dev)
+
+
 def main() -> None:
     dev = torch.device('cuda')
-    tot_single = tot_batched = tot_best = 0.0
+    lib = native()
+    totals = {}
+    allmats = []
     for n, cnt in SIZES.items():
-        x = torch.randn(cnt, n, 2 * n, device=dev)
-        a = (x @ x.transpose(1, 2)) / (2 * n) + 1e-3 * torch.eye(n, device=dev)
+        a = make(n, cnt, dev)
+        allmats += [a[i] for i in range(cnt)]
         reps = 1 if n >= 2048 else 2
-        single = timed(lambda: [torch.linalg.eigh(a[i]) for i in range(cnt)], reps)
-        batched = timed(lambda: torch.linalg.eigh(a), reps)
-        row = {'n': n, 'count': cnt, 'single_ms': round(single, 2),
-               'batched_ms': round(batched, 2)}
-        best = min(single, batched)
+        row = {'n': n, 'count': cnt}
+        row['torch_batched'] = timed(lambda: torch.linalg.eigh(a), reps)
+        for name, algo in (('syevd', 0), ('syevj', 1), ('syevdj', 2)):
+            if name == 'syevj' and n > 2304:
+                continue
+            try:
+                row[name] = timed(lambda: lib.rocsolver_eigh(a.clone(), algo, 100, 1e-7), reps)
+            except Exception as e:  # noqa: BLE001
+                row[name] = str(e)[:80]
         if n <= linalg.jacobi_max_n():
-            jac = timed(lambda: native().jacobi_eigh(a.contiguous(), 15, 1e-7), reps)
-            row['jacobi_ms'] = round(jac, 2)
-            best = min(best, jac)
-        tot_single += single
-        tot_batched += batched
-        tot_best += best
+            row['jacobi'] = timed(lambda: lib.jacobi_eigh(a.contiguous(), 15, 1e-7), reps)
+        for k, v in row.items():
+            if isinstance(v, float):
+                row[k] = round(v, 2)
+                totals[k] = totals.get(k, 0.0) + v
+        # accuracy of syevj/syevd vs torch
+        d_ref = torch.linalg.eigvalsh(a.double())
+        for name, algo in (('syevd', 0), ('syevj', 1)):
+            if name in row and isinstance(row[name], float):
+                w, v = lib.rocsolver_eigh(a.clone(), algo, 100, 1e-7)
+                rec = v @ torch.diag_embed(w) @ v.transpose(1, 2)
+                row[f'{name}_recon_err'] = float((rec - a).abs().max() / a.abs().max())
+                row[f'{name}_eval_err'] = float((w.double() - d_ref).abs().max() / d_ref.abs().max())
         print(json.dumps(row), flush=True)
-    print(json.dumps({'total_single_ms': round(tot_single, 1),
-                      'total_batched_ms': round(tot_batched, 1),
-                      'total_best_ms': round(tot_best, 1)}), flush=True)
+    print(json.dumps({'sequential_totals_ms': {k: round(v, 1) for k, v in totals.items()}}), flush=True)
+    for mode in ('auto', 'syevd', 'torch'):
+        os.environ['KFAC_EIGH'] = mode
+        for streams in ('1', '4'):
+            os.environ['KFAC_EIGH_STREAMS'] = streams
+            ms = timed(lambda: linalg.eigh_many(allmats), 2)
+            print(json.dumps({'eigh_many': mode, 'streams': streams, 'ms': round(ms, 1)}), flush=True)
 
 
 if __name__ == '__main__':

@@ -1,9 +1,9 @@
 """Build the in-tree HIP extension ``distributed_kfac_pytorch_amd/_C*.so``.
 
 Drives ``hipcc --offload-arch=gfx950`` directly (no hipify, no JIT cache):
-every ``csrc/*.hip`` kernel file is compiled to an object, ``bindings.cpp``
-(the only torch-aware translation unit) is compiled against the installed
-PyTorch-ROCm headers, and everything is linked into one shared object next
+every ``csrc/*.hip`` kernel file is compiled to an object, the
+``csrc/*.cpp`` host files (bindings, rocSOLVER tier -- the only torch-aware
+translation units) are compiled against the installed PyTorch-ROCm headers, and everything is linked into one shared object next
 to the Python package so it travels with the repo snapshot to the GPU box.
 
 Usage:  python tools/build_native.py [--force] [--jobs N] [--verbose]
@@ -92,27 +92,30 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = False) -> str:
         objs.append(obj)
         if force or _newer([src] + header_deps, obj):
             jobs_list.append([hipcc, *common, '-c', src, '-o', obj])
-    bind = os.path.join(CSRC, 'bindings.cpp')
-    bind_obj = os.path.join(BUILD, 'bindings.o')
-    objs.append(bind_obj)
     py_inc = sysconfig.get_paths()['include']
-    if force or _newer([bind] + header_deps, bind_obj):
-        jobs_list.append(
-            [
-                hipcc,
-                *common,
-                '-DTORCH_EXTENSION_NAME=_C',
-                '-DTORCH_API_INCLUDE_EXTENSION_H',
-                '-Wno-unused-result',
-                '-Wno-deprecated-declarations',
-                *[f'-I{p}' for p in incs],
-                f'-I{py_inc}',
-                '-c',
-                bind,
-                '-o',
-                bind_obj,
-            ],
-        )
+    torch_srcs = sorted(
+        os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith('.cpp')
+    )
+    for src in torch_srcs:
+        obj = os.path.join(BUILD, os.path.basename(src) + '.o')
+        objs.append(obj)
+        if force or _newer([src] + header_deps, obj):
+            jobs_list.append(
+                [
+                    hipcc,
+                    *common,
+                    '-DTORCH_EXTENSION_NAME=_C',
+                    '-DTORCH_API_INCLUDE_EXTENSION_H',
+                    '-Wno-unused-result',
+                    '-Wno-deprecated-declarations',
+                    *[f'-I{p}' for p in incs],
+                    f'-I{py_inc}',
+                    '-c',
+                    src,
+                    '-o',
+                    obj,
+                ],
+            )
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         futs = [ex.submit(_run, cmd, verbose) for cmd in jobs_list]
         for f in futs:
@@ -136,6 +139,10 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = False) -> str:
             '-ltorch_hip',
             '-ltorch_python',
             '-lamdhip64',
+            '-L/opt/rocm/lib',
+            '-Wl,-rpath,/opt/rocm/lib',
+            '-lrocsolver',
+            '-lrocblas',
         ]
         _run(link, verbose)
     return out
