@@ -35,7 +35,12 @@ import distributed_kfac_pytorch_amd as kfac  # noqa: E402
 from distributed_kfac_pytorch_amd import tracing  # noqa: E402
 from distributed_kfac_pytorch_amd.models.resnet import get_model  # noqa: E402
 
-BASELINE_IMG_S = None  # no published reference number
+# The reference publishes no number.  Measured on MI355X: the
+# upstream kfac_pytorch package, same config, 1 GPU (it cannot run
+# channels_last weights, so NCHW): 728.91 img/s (profiles/
+# bench_reference_impl_mi355x_1gpu.json).  For N GPUs the comparison point is
+# the reference's linear-scaling upper bound N * 728.91.
+REFERENCE_IMG_S_PER_GPU = 728.91
 
 
 def parse_args() -> argparse.Namespace:
@@ -61,17 +66,29 @@ def parse_args() -> argparse.Namespace:
     p.add_argument('--fp32', action='store_true', help='disable bf16 autocast')
     p.add_argument('--phase-timing', action='store_true')
     p.add_argument('--lr', type=float, default=0.0125)
+    p.add_argument('--impl', default='native', choices=['native', 'reference'],
+                   help='reference = time the upstream kfac_pytorch package '
+                        'found on $KFAC_REFERENCE_PATH (same config) to '
+                        'establish the MI355X baseline')
+    p.add_argument('--backend', default='nccl',
+                   help='torch.distributed backend (nccl = RCCL)')
+    p.add_argument('--same-device', action='store_true',
+                   help='put every rank on cuda:0 (multi-rank rehearsal on a '
+                        '1-GPU box; use with --backend gloo)')
     return p.parse_args()
 
 
-def setup() -> tuple[int, int, torch.device]:
+def setup(args: argparse.Namespace) -> tuple[int, int, torch.device]:
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
+    local = 0 if args.same_device else int(os.environ.get('LOCAL_RANK', '0'))
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
     if world > 1:
-        dist.init_process_group('nccl', device_id=dev)
+        if args.backend == 'nccl':
+            dist.init_process_group('nccl', device_id=dev)
+        else:
+            dist.init_process_group(args.backend)
     return rank, world, dev
 
 
@@ -97,8 +114,13 @@ def run(args: argparse.Namespace, use_kfac: bool, rank: int, world: int,
     opt = torch.optim.SGD(model.parameters(), lr=lr, momentum=0.9,
                           weight_decay=5e-5)
     precond = None
+    impl = kfac
+    if use_kfac and args.impl == 'reference':
+        sys.path.insert(0, os.environ['KFAC_REFERENCE_PATH'])
+        import kfac as ref_kfac  # upstream package, same constructor API
+        impl = ref_kfac.preconditioner
     if use_kfac:
-        precond = kfac.KFACPreconditioner(
+        precond = impl.KFACPreconditioner(
             model,
             factor_update_steps=args.kfac_factor_update_steps,
             inv_update_steps=args.kfac_inv_update_steps,
@@ -151,7 +173,7 @@ def run(args: argparse.Namespace, use_kfac: bool, rank: int, world: int,
         }
         out['phase_counts'] = timer.counts()
         tracing.enable_phase_timing(False)
-    if precond is not None:
+    if precond is not None and args.impl == 'native':
         out['kfac_layers'] = len(precond._layers)
         out['kfac_steps_end'] = precond.steps
         mem = precond.memory_usage()
@@ -163,7 +185,7 @@ def run(args: argparse.Namespace, use_kfac: bool, rank: int, world: int,
 
 def main() -> None:
     args = parse_args()
-    rank, world, dev = setup()
+    rank, world, dev = setup(args)
     if world != args.gpus and rank == 0:
         print(f'[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}',
               file=sys.stderr)
@@ -174,6 +196,7 @@ def main() -> None:
     gb = args.batch_size * world
     value = gb * args.steps / res['seconds']
     line = {
+        'impl': args.impl,
         'metric': 'images/sec (whole node), ResNet-50 ImageNet K-FAC training',
         'value': round(value, 2),
         'unit': 'images/s',
@@ -183,8 +206,7 @@ def main() -> None:
         'ms_per_step': round(res['ms_per_step'], 3),
         'higher_is_better': True,
         'scaling': 'weak',
-        'vs_baseline': (round(value / BASELINE_IMG_S, 4)
-                        if BASELINE_IMG_S else None),
+        'vs_baseline': round(value / (REFERENCE_IMG_S_PER_GPU * world), 4),
         'dtype': 'fp32' if args.fp32 else 'bf16',
         'data': 'synthetic (random 224x224 images / labels, random-init '
                 'weights)',

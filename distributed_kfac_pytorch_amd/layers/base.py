@@ -276,7 +276,9 @@ class KFACBaseLayer:
 
     def save_layer_input(self, input: list[torch.Tensor]) -> None:
         """Accumulate the A contribution of one forward input."""
-        a = input[0]
+        self._save_a(input[0])
+
+    def _save_a(self, a: torch.Tensor) -> None:
         dtype = self._storage_dtype(a)
         d = self.module.a_factor_shape[0]
         if self._a_batch is None:
@@ -289,7 +291,9 @@ class KFACBaseLayer:
 
     def save_layer_grad_output(self, grad_output: tuple[torch.Tensor, ...]) -> None:
         """Accumulate the G contribution of one output gradient."""
-        g = grad_output[0]
+        self._save_g(grad_output[0])
+
+    def _save_g(self, g: torch.Tensor) -> None:
         dtype = self._storage_dtype(g)
         d = self.module.g_factor_shape[0]
         alpha = self._g_unscale()
@@ -337,11 +341,13 @@ class KFACBaseLayer:
 
     # fused fast paths (one micro-batch per factor update)
     def save_and_update_a(self, input: list[torch.Tensor], alpha: float) -> None:
-        a = input[0]
+        self._save_and_update_a(input[0], alpha)
+
+    def _save_and_update_a(self, a: torch.Tensor, alpha: float) -> None:
         if self._a_batch is not None or not (
             a.is_cuda and self._storage_dtype(a) == torch.float32
         ):
-            self.save_layer_input(input)
+            self._save_a(a)
             self.update_a_factor(alpha)
             return
         if self.a_factor is None:
@@ -350,11 +356,13 @@ class KFACBaseLayer:
         self.module.accumulate_a_factor(a, self.a_factor, 1.0 - alpha, alpha)
 
     def save_and_update_g(self, grad_output: tuple[torch.Tensor, ...], alpha: float) -> None:
-        g = grad_output[0]
+        self._save_and_update_g(grad_output[0], alpha)
+
+    def _save_and_update_g(self, g: torch.Tensor, alpha: float) -> None:
         if self._g_batch is not None or not (
             g.is_cuda and self._storage_dtype(g) == torch.float32
         ):
-            self.save_layer_grad_output(grad_output)
+            self._save_g(g)
             self.update_g_factor(alpha)
             return
         if self.g_factor is None:
