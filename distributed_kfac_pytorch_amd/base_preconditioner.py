@@ -47,23 +47,27 @@ logger = logging.getLogger(__name__)
 
 
 class StepGraphs:
-    """HIP-graph replay of the per-step precondition + apply phases.
+    """HIP-graph replay of the per-step precondition (+ apply) phases.
 
     Between second-order updates the precondition phase is a fixed chain of
     ~6 launches per layer (4 hipBLASLt GEMMs, a rank-1 update, the eigenvalue
     scaling) plus the three multi-tensor KL / apply launches -- ~330 small
     launches per ResNet-50 step, host-launch bound from Python.  All operands
-    live in persistent buffers (factors' eigenbases are installed in place,
-    P / temporaries are per-layer buffers, gradients are the parameters'
+    live in persistent buffers (eigenbases are installed in place, P and the
+    temporaries are per-layer buffers, gradients are the parameters'
     ``.grad``), so the chain is captured once into a HIP graph and replayed.
 
+    * Without gradient broadcasts (COMM-OPT, one rank): one graph covers
+      precondition + KL clip + gradient write.
+    * With gradient broadcasts (HYBRID / MEM-OPT): the graph covers this
+      rank's preconditioning only; the bucketed RCCL broadcasts and the
+      three apply launches follow eagerly.
+
     Capture happens on the second consecutive eligible step with the same
-    buffer addresses and hyperparameters baked into kernels (damping without
-    prediv); any change falls back to eager execution and re-captures.
-    Eligible steps: GPU, native extension present, not an inverse-update step,
-    and no gradient broadcast inside the phase (COMM-OPT / single rank).
-    KL-clip and lr values are read by the kernels from a device buffer that
-    is refreshed before each replay, so LR schedules do not force re-capture.
+    buffer addresses and baked-in hyperparameters (damping without prediv);
+    any change falls back to eager execution and re-captures.  Inverse-update
+    steps always run eagerly.  KL-clip / lr values are read by the kernels
+    from a device buffer refreshed before each replay.
     """
 
     def __init__(self) -> None:
@@ -77,29 +81,38 @@ class StepGraphs:
     def _ptr(t: Any) -> int:
         return t.data_ptr() if isinstance(t, torch.Tensor) else 0
 
-    def _key(self, pre: 'BaseKFACPreconditioner', ordered: list) -> tuple | None:
-        parts: list = []
+    def _key(
+        self,
+        pre: 'BaseKFACPreconditioner',
+        ordered: list,
+        bcast: bool,
+    ) -> tuple | None:
+        parts: list = [bcast]
         for name, layer in ordered:
-            if not pre._assignment.is_grad_worker(name):
+            worker = pre._assignment.is_grad_worker(name)
+            if not worker and not bcast:
                 return None
-            if not isinstance(layer, KFACEigenLayer):
-                parts.append(('inv', self._ptr(getattr(layer, 'a_inv', None)),
-                              self._ptr(getattr(layer, 'g_inv', None))))
-            else:
-                if layer.qa is None or layer.qa.dtype != torch.float32:
-                    return None
-                parts.append((self._ptr(layer.qa), self._ptr(layer.qg),
-                              self._ptr(layer.dgda), self._ptr(layer.da),
-                              self._ptr(layer.dg), layer.prediv_eigenvalues))
             m = layer.module
             w = m.module.weight.grad
             if w is None or not w.is_cuda:
                 return None
             b = m.module.bias.grad if m.has_bias() else None
-            parts.append((w.data_ptr(), self._ptr(b),
-                          self._ptr(layer._grad_buf),
-                          self._ptr(getattr(layer, '_tmp1', None)),
-                          self._ptr(getattr(layer, '_tmp2', None))))
+            parts.append((worker, w.data_ptr(), self._ptr(b), self._ptr(layer._grad_buf)))
+            if not worker:
+                continue
+            if isinstance(layer, KFACEigenLayer):
+                if layer.qa is None or layer.qa.dtype != torch.float32:
+                    return None
+                parts.append((self._ptr(layer.qa), self._ptr(layer.qg),
+                              self._ptr(layer.dgda), self._ptr(layer.da),
+                              self._ptr(layer.dg), layer.prediv_eigenvalues,
+                              self._ptr(layer._tmp1), self._ptr(layer._tmp2)))
+            else:
+                a_inv = getattr(layer, 'a_inv', None)
+                if a_inv is None or a_inv.dtype != torch.float32:
+                    return None
+                parts.append((self._ptr(a_inv), self._ptr(layer.g_inv),
+                              self._ptr(getattr(layer, '_tmp1', None))))
         needs_damping = any(
             isinstance(l, KFACEigenLayer) and not l.prediv_eigenvalues
             for _, l in ordered
@@ -119,53 +132,62 @@ class StepGraphs:
         if inverse_step or not ordered or _native.native() is None:
             self.pending_key = None
             return False
-        if pre._assignment.broadcast_gradients():
+        if ordered[0][1].module.device.type != 'cuda':
             return False
-        if not ordered[0][1].module.device.type == 'cuda':
-            return False
-        key = self._key(pre, ordered)
+        bcast = pre._assignment.broadcast_gradients()
+        key = self._key(pre, ordered, bcast)
         if key is None:
             return False
         layers = [l for _, l in ordered]
+        workers = [l for n, l in ordered if pre._assignment.is_grad_worker(n)]
         if pre._multi_apply is None:
             pre._multi_apply = pops.MultiLayerApply()
         kl = pre.kl_clip
-        if key == self.key and self.graph is not None:
-            if not pre._multi_apply.prepare(layers, kl, float(pre.lr), use_buffers=True):
+        lr = float(pre.lr)
+        if not (key == self.key and self.graph is not None):
+            if key != self.pending_key:
+                # first sighting of this configuration: run eagerly, capture next
+                self.pending_key = key
                 return False
-            with tracing.phase('precondition+apply(graph)'):
-                self.graph.replay()
-            self.replays += 1
+            if not bcast and not pre._multi_apply.prepare(layers, kl, lr, use_buffers=True):
+                return False
+            damping = pre.damping
+            g = torch.cuda.CUDAGraph()
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                with torch.cuda.graph(g, stream=side):
+                    for l in workers:
+                        l.preconditioned_grad(damping=damping)
+                    if not bcast:
+                        pre._multi_apply.launch(kl is not None)
+            torch.cuda.current_stream().wait_stream(side)
+            self.graph, self.key, self.pending_key = g, key, None
+            self.captures += 1
+        elif not bcast and not pre._multi_apply.prepare(layers, kl, lr, use_buffers=True):
+            return False
+        label = 'precondition(graph)' if bcast else 'precondition+apply(graph)'
+        with tracing.phase(label):
+            self.graph.replay()
+        self.replays += 1
+        if not bcast:
             for l in layers:
                 l.grad = None
             return True
-        if key != self.pending_key:
-            # first sighting of this configuration: run eagerly, capture next
-            self.pending_key = key
-            return False
-        # second consecutive sighting: capture, then replay once for this step
-        if not pre._multi_apply.prepare(layers, kl, float(pre.lr), use_buffers=True):
-            return False
-        damping = pre.damping
-        g = torch.cuda.CUDAGraph()
-        side = torch.cuda.Stream()
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            with torch.cuda.graph(g, stream=side):
-                for _, l in ordered:
-                    l.preconditioned_grad(damping=damping)
-                pre._multi_apply.launch(kl is not None)
-        torch.cuda.current_stream().wait_stream(side)
-        self.graph = g
-        self.key = key
-        self.pending_key = None
-        self.captures += 1
-        with tracing.phase('precondition+apply(graph)'):
-            g.replay()
-        for l in layers:
-            l.grad = None
+        for l in workers:
+            l.grad = l._grad_buf
+        with tracing.phase('grad_broadcast'):
+            for name, l in ordered:
+                l.broadcast_grad(
+                    src=pre._assignment.src_grad_worker(name),
+                    group=pre._assignment.grad_receiver_group(name),
+                    bucketed=True,
+                )
+            pre._tdc.flush_broadcast_buckets()
+            pre._tdc.flush_allreduce_buckets()
+        with tracing.phase('apply'):
+            pre._apply_gradients(ordered, kl)
         return True
-
 
 class BaseKFACPreconditioner:
     """Distributed K-FAC gradient preconditioner (layer-agnostic runtime)."""
@@ -479,7 +501,9 @@ class BaseKFACPreconditioner:
                 layer.broadcast_grad(
                     src=self._assignment.src_grad_worker(name),
                     group=self._assignment.grad_receiver_group(name),
+                    bucketed=True,
                 )
+        self._tdc.flush_broadcast_buckets()
         self._tdc.flush_allreduce_buckets()
 
     def _apply_gradients(

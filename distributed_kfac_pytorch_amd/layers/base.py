@@ -202,9 +202,16 @@ class KFACBaseLayer:
             self._grad_buf = torch.empty(shape, dtype=torch.float32, device=device)
         return self._grad_buf
 
-    def broadcast_grad(self, src: int, group: dist.ProcessGroup | None = None) -> None:
+    def broadcast_grad(
+        self,
+        src: int,
+        group: dist.ProcessGroup | None = None,
+        bucketed: bool = False,
+    ) -> None:
         """Broadcast the preconditioned gradient from ``src`` (every rank of
-        the receiver group enters)."""
+        the receiver group enters).  ``bucketed`` routes it through the
+        communicator's fused per-(group, src) broadcast buckets; the caller
+        must then call ``tdc.flush_broadcast_buckets()`` on every rank."""
         if self.grad is None:
             if get_rank() == src:
                 raise RuntimeError(
@@ -212,7 +219,12 @@ class KFACBaseLayer:
                     'rank has not computed the preconditioned gradient yet.',
                 )
             self.grad = self._grad_buffer(self.module.device)
-        self.grad = self.tdc.broadcast(self.grad, src=src, group=group)
+        g = self.grad
+        if bucketed and self.tdc.bucket_cap_bytes > 0 and g.is_contiguous():
+            # fused per-(group, src) broadcast; flushed by the preconditioner
+            self.grad = self.tdc.broadcast_bucketed(g, src=src, group=group)
+        else:
+            self.grad = self.tdc.broadcast(g, src=src, group=group)
 
     def update_grad(self, scale: torch.Tensor | float | None = None) -> None:
         """Write ``scale * preconditioned grad`` into the module gradients."""

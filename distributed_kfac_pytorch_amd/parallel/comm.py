@@ -239,6 +239,7 @@ class TorchDistributedCommunicator:
         self._bucket_cap_mb = bucket_cap_mb
         self._bucket_cap_bytes = int(bucket_cap_mb * 1000 * 1000)
         self._allreduce_buckets: dict[Any, AllreduceTensorBucket | None] = {}
+        self._broadcast_buckets: dict[Any, BroadcastTensorBucket] = {}
 
     @property
     def bucket_cap_bytes(self) -> int:
@@ -363,6 +364,44 @@ class TorchDistributedCommunicator:
 
         return bucket.add_tensor(tensor, symmetric=symmetric, finalize=_finish)
 
+    def broadcast_bucketed(
+        self,
+        tensor: torch.Tensor,
+        *,
+        src: int,
+        group: dist.ProcessGroup | None = None,
+    ) -> AsyncTensor | torch.Tensor:
+        """Broadcast through a flat bucket per (group, src).
+
+        Used for the per-step preconditioned-gradient broadcasts:
+        ResNet-50 would otherwise issue 54 small RCCL broadcasts per step.
+        Buckets are launched when full (``bucket_cap_mb``) or on
+        ``flush_broadcast_buckets()``; every rank of ``group`` must add the
+        same tensors (shapes) in the same order.  The value is written in
+        place into ``tensor`` on receivers.
+        """
+        if get_world_size(group) == 1:
+            return tensor
+        if not tensor.is_contiguous():
+            raise RuntimeError('bucketed broadcast needs contiguous tensors')
+        key = (group, src)
+        nbytes = tensor.numel() * tensor.element_size()
+        bucket = self._broadcast_buckets.get(key)
+        if bucket is None:
+            bucket = BroadcastTensorBucket(group, src)
+            self._broadcast_buckets[key] = bucket
+        elif bucket.size + nbytes > self._bucket_cap_bytes:
+            bucket.broadcast()
+            bucket = BroadcastTensorBucket(group, src)
+            self._broadcast_buckets[key] = bucket
+        return bucket.add_tensor(tensor)
+
+    def flush_broadcast_buckets(self) -> None:
+        """Launch every pending broadcast bucket, in creation order."""
+        for key in list(self._broadcast_buckets):
+            bucket = self._broadcast_buckets.pop(key)
+            bucket.broadcast()
+
     def flush_allreduce_buckets(self) -> None:
         """Launch every partially filled bucket (collective on all ranks)."""
         for key in list(self._allreduce_buckets):
@@ -370,3 +409,66 @@ class TorchDistributedCommunicator:
             if bucket is not None:
                 bucket.allreduce()
                 self._allreduce_buckets[key] = None
+
+
+class BroadcastTensorBucket:
+    """A fused broadcast of several same-dtype tensors from one source."""
+
+    def __init__(self, group: dist.ProcessGroup | None, src: int) -> None:
+        self._group = group
+        self._src = src
+        self._tensors: list[torch.Tensor] = []
+        self._size = 0
+        self._sent = False
+        self.work: Any | None = None
+        self.flat: torch.Tensor | None = None
+
+    @property
+    def size(self) -> int:
+        return self._size
+
+    def communicated(self) -> bool:
+        return self._sent
+
+    def add_tensor(self, tensor: torch.Tensor) -> AsyncTensor:
+        if self._sent:
+            raise RuntimeError('bucket was already communicated')
+        if self._tensors and tensor.dtype != self._tensors[0].dtype:
+            raise RuntimeError('a broadcast bucket holds a single dtype')
+        offset = sum(t.numel() for t in self._tensors)
+        n = tensor.numel()
+        self._tensors.append(tensor)
+        self._size += n * tensor.element_size()
+        is_src = get_rank() == self._src
+
+        def _finish() -> torch.Tensor:
+            assert self.flat is not None
+            sl = self.flat[offset: offset + n]
+            if not is_src and sl.data_ptr() != tensor.data_ptr():
+                comm_pack.scale_copy_(tensor, sl, 1.0)
+            return tensor
+
+        return AsyncTensor(finalize=_finish, bucket=self)  # type: ignore[arg-type]
+
+    def allreduce(self) -> Any:  # AsyncTensor resolves through .work
+        return self.broadcast()
+
+    def broadcast(self) -> Any | None:
+        if self._sent:
+            raise RuntimeError('bucket was already communicated')
+        self._sent = True
+        if not self._tensors:
+            return None
+        ref = self._tensors[0]
+        total = sum(t.numel() for t in self._tensors)
+        if len(self._tensors) == 1:
+            self.flat = ref.view(-1)
+        else:
+            self.flat = torch.empty(total, dtype=ref.dtype, device=ref.device)
+            if get_rank() == self._src:
+                off = 0
+                for t in self._tensors:
+                    self.flat[off: off + t.numel()].copy_(t.view(-1))
+                    off += t.numel()
+        self.work = dist.broadcast(self.flat, src=self._src, group=self._group, async_op=True)
+        return self.work

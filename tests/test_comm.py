@@ -176,3 +176,25 @@ def _subgroup_body():
 
 def test_subgroup_buckets():
     _subgroup_body()
+
+
+@distributed_test(2)
+def _bcast_bucket_body():
+    rank = dist.get_rank()
+    tdc = TorchDistributedCommunicator(bucket_cap_mb=1e-4)  # 100 bytes
+    shapes = [(2, 3), (4, 4), (10, 10), (1, 5)]
+    srcs = [0, 1, 0, 1]
+    handles, expect = [], []
+    for i, (s, src) in enumerate(zip(shapes, srcs)):
+        val = torch.full(s, float(i + 10 * src))
+        t = val.clone() if rank == src else torch.zeros(s)
+        handles.append(tdc.broadcast_bucketed(t, src=src))
+        expect.append(val)
+    tdc.flush_broadcast_buckets()
+    for h, e in zip(handles, expect):
+        out = h.wait() if isinstance(h, AsyncTensor) else h
+        assert torch.equal(out, e)
+
+
+def test_broadcast_bucketed():
+    _bcast_bucket_body()
