@@ -418,8 +418,15 @@ class BaseKFACPreconditioner:
             (n, l) for n, l in items
             if all_ranks or rank == self._assignment.inv_worker(n, 'G')
         ]
-        eig_a = [(n, l) for n, l in mine_a if isinstance(l, KFACEigenLayer) and l.symmetric_factors]
-        eig_g = [(n, l) for n, l in mine_g if isinstance(l, KFACEigenLayer) and l.symmetric_factors]
+        def batchable(l: KFACBaseLayer) -> bool:
+            return (
+                isinstance(l, KFACEigenLayer)
+                and l.symmetric_factors
+                and getattr(l, 'supports_batched_eigh', True)
+            )
+
+        eig_a = [(n, l) for n, l in mine_a if batchable(l)]
+        eig_g = [(n, l) for n, l in mine_g if batchable(l)]
         batched = {id(l) for _, l in eig_a} | {id(l) for _, l in eig_g}
         mats = []
         for _, l in eig_a:

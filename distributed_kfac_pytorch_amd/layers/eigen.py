@@ -35,6 +35,9 @@ from distributed_kfac_pytorch_amd.parallel.comm import get_rank
 class KFACEigenLayer(KFACBaseLayer):
     """K-FAC layer preconditioning through factor eigendecompositions."""
 
+    #: factors can go through the batched multi-layer eigensolver
+    supports_batched_eigh = True
+
     def __init__(self, module: Any, *, prediv_eigenvalues: bool = False, **kwargs: Any) -> None:
         """Init KFACEigenLayer.
 

@@ -74,6 +74,40 @@ def resolve_grad_worker_fraction(
     return frac, DistributedStrategy.HYBRID_OPT
 
 
+def _add_embeddings(
+    model: torch.nn.Module,
+    layers: dict,
+    compute_method: ComputeMethod,
+    skip_layers: list[str],
+    layer_kwargs: dict,
+) -> dict:
+    """Register ``nn.Embedding`` modules too, keeping model order."""
+    from distributed_kfac_pytorch_amd.layers.embedding import EmbeddingModuleHelper
+    from distributed_kfac_pytorch_amd.layers.embedding import KFACEmbeddingEigenLayer
+    from distributed_kfac_pytorch_amd.layers.embedding import KFACEmbeddingInverseLayer
+    from distributed_kfac_pytorch_amd.layers.register import get_flattened_modules
+
+    def factory(m: torch.nn.Module) -> EmbeddingModuleHelper | None:
+        if isinstance(m, torch.nn.Embedding) and not m.sparse and m.max_norm is None:
+            return EmbeddingModuleHelper(m)
+        return None
+
+    if compute_method == ComputeMethod.EIGEN:
+        emb_type: type[KFACBaseLayer] = KFACEmbeddingEigenLayer
+        kw = layer_kwargs
+    else:
+        emb_type = KFACEmbeddingInverseLayer
+        kw = {k: v for k, v in layer_kwargs.items() if k != 'prediv_eigenvalues'}
+    emb = register_modules(model, emb_type, skip_layers, helper_factory=factory, **kw)
+    merged = {}
+    for _, m in get_flattened_modules(model):
+        if m in layers:
+            merged[m] = layers[m]
+        elif m in emb:
+            merged[m] = emb[m]
+    return merged
+
+
 class KFACPreconditioner(BaseKFACPreconditioner):
     """KFAC distributed gradient preconditioner with KAISA placement."""
 
@@ -101,6 +135,7 @@ class KFACPreconditioner(BaseKFACPreconditioner):
         skip_layers: list[str] | None = None,
         update_factors_in_hook: bool = True,
         loglevel: int = logging.DEBUG,
+        register_embeddings: bool = False,
     ) -> None:
         """Init KFACPreconditioner.
 
@@ -128,6 +163,9 @@ class KFACPreconditioner(BaseKFACPreconditioner):
             skip_layers: regexes of module names / class names to skip.
             update_factors_in_hook: update factors inside the hooks.
             loglevel: logging level of registration messages.
+            register_embeddings: also precondition ``nn.Embedding`` layers
+                (diagonal A factor, ``layers.embedding``).  Off by default
+                for parity with the reference, which ignores embeddings.
         """
         if allreduce_bucket_cap_mb < 0:
             raise ValueError('allreduce_bucket_cap_mb must be >= 0')
@@ -195,6 +233,11 @@ class KFACPreconditioner(BaseKFACPreconditioner):
             skip_layers=self.skip_layers,
             **layer_kwargs,
         )
+        self.register_embeddings = register_embeddings
+        if register_embeddings:
+            kfac_layers = _add_embeddings(
+                model, kfac_layers, compute_method, self.skip_layers, layer_kwargs,
+            )
         for name, layer in kfac_layers.values():
             logger.log(loglevel, f'Registered name="{name}": {layer!r}')
 
@@ -238,6 +281,7 @@ class KFACPreconditioner(BaseKFACPreconditioner):
             'inv_dtype': self.inv_dtype,
             'skip_layers': self.skip_layers,
             'symmetry_aware': self.symmetry_aware,
+            'register_embeddings': self.register_embeddings,
         }
         super().__init__(
             kfac_layers,
