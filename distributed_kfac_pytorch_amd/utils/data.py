@@ -112,3 +112,77 @@ class TokenFile(Dataset):
 
     def __getitem__(self, i: int) -> tuple[torch.Tensor, torch.Tensor]:
         return self.inputs[i], self.targets[i]
+
+
+IMAGENET_MEAN = (0.485, 0.456, 0.406)
+IMAGENET_STD = (0.229, 0.224, 0.225)
+_IMG_EXT = ('.jpg', '.jpeg', '.png', '.bmp', '.webp', '.JPEG')
+
+
+class ImageFolder(Dataset):
+    """``root/<class>/<image>`` dataset decoded with PIL (torchvision is not
+    available in this image).  Train: RandomResizedCrop(size, scale
+    (0.08, 1), ratio (3/4, 4/3)) + horizontal flip; eval: resize the short
+    side to ``size*8/7`` then center crop -- the standard ImageNet recipe
+    the reference gets from torchvision (``examples/vision/datasets.py:
+    71-151``).  Returns a normalised float CHW tensor and the class index.
+    """
+
+    def __init__(self, root: str, train: bool = True, size: int = 224) -> None:
+        self.classes = sorted(
+            d for d in os.listdir(root) if os.path.isdir(os.path.join(root, d))
+        )
+        self.samples: list[tuple[str, int]] = []
+        for ci, c in enumerate(self.classes):
+            for dirpath, _, files in sorted(os.walk(os.path.join(root, c))):
+                for f in sorted(files):
+                    if f.endswith(_IMG_EXT):
+                        self.samples.append((os.path.join(dirpath, f), ci))
+        self.train, self.size = train, size
+        self._mean = torch.tensor(IMAGENET_MEAN).view(3, 1, 1)
+        self._std = torch.tensor(IMAGENET_STD).view(3, 1, 1)
+
+    def __len__(self) -> int:
+        return len(self.samples)
+
+    def _random_resized_crop(self, img):  # type: ignore[no-untyped-def]
+        import math
+        import random
+        w, h = img.size
+        area = w * h
+        for _ in range(10):
+            target = area * random.uniform(0.08, 1.0)
+            ar = math.exp(random.uniform(math.log(3 / 4), math.log(4 / 3)))
+            cw = int(round(math.sqrt(target * ar)))
+            ch = int(round(math.sqrt(target / ar)))
+            if 0 < cw <= w and 0 < ch <= h:
+                x0 = random.randint(0, w - cw)
+                y0 = random.randint(0, h - ch)
+                return img.crop((x0, y0, x0 + cw, y0 + ch))
+        s = min(w, h)
+        return img.crop(((w - s) // 2, (h - s) // 2, (w - s) // 2 + s, (h - s) // 2 + s))
+
+    def __getitem__(self, i: int) -> tuple[torch.Tensor, int]:
+        import random
+
+        import numpy as np
+        from PIL import Image
+        path, label = self.samples[i]
+        with Image.open(path) as im:
+            img = im.convert('RGB')
+        if self.train:
+            img = self._random_resized_crop(img).resize((self.size, self.size), Image.BILINEAR)
+            if random.random() < 0.5:
+                img = img.transpose(Image.FLIP_LEFT_RIGHT)
+        else:
+            short = int(self.size * 8 / 7)
+            w, h = img.size
+            scale = short / min(w, h)
+            img = img.resize((max(short, round(w * scale)), max(short, round(h * scale))),
+                             Image.BILINEAR)
+            w, h = img.size
+            x0, y0 = (w - self.size) // 2, (h - self.size) // 2
+            img = img.crop((x0, y0, x0 + self.size, y0 + self.size))
+        x = torch.from_numpy(np.asarray(img, dtype=np.uint8).copy()).permute(2, 0, 1)
+        x = (x.float() / 255.0 - self._mean) / self._std
+        return x, label
