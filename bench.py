@@ -65,6 +65,10 @@ def parse_args() -> argparse.Namespace:
     p.add_argument('--no-channels-last', action='store_true')
     p.add_argument('--fp32', action='store_true', help='disable bf16 autocast')
     p.add_argument('--phase-timing', action='store_true')
+    p.add_argument('--cudnn-benchmark', type=int, default=0,
+                   help='MIOpen exhaustive find for the model convolutions')
+    p.add_argument('--profile-mark', action='store_true',
+                   help='bracket the timed steps with marker kernels (rocprof windows)')
     p.add_argument('--lr', type=float, default=0.0125)
     p.add_argument('--impl', default='native', choices=['native', 'reference'],
                    help='reference = time the upstream kfac_pytorch package '
@@ -84,6 +88,7 @@ def setup(args: argparse.Namespace) -> tuple[int, int, torch.device]:
     local = 0 if args.same_device else int(os.environ.get('LOCAL_RANK', '0'))
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
+    torch.backends.cudnn.benchmark = bool(args.cudnn_benchmark)
     if world > 1:
         if args.backend == 'nccl':
             dist.init_process_group('nccl', device_id=dev)
@@ -97,6 +102,21 @@ def barrier_sync(world: int) -> None:
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+
+
+def _profile_marker(dev: torch.device):  # type: ignore[no-untyped-def]
+    """Launch a tiny native ``identity_kernel`` at both ends of the timed
+    region so ``tools/trace_summary.py --window identity_kernel`` can cut
+    the steady-state steps out of a rocprofv3 kernel trace."""
+    from distributed_kfac_pytorch_amd.ops import _native
+    buf = torch.empty(1, 1, device=dev)
+    ext = _native.native()
+    assert ext is not None, _native.load_error()
+
+    def mark() -> None:
+        ext.fill_identity(buf)
+
+    return mark
 
 
 def run(args: argparse.Namespace, use_kfac: bool, rank: int, world: int,
@@ -156,10 +176,15 @@ def run(args: argparse.Namespace, use_kfac: bool, rank: int, world: int,
     timer = None
     if args.phase_timing and precond is not None:
         timer = tracing.enable_phase_timing(True)
+    marker = _profile_marker(dev) if args.profile_mark else None
     barrier_sync(world)
+    if marker is not None:
+        marker()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    if marker is not None:
+        marker()
     barrier_sync(world)
     elapsed = time.perf_counter() - t0
     t = torch.tensor([elapsed], device=dev, dtype=torch.float64)

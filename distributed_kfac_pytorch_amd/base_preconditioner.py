@@ -76,6 +76,36 @@ class StepGraphs:
         self.pending_key: tuple | None = None
         self.replays = 0
         self.captures = 0
+        self._lane_streams: list = []
+
+    def _streams(self, n: int) -> list:
+        while len(self._lane_streams) < n:
+            self._lane_streams.append(torch.cuda.Stream())
+        return self._lane_streams[:n]
+
+    @staticmethod
+    def _lanes(workers: list) -> list[list]:
+        """Split the layers into ``KFAC_PRECOND_STREAMS`` (default 4)
+        cost-balanced lanes (greedy LPT on the precondition GEMM flops
+        ``g*a*(g+a)``); each lane keeps model order."""
+        n = max(1, min(int(os.environ.get('KFAC_PRECOND_STREAMS', '4')), len(workers)))
+        if n == 1:
+            return [list(workers)]
+
+        def cost(l: Any) -> float:
+            g, a = l.module.g_factor_shape[0], l.module.a_factor_shape[0]
+            return float(g) * a * (g + a)
+
+        load = [0.0] * n
+        which: dict[int, int] = {}
+        for i in sorted(range(len(workers)), key=lambda i: -cost(workers[i])):
+            k = min(range(n), key=lambda j: load[j])
+            load[k] += cost(workers[i])
+            which[i] = k
+        lanes: list[list] = [[] for _ in range(n)]
+        for i, l in enumerate(workers):
+            lanes[which[i]].append(l)
+        return [ln for ln in lanes if ln]
 
     @staticmethod
     def _ptr(t: Any) -> int:
@@ -155,10 +185,18 @@ class StepGraphs:
             g = torch.cuda.CUDAGraph()
             side = torch.cuda.Stream()
             side.wait_stream(torch.cuda.current_stream())
+            lanes = self._lanes(workers)
             with torch.cuda.stream(side):
                 with torch.cuda.graph(g, stream=side):
-                    for l in workers:
-                        l.preconditioned_grad(damping=damping)
+                    # fork: independent per-layer GEMM chains run as parallel
+                    # graph branches (small layers cannot fill 256 CUs alone)
+                    for lane, members in zip(self._streams(len(lanes)), lanes):
+                        lane.wait_stream(side)
+                        with torch.cuda.stream(lane):
+                            for l in members:
+                                l.preconditioned_grad(damping=damping)
+                    for lane in self._streams(len(lanes)):
+                        side.wait_stream(lane)
                     if not bcast:
                         pre._multi_apply.launch(kl is not None)
             torch.cuda.current_stream().wait_stream(side)
