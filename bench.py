@@ -65,8 +65,8 @@ def parse_args() -> argparse.Namespace:
     p.add_argument('--no-channels-last', action='store_true')
     p.add_argument('--fp32', action='store_true', help='disable bf16 autocast')
     p.add_argument('--phase-timing', action='store_true')
-    p.add_argument('--cudnn-benchmark', type=int, default=0,
-                   help='MIOpen exhaustive find for the model convolutions')
+    p.add_argument('--cudnn-benchmark', type=int, default=1,
+                   help='MIOpen find (benchmark mode) for the model convolutions')
     p.add_argument('--profile-mark', action='store_true',
                    help='bracket the timed steps with marker kernels (rocprof windows)')
     p.add_argument('--lr', type=float, default=0.0125)
@@ -131,8 +131,9 @@ def run(args: argparse.Namespace, use_kfac: bool, rank: int, world: int,
             model, device_ids=[dev.index], gradient_as_bucket_view=True,
         )
     lr = args.lr * world
+    # foreach: multi-tensor SGD step and a multi-tensor zero_grad
     opt = torch.optim.SGD(model.parameters(), lr=lr, momentum=0.9,
-                          weight_decay=5e-5)
+                          weight_decay=5e-5, foreach=True)
     precond = None
     impl = kfac
     if use_kfac and args.impl == 'reference':

@@ -7,11 +7,13 @@
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cstring>
 #include <tuple>
 #include <vector>
 
 #include "common.h"
+#include "descs.h"
 
 namespace kfac {
 // pack.hip
@@ -57,14 +59,6 @@ void jacobi_eigh_batched(const float* A, int64_t n, int64_t batch,
                          int64_t strideV, int max_sweeps, float tol,
                          hipStream_t s);
 // multi.hip
-struct LayerDesc {
-  const float* p;
-  void* w;
-  void* b;
-  int64_t rows, cols, ldp, wcols;
-  int64_t block_start;
-  int32_t wdt, bdt;
-};
 int64_t multi_blocks_for(int64_t rows, int64_t cols);
 void kl_dot_multi(const LayerDesc* descs, int nlayers, int64_t total_blocks,
                   double* acc, hipStream_t s);
@@ -72,6 +66,10 @@ void kl_finalize_dev(double* acc, const float* params, float* scale,
                      hipStream_t s);
 void apply_multi(const LayerDesc* descs, int nlayers, int64_t total_blocks,
                  const float* scale, hipStream_t s);
+// gemm3.hip
+int gemm3_grid(int total_tiles);
+void gemm3_grouped(const GemmDesc* table, int nlayers, int total_tiles,
+                   bool a_kc, bool b_kc, hipStream_t s);
 }  // namespace kfac
 
 // solver.cpp
@@ -391,6 +389,115 @@ void apply_multi(const at::Tensor& table, int64_t nlayers,
                     cur_stream());
 }
 
+const float* opt_ptr(const c10::optional<at::Tensor>& t, int64_t numel,
+                     const char* what) {
+  if (!t.has_value()) return nullptr;
+  TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous() &&
+                  t->numel() == numel,
+              what, ": expected a contiguous fp32 tensor of ", numel, " elements");
+  return t->data_ptr<float>();
+}
+
+bool vec_ok(const at::Tensor& t) {
+  return (t.stride(0) % 4 == 0) &&
+         ((reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0);
+}
+
+// Grouped bf16x3 GEMM table.  For layer i (logical C = A . B, [M,N,K]):
+//   a_kc: As[i] is [M, Kmain] (+ optional A_extra column -> K = Kmain + 1),
+//   else As[i] is the stored [K, M] (logical A = As^T);
+//   b_kc: Bs[i] is the stored [N, K] (logical B = Bs^T), else [K, N].
+// Optional epilogue scale: Ss[i] [M, N] or dgs[i] [M] with das[i] [N].
+// Layers are sorted by K (descending) so long tiles are dispatched first.
+std::tuple<at::Tensor, int64_t> build_gemm_table(
+    const std::vector<at::Tensor>& As,
+    const std::vector<c10::optional<at::Tensor>>& A_extras,
+    const std::vector<at::Tensor>& Bs, const std::vector<at::Tensor>& Cs,
+    const std::vector<c10::optional<at::Tensor>>& Ss,
+    const std::vector<c10::optional<at::Tensor>>& dgs,
+    const std::vector<c10::optional<at::Tensor>>& das,
+    const std::vector<double>& dampings, bool a_kc, bool b_kc) {
+  const size_t n = As.size();
+  TORCH_CHECK(A_extras.size() == n && Bs.size() == n && Cs.size() == n &&
+              Ss.size() == n && dgs.size() == n && das.size() == n &&
+              dampings.size() == n);
+  std::vector<kfac::GemmDesc> host(n);
+  for (size_t i = 0; i < n; ++i) {
+    const auto& A = As[i];
+    const auto& B = Bs[i];
+    const auto& C = Cs[i];
+    for (const at::Tensor* t : {&A, &B, &C}) {
+      check_cuda(*t, "gemm operand");
+      TORCH_CHECK(t->scalar_type() == at::kFloat && t->dim() == 2 &&
+                      (t->stride(1) == 1 || t->size(1) == 1),
+                  "gemm3: operands must be fp32 2-D with unit column stride");
+    }
+    const int64_t M = C.size(0), N = C.size(1);
+    const bool extra = A_extras[i].has_value();
+    TORCH_CHECK(!extra || a_kc, "gemm3: an extra A column needs a k-contiguous A");
+    const int64_t Kmain = a_kc ? A.size(1) : A.size(0);
+    const int64_t K = Kmain + (extra ? 1 : 0);
+    TORCH_CHECK((a_kc ? A.size(0) : A.size(1)) == M, "gemm3 layer ", i, ": A shape");
+    TORCH_CHECK(b_kc ? (B.size(0) == N && B.size(1) == K) : (B.size(0) == K && B.size(1) == N),
+                "gemm3 layer ", i, ": B shape");
+    TORCH_CHECK(M < (1 << 30) && N < (1 << 30) && K < (1 << 30));
+    kfac::GemmDesc d{};
+    d.A = A.data_ptr<float>();
+    d.A_extra = opt_ptr(A_extras[i], M, "A_extra");
+    d.B = B.data_ptr<float>();
+    d.C = C.data_ptr<float>();
+    d.lda = A.stride(0);
+    d.ldb = B.stride(0);
+    d.ldc = C.stride(0);
+    d.S = nullptr;
+    d.lds = 0;
+    if (Ss[i].has_value()) {
+      const auto& S = *Ss[i];
+      TORCH_CHECK(S.scalar_type() == at::kFloat && S.dim() == 2 && S.size(0) == M &&
+                  S.size(1) == N && (S.stride(1) == 1 || N == 1), "gemm3: S shape");
+      d.S = S.data_ptr<float>();
+      d.lds = S.stride(0);
+    }
+    d.dg = opt_ptr(dgs[i], M, "dg");
+    d.da = opt_ptr(das[i], N, "da");
+    TORCH_CHECK((d.dg == nullptr) == (d.da == nullptr), "gemm3: dg and da go together");
+    d.M = (int32_t)M;
+    d.N = (int32_t)N;
+    d.K = (int32_t)K;
+    d.Kmain = (int32_t)Kmain;
+    d.tiles_n = (int32_t)((N + 127) / 128);
+    d.damping = (float)dampings[i];
+    d.vec = (vec_ok(A) ? 1 : 0) | (vec_ok(B) ? 2 : 0);
+    host[i] = d;
+  }
+  std::stable_sort(host.begin(), host.end(),
+                   [](const kfac::GemmDesc& x, const kfac::GemmDesc& y) { return x.K > y.K; });
+  int64_t tiles = 0;
+  for (auto& d : host) {
+    d.tile_start = (int32_t)tiles;
+    tiles += (int64_t)((d.M + 127) / 128) * d.tiles_n;
+  }
+  TORCH_CHECK(tiles < (1LL << 30));
+  at::Tensor dev_t;
+  if (n > 0) {
+    const int64_t nbytes = (int64_t)(n * sizeof(kfac::GemmDesc));
+    auto cpu = at::empty({nbytes}, at::TensorOptions().dtype(at::kByte).pinned_memory(true));
+    std::memcpy(cpu.data_ptr(), host.data(), nbytes);
+    dev_t = cpu.to(Cs[0].device(), /*non_blocking=*/true);
+  }
+  return {dev_t, tiles};
+}
+
+void gemm3_grouped(const at::Tensor& table, int64_t nlayers, int64_t total_tiles,
+                   bool a_kc, bool b_kc) {
+  check_cuda(table, "table");
+  TORCH_CHECK(table.numel() == nlayers * (int64_t)sizeof(kfac::GemmDesc),
+              "gemm3: table size does not match the layer count");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(table.device());
+  kfac::gemm3_grouped((const kfac::GemmDesc*)table.data_ptr(), (int)nlayers,
+                      (int)total_tiles, a_kc, b_kc, cur_stream());
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -415,5 +522,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("apply_multi", &apply_multi);
   m.def("rocsolver_eigh", &rocsolver_eigh, py::arg("A"), py::arg("algo") = 0,
         py::arg("max_sweeps") = 100, py::arg("tol") = 1e-7);
+  m.def("build_gemm_table", &build_gemm_table);
+  m.def("gemm3_grouped", &gemm3_grouped);
   m.attr("arch") = "gfx950";
 }

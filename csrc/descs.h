@@ -1,0 +1,34 @@
+// Device descriptor tables shared by the multi-tensor kernels and the
+// bindings (one definition; the bindings pack them on the host).
+#pragma once
+#include <cstdint>
+
+namespace kfac {
+
+// multi.hip: one K-FAC layer of the KL-clip / apply launches
+struct LayerDesc {
+  const float* p;   // preconditioned grad [rows, cols], row stride ldp
+  void* w;          // weight grad [rows, wcols] contiguous
+  void* b;          // bias grad [rows] or null
+  int64_t rows, cols, ldp, wcols;
+  int64_t block_start;  // first block of this layer
+  int32_t wdt, bdt;     // dtype tags
+};
+
+// gemm3.hip: one GEMM of a grouped launch
+struct GemmDesc {
+  const float* A;        // A storage: [M][lda] (k-contig) or [K][lda] (m-contig)
+  const float* A_extra;  // optional column Kmain of A (k-contig only): [M]
+  const float* B;        // B storage: [K][ldb] (n-contig) or [N][ldb] (k-contig)
+  float* C;              // [M][ldc]
+  const float* S;        // optional scale matrix [M][lds]
+  const float* dg;       // optional scale vectors: C = acc / (dg[m]*da[n] + damping)
+  const float* da;
+  int64_t lda, ldb, ldc, lds;
+  int32_t M, N, K, Kmain;
+  int32_t tiles_n, tile_start;
+  float damping;
+  int32_t vec;  // bit0: A float4 loads ok, bit1: B float4 loads ok
+};
+
+}  // namespace kfac

@@ -1,0 +1,420 @@
+// K-HIP-4: grouped fp32 GEMM for the per-step K-FAC preconditioning, on
+// bf16 MFMA with a three-term split ("bf16x3").
+//
+// Every step the eigen method computes, for every layer l (reference
+// kfac/layers/eigen.py:349-384):
+//     V1 = QG^T [Wg | bg] QA,   V2 = V1 (.) S,   P = QG V2 QA^T
+// i.e. four dependent fp32 GEMMs per layer (S = 1/(dG (x) dA + damping) or
+// the precomputed dGdA).  ResNet-50 has 54 layers with shapes from 64x64 to
+// 512x4608 (K up to 4608): ~310 GFLOP/step.  The reference issues 4 cuBLAS
+// calls + elementwise ops per layer; on MI355X that is ~220 launches per
+// step, most of them too small to fill 256 CUs, and fp32 MFMA runs at
+// 1/16 of the bf16 rate (v_mfma_f32_32x32x2_f32: 64 cyc/SIMD vs 32 cyc for
+// a 32x32x16 bf16 MFMA of 8x the FLOPs).
+//
+// Here each chain step is ONE launch over all layers ("grouped GEMM"):
+//   * a device descriptor table lists the layers (sorted heavy-K first so
+//     the long tiles start first); a block finds its layer by binary search
+//     over per-layer tile prefix sums;
+//   * blockIdx -> tile mapping is XCD-aware: hardware dispatches block b to
+//     XCD b % 8, so chunks of CH consecutive tiles (same A row panel) are
+//     given to one XCD to share its L2, chunks round-robin across XCDs so
+//     the heavy-first order is kept on every XCD;
+//   * fp32 operands are split on the way into LDS: x = hi + lo with
+//     hi = bf16_rn(x), lo = bf16_rn(x - hi), and A.B is accumulated in fp32
+//     as hi.hi + hi.lo + lo.hi (3 bf16 MFMAs instead of 8 fp32 MFMAs per
+//     32x32x16 block; dropped lo.lo and the representation error give a
+//     relative error ~1e-5 per product -- fp32-class, far tighter than TF32);
+//   * the A operand can carry one extra column from a vector (the bias
+//     gradient of [Wg | bg], so the reference's torch.cat is never built);
+//   * the epilogue applies the eigenvalue scaling S (matrix dGdA or vectors
+//     dG, dA with damping) before the store, so V1 never round-trips.
+//
+// Tiling: 128x128 output tile per 256-thread block (4 waves in 2x2, 64x64
+// each = 2x2 MFMA 32x32 accumulators), BK = 32, operands register-staged and
+// split while being written to LDS; the LDS tile is double-buffered so the
+// split + store of k-tile kt+1 overlaps the MFMAs of k-tile kt (the split's
+// VALU work -- v_cvt_pk_bf16_f32 pairs -- is comparable to the MFMA time).  LDS layouts per operand:
+//   k-contiguous in memory ([m][k]): LDS [m][40] bf16, fragment = one
+//     ds_read_b128 (8 consecutive k) -- rows 80 B apart: conflict-free;
+//   m-contiguous in memory ([k][m]): LDS [k][160] bf16, fragment = two
+//     ds_read_b64_tr_b16 (transposing read).
+#include "common.h"
+#include "descs.h"
+
+namespace kfac {
+
+
+namespace {
+
+constexpr int GT = 128;   // output tile edge
+constexpr int GK = 32;    // k per LDS tile
+constexpr int GNT = 256;  // threads per block
+constexpr int LDK = 40;   // k-contig LDS row (32 + 8 pad) in shorts
+constexpr int LDM = 160;  // m-contig LDS row (128 + 32 pad) in shorts
+#ifndef GEMM3_CH
+#define GEMM3_CH 16
+#endif
+#ifndef GEMM3_GM
+#define GEMM3_GM 4
+#endif
+constexpr int CH = GEMM3_CH;  // consecutive tiles per XCD chunk
+constexpr int GM = GEMM3_GM;  // tile rows per column group (L2 reuse)
+
+// diagnostic builds only (tools/gemm3_bench.cpp): drop a phase to price it
+#ifndef GEMM3_DIAG
+#define GEMM3_DIAG 0  // 1: no global loads, 2: no LDS stores, 3: no MFMA
+#endif
+
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef short v8i16 __attribute__((ext_vector_type(8)));
+typedef __bf16 v8bf16 __attribute__((ext_vector_type(8)));
+typedef float v16f __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+
+__device__ __forceinline__ int find_tile_layer(const GemmDesc* d, int n, int t) {
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (d[mid].tile_start <= t) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f2_t __attribute__((ext_vector_type(2)));
+
+// x = hi + lo with hi = bf16_rn(x), lo = bf16_rn(x - hi): two
+// v_cvt_pk_bf16_f32 (RNE) + mask/shift/sub per pair of values
+__device__ __forceinline__ void split2(float x0, float x1, uint32_t& hi, uint32_t& lo) {
+  const f2_t x = {x0, x1};
+  hi = __builtin_bit_cast(uint32_t, __builtin_convertvector(x, bf16x2_t));
+  const float h0 = __uint_as_float(hi << 16);
+  const float h1 = __uint_as_float(hi & 0xFFFF0000u);
+  const f2_t r = {x0 - h0, x1 - h1};
+  lo = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, bf16x2_t));
+}
+
+__device__ __forceinline__ void split4(const float4 v, v4i16& hi, v4i16& lo) {
+  uint32_t h0, l0, h1, l1;
+  split2(v.x, v.y, h0, l0);
+  split2(v.z, v.w, h1, l1);
+  const uint2 hh = make_uint2(h0, h1), ll = make_uint2(l0, l1);
+  hi = __builtin_bit_cast(v4i16, hh);
+  lo = __builtin_bit_cast(v4i16, ll);
+}
+
+// one operand's staging registers: 4 float4 per thread per k-tile
+struct Stage {
+  float4 r[4];
+};
+
+// Pointers come out of the descriptor table, so the compiler cannot infer
+// their address space and would emit FLAT loads (which also count on
+// lgkmcnt and serialise against the LDS traffic): cast to global.
+typedef const float __attribute__((address_space(1)))* gptr_t;
+typedef float f4v_t __attribute__((ext_vector_type(4)));
+typedef const f4v_t __attribute__((address_space(1)))* gptr4_t;
+
+__device__ __forceinline__ float4 gload4(const float* p) {
+  const f4v_t v = *(gptr4_t)(p);
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ float gload(const float* p) {
+  return *(gptr_t)(p);
+}
+
+// k-contiguous operand: rows [r0, r0+128) of a [rows][ld] matrix, columns
+// [k0, k0+32).  Thread t: chunk = t & 7 (4 columns), row = (t >> 3) + 32p.
+// `full` (uniform per block and k-tile): the tile is interior and float4
+// loads are legal -> no per-element checks.
+__device__ __forceinline__ void load_kc(Stage& st, const float* __restrict__ P,
+                                        const float* __restrict__ extra,
+                                        int64_t ld, int rows, int r0,
+                                        int kmain, int k0, bool vec) {
+  const int t = threadIdx.x;
+  const int c = k0 + (t & 7) * 4;
+  const bool full = vec && (r0 + GT <= rows) && (k0 + GK <= kmain);
+  if (full) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int r = r0 + (t >> 3) + 32 * p;
+      st.r[p] = gload4(P + (int64_t)r * ld + c);
+    }
+    return;
+  }
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int r = r0 + (t >> 3) + 32 * p;
+    float tmp[4] = {0.f, 0.f, 0.f, 0.f};
+    if (r < rows) {
+      const float* row = P + (int64_t)r * ld;
+      if (vec && c + 3 < kmain) {
+        const float4 v = gload4(row + c);
+        tmp[0] = v.x; tmp[1] = v.y; tmp[2] = v.z; tmp[3] = v.w;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int k = c + e;
+          if (k < kmain) tmp[e] = gload(row + k);
+          else if (extra != nullptr && k == kmain) tmp[e] = gload(extra + r);
+        }
+      }
+    }
+    st.r[p] = make_float4(tmp[0], tmp[1], tmp[2], tmp[3]);
+  }
+}
+
+__device__ __forceinline__ void store_kc(const Stage& st, short* Lh, short* Ll) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int r = (t >> 3) + 32 * p;
+    v4i16 h, l;
+    split4(st.r[p], h, l);
+    *reinterpret_cast<v4i16*>(Lh + r * LDK + (t & 7) * 4) = h;
+    *reinterpret_cast<v4i16*>(Ll + r * LDK + (t & 7) * 4) = l;
+  }
+}
+
+// m-contiguous operand: k-rows [k0, k0+32) of a [K][ld] matrix, columns
+// [m0, m0+128).  Thread t: chunk = t & 31 (4 columns), krow = (t >> 5) + 8p.
+__device__ __forceinline__ void load_mc(Stage& st, const float* __restrict__ P,
+                                        int64_t ld, int cols, int m0, int K,
+                                        int k0, bool vec) {
+  const int t = threadIdx.x;
+  const int m = m0 + (t & 31) * 4;
+  const bool full = vec && (m0 + GT <= cols) && (k0 + GK <= K);
+  if (full) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int k = k0 + (t >> 5) + 8 * p;
+      st.r[p] = gload4(P + (int64_t)k * ld + m);
+    }
+    return;
+  }
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int k = k0 + (t >> 5) + 8 * p;
+    float tmp[4] = {0.f, 0.f, 0.f, 0.f};
+    if (k < K) {
+      const float* row = P + (int64_t)k * ld;
+      if (vec && m + 3 < cols) {
+        const float4 v = gload4(row + m);
+        tmp[0] = v.x; tmp[1] = v.y; tmp[2] = v.z; tmp[3] = v.w;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (m + e < cols) tmp[e] = gload(row + m + e);
+      }
+    }
+    st.r[p] = make_float4(tmp[0], tmp[1], tmp[2], tmp[3]);
+  }
+}
+
+__device__ __forceinline__ void store_mc(const Stage& st, short* Lh, short* Ll) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int k = (t >> 5) + 8 * p;
+    v4i16 h, l;
+    split4(st.r[p], h, l);
+    *reinterpret_cast<v4i16*>(Lh + k * LDM + (t & 31) * 4) = h;
+    *reinterpret_cast<v4i16*>(Ll + k * LDM + (t & 31) * 4) = l;
+  }
+}
+
+// fragment: lane l gets X[row = base + (l & 31)][k = kk + 8 (l >> 5) + 0..7]
+__device__ __forceinline__ v8bf16 frag_kc(const short* L, int base, int kk) {
+  const int l = threadIdx.x & 63;
+  const v8i16 v = *reinterpret_cast<const v8i16*>(L + (base + (l & 31)) * LDK + kk + 8 * (l >> 5));
+  return __builtin_bit_cast(v8bf16, v);
+}
+
+// fragment from a [k][m] LDS tile: lane l gets X[k = kk + 8h + j][m = base + (l & 31)]
+__device__ __forceinline__ v8bf16 frag_mc(const short* L, int base, int kk) {
+  const int l = threadIdx.x & 63;
+  const int g = l >> 4;
+  const int i = l & 15;
+  const int q = i >> 2, p = i & 3;
+  const int col = base + 16 * (g & 1) + 4 * p;
+  const int krow = kk + 8 * (g >> 1) + q;
+  const short* a0 = L + krow * LDM + col;
+  const short* a1 = a0 + 4 * LDM;
+  v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)a0);
+  v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)a1);
+  v8i16 c = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(v8bf16, c);
+}
+
+template <bool A_KC, bool B_KC>
+__global__ void __launch_bounds__(GNT, 2)
+gemm3_kernel(const GemmDesc* __restrict__ descs, int nlayers, int total_tiles) {
+  constexpr int A_SZ = A_KC ? GT * LDK : GK * LDM;
+  constexpr int B_SZ = B_KC ? GT * LDK : GK * LDM;
+  constexpr int BUF = 2 * A_SZ + 2 * B_SZ;
+  // double-buffered: the split + LDS store of k-tile kt+1 overlaps the
+  // MFMAs on k-tile kt; one barrier per k-tile
+  __shared__ __attribute__((aligned(16))) short lds[2 * BUF];
+
+  // XCD-aware chunked remap (see header)
+  const int b = blockIdx.x;
+  const int xcd = b & 7, r = b >> 3;
+  const int t = ((r / CH) * 8 + xcd) * CH + (r % CH);
+  if (t >= total_tiles) return;
+  const GemmDesc d = descs[find_tile_layer(descs, nlayers, t)];
+  // grouped order inside a layer: GM tile rows x one tile column, column
+  // after column, so a chunk of CH consecutive tiles covers a GM x CH/GM
+  // block of C whose A and B panels are shared in the XCD's L2
+  const int tl = t - d.tile_start;
+  const int tiles_m = (d.M + GT - 1) / GT;
+  const int per_group = GM * d.tiles_n;
+  const int first_m = (tl / per_group) * GM;
+  const int gm = min(tiles_m - first_m, GM);
+  const int in_group = tl % per_group;
+  const int m0 = (first_m + in_group % gm) * GT;
+  const int n0 = (in_group / gm) * GT;
+  const bool avec = d.vec & 1, bvec = (d.vec >> 1) & 1;
+
+  const int w = threadIdx.x >> 6;
+  const int l = threadIdx.x & 63;
+  const int wr = w >> 1, wc = w & 1;
+
+  v16f acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  // two register stages: the global loads of k-tile kt+2 are issued while
+  // k-tile kt is multiplied, so each load has two k-tiles of MFMA time
+  // (plus the co-resident block's) to land before it is split and stored
+  Stage sa0, sb0, sa1, sb1;
+  auto load = [&](Stage& sa, Stage& sb, int k0) {
+    if constexpr (GEMM3_DIAG == 1) {
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        sa.r[p] = make_float4(k0, 1.f, 2.f, 3.f);
+        sb.r[p] = make_float4(k0, 1.f, 2.f, 3.f);
+      }
+      return;
+    }
+    if constexpr (A_KC) load_kc(sa, d.A, d.A_extra, d.lda, d.M, m0, d.Kmain, k0, avec);
+    else load_mc(sa, d.A, d.lda, d.M, m0, d.K, k0, avec);
+    if constexpr (B_KC) load_kc(sb, d.B, nullptr, d.ldb, d.N, n0, d.K, k0, bvec);
+    else load_mc(sb, d.B, d.ldb, d.N, n0, d.K, k0, bvec);
+  };
+  auto store = [&](const Stage& sa, const Stage& sb, short* buf) {
+    if constexpr (GEMM3_DIAG == 2) {
+      if (sa.r[0].x == 12345.f && sb.r[3].w == 54321.f) buf[threadIdx.x] = 1;
+      return;
+    }
+    if constexpr (A_KC) store_kc(sa, buf, buf + A_SZ);
+    else store_mc(sa, buf, buf + A_SZ);
+    if constexpr (B_KC) store_kc(sb, buf + 2 * A_SZ, buf + 2 * A_SZ + B_SZ);
+    else store_mc(sb, buf + 2 * A_SZ, buf + 2 * A_SZ + B_SZ);
+  };
+  auto compute = [&](const short* cur) {
+    const short* Ah = cur;
+    const short* Al = cur + A_SZ;
+    const short* Bh = cur + 2 * A_SZ;
+    const short* Bl = cur + 2 * A_SZ + B_SZ;
+#pragma unroll
+    for (int kk = 0; kk < GK; kk += 16) {
+      v8bf16 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int am = wr * 64 + i * 32;
+        const int bn = wc * 64 + i * 32;
+        if constexpr (A_KC) {
+          ah[i] = frag_kc(Ah, am, kk);
+          al[i] = frag_kc(Al, am, kk);
+        } else {
+          ah[i] = frag_mc(Ah, am, kk);
+          al[i] = frag_mc(Al, am, kk);
+        }
+        if constexpr (B_KC) {
+          bh[i] = frag_kc(Bh, bn, kk);
+          bl[i] = frag_kc(Bl, bn, kk);
+        } else {
+          bh[i] = frag_mc(Bh, bn, kk);
+          bl[i] = frag_mc(Bl, bn, kk);
+        }
+      }
+      if constexpr (GEMM3_DIAG == 3) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          acc[i][i][0] += (float)(ah[i][0] + al[i][1] + bh[i][2] + bl[i][3]);
+        continue;
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        }
+    }
+  };
+  // iteration kt: LDS buf[kt&1] holds tile kt, stage (kt+1)&1 holds tile
+  // kt+1 (in flight), stage kt&1 is free for tile kt+2
+  auto step = [&](int kt, int nt, Stage& fa, Stage& fb, Stage& na, Stage& nb) {
+    if (kt + 2 < nt) load(fa, fb, (kt + 2) * GK);
+    compute(lds + (kt & 1) * BUF);
+    if (kt + 1 < nt) store(na, nb, lds + ((kt + 1) & 1) * BUF);
+    __syncthreads();
+  };
+
+  const int ntiles = (d.K + GK - 1) / GK;
+  load(sa0, sb0, 0);
+  if (ntiles > 1) load(sa1, sb1, GK);
+  store(sa0, sb0, lds);
+  __syncthreads();
+  for (int kt = 0; kt < ntiles; kt += 2) {
+    step(kt, ntiles, sa0, sb0, sa1, sb1);
+    if (kt + 1 < ntiles) step(kt + 1, ntiles, sa1, sb1, sa0, sb0);
+  }
+
+  // epilogue: C/D layout col = lane & 31, row = (reg&3) + 8 (reg>>2) + 4 (lane>>5)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + wc * 64 + j * 32 + (l & 31);
+      if (n >= d.N) continue;
+      const float dan = d.da != nullptr ? gload(d.da + n) : 0.f;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int m = m0 + wr * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (l >> 5);
+        if (m >= d.M) continue;
+        float v = acc[i][j][e];
+        if (d.S != nullptr) v *= gload(d.S + (int64_t)m * d.lds + n);
+        else if (d.dg != nullptr) v = v / (gload(d.dg + m) * dan + d.damping);
+        *(float __attribute__((address_space(1)))*)(d.C + (int64_t)m * d.ldc + n) = v;
+      }
+    }
+  }
+}
+
+}  // namespace
+
+int gemm3_grid(int total_tiles) {
+  const int per = 8 * CH;
+  return ((total_tiles + per - 1) / per) * per;
+}
+
+void gemm3_grouped(const GemmDesc* table, int nlayers, int total_tiles,
+                   bool a_kc, bool b_kc, hipStream_t s) {
+  if (nlayers <= 0 || total_tiles <= 0) return;
+  const dim3 grid((unsigned)gemm3_grid(total_tiles));
+  if (a_kc && b_kc) gemm3_kernel<true, true><<<grid, dim3(GNT), 0, s>>>(table, nlayers, total_tiles);
+  else if (a_kc) gemm3_kernel<true, false><<<grid, dim3(GNT), 0, s>>>(table, nlayers, total_tiles);
+  else if (b_kc) gemm3_kernel<false, true><<<grid, dim3(GNT), 0, s>>>(table, nlayers, total_tiles);
+  else gemm3_kernel<false, false><<<grid, dim3(GNT), 0, s>>>(table, nlayers, total_tiles);
+}
+
+}  // namespace kfac

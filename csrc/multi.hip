@@ -13,17 +13,10 @@
 // kl_clip and lr are read from a small device array so the launches can be
 // captured in a HIP graph and replayed with new hyperparameters.
 #include "common.h"
+#include "descs.h"
 
 namespace kfac {
 
-struct LayerDesc {
-  const float* p;   // preconditioned grad [rows, cols], row stride ldp
-  void* w;          // weight grad [rows, wcols] contiguous
-  void* b;          // bias grad [rows] or null
-  int64_t rows, cols, ldp, wcols;
-  int64_t block_start;  // first block of this layer
-  int32_t wdt, bdt;     // dtype tags
-};
 
 namespace {
 

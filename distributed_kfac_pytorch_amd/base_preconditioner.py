@@ -182,14 +182,22 @@ class StepGraphs:
             if not bcast and not pre._multi_apply.prepare(layers, kl, lr, use_buffers=True):
                 return False
             damping = pre.damping
+            if pre._grouped is None:
+                pre._grouped = pops.GroupedPrecondition()
+            # grouped MFMA GEMMs (4 launches for all layers); tables are built
+            # here, outside the capture
+            grouped = pre._grouped.prepare(workers, damping)
             g = torch.cuda.CUDAGraph()
             side = torch.cuda.Stream()
             side.wait_stream(torch.cuda.current_stream())
-            lanes = self._lanes(workers)
+            lanes = [] if grouped else self._lanes(workers)
             with torch.cuda.stream(side):
                 with torch.cuda.graph(g, stream=side):
-                    # fork: independent per-layer GEMM chains run as parallel
-                    # graph branches (small layers cannot fill 256 CUs alone)
+                    if grouped:
+                        pre._grouped.launch()
+                    # otherwise fork: independent per-layer GEMM chains run as
+                    # parallel graph branches (small layers cannot fill 256
+                    # CUs alone)
                     for lane, members in zip(self._streams(len(lanes)), lanes):
                         lane.wait_stream(side)
                         with torch.cuda.stream(lane):
@@ -308,6 +316,7 @@ class BaseKFACPreconditioner:
         self._kl_acc: torch.Tensor | None = None
         self._kl_scale: torch.Tensor | None = None
         self._multi_apply: Any = None
+        self._grouped: Any = None
         self._graphs: Any = None
         if os.environ.get('KFAC_GRAPHS', '1') != '0':
             self._graphs = StepGraphs()
@@ -539,8 +548,14 @@ class BaseKFACPreconditioner:
         """Precondition this rank's layers; broadcast results if needed."""
         damping = self.damping
         bcast = self._assignment.broadcast_gradients()
+        workers = [l for n, l in ordered if self._assignment.is_grad_worker(n)]
+        grouped = False
+        if workers and workers[0].module.device.type == 'cuda':
+            if self._grouped is None:
+                self._grouped = pops.GroupedPrecondition()
+            grouped = self._grouped.run(workers, damping)
         for name, layer in ordered:
-            if self._assignment.is_grad_worker(name):
+            if not grouped and self._assignment.is_grad_worker(name):
                 layer.preconditioned_grad(damping=damping)
             if bcast:
                 layer.broadcast_grad(

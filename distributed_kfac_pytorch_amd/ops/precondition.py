@@ -1,9 +1,11 @@
-"""Gradient-preconditioning epilogues and the device-side KL clip (K-HIP-7).
+"""Gradient preconditioning (K-HIP-4) and the device-side KL clip (K-HIP-7).
 
-The GEMM chain ``QG^T [Wg | bg] QA -> scale -> QG (.) QA^T`` runs on
-hipBLASLt through ``torch.mm(..., out=)`` into per-layer persistent buffers
-(plain library GEMMs); everything between and after the GEMMs is a native
-kernel here, so a K-FAC step performs no host synchronisation:
+The GEMM chain ``QG^T [Wg | bg] QA -> scale -> QG (.) QA^T`` of every layer
+runs as four grouped bf16x3 MFMA launches (``GroupedPrecondition``,
+csrc/gemm3.hip) on CUDA; the per-layer ``torch.mm(..., out=)`` chain is the
+fallback (CPU, ``KFAC_PRECOND_GEMM=torch``, unsupported layer types).
+Everything between and after the GEMMs is a native kernel here, so a K-FAC
+step performs no host synchronisation:
 
 * ``eigen_scale_(v, dgda=..)`` / ``(v, dg=.., da=.., damping=..)``:
   ``v *= dgda`` or ``v /= outer(dg, da) + damping`` in place.
@@ -17,6 +19,8 @@ kernel here, so a K-FAC step performs no host synchronisation:
 from __future__ import annotations
 
 import math
+import os
+from typing import Any
 
 import torch
 
@@ -230,4 +234,158 @@ class MultiLayerApply:
         self.launch(kl_clip is not None)
         for layer in layers:
             layer.grad = None
+        return True
+
+
+def grouped_gemm_enabled() -> bool:
+    """``KFAC_PRECOND_GEMM=torch`` keeps the per-layer hipBLASLt fp32 chain;
+    the default is the grouped bf16x3 MFMA kernel (csrc/gemm3.hip)."""
+    return os.environ.get('KFAC_PRECOND_GEMM', 'bf16x3').lower() != 'torch'
+
+
+class GroupedPrecondition:
+    """All layers' preconditioning GEMM chains in four grouped launches.
+
+    Eigen layers (reference ``kfac/layers/eigen.py:349-384``)::
+
+        T1: t1 = [Wg | bg] QA          (bias column read from bg in place)
+        T2: t2 = (QG^T t1) (.) S       (S = dGdA, or 1/(dG (x) dA + damping))
+        T3: t1 = QG t2
+        T4: P  = t1 QA^T               (P = the layer's persistent grad buffer)
+
+    Inverse layers (``kfac/layers/inverse.py:214-233``) use T1 with
+    ``A^-1`` and write ``P = G^-1 t1`` in T3.  Each launch covers every
+    layer (csrc/gemm3.hip), so a ResNet-50 step issues 4 GEMM launches
+    instead of ~220.  Tables are cached on the operand addresses (all
+    persistent between second-order updates).
+    """
+
+    def __init__(self) -> None:
+        self._key: tuple | None = None
+        self._tables: list = []
+
+    @staticmethod
+    def _operands(layer: Any) -> tuple | None:
+        from distributed_kfac_pytorch_amd.layers.eigen import KFACEigenLayer
+        from distributed_kfac_pytorch_amd.layers.inverse import KFACInverseLayer
+
+        # only the stock layer math: subclasses that override the
+        # preconditioning (embedding, tensor-parallel NeoX) keep their path
+        if type(layer).preconditioned_grad not in (
+            KFACEigenLayer.preconditioned_grad, KFACInverseLayer.preconditioned_grad,
+        ):
+            return None
+        helper = layer.module
+        wg = helper.get_weight_grad()
+        if wg is None or not wg.is_cuda or wg.dtype != torch.float32:
+            return None
+        wm = helper.weight_grad_matrix()
+        if not (wm.is_contiguous() and wm.data_ptr() == wg.data_ptr()):
+            return None
+        bg = helper.get_bias_grad() if helper.has_bias() else None
+        if bg is not None and (bg.dtype != torch.float32 or not bg.is_contiguous()):
+            return None
+        if isinstance(layer, KFACEigenLayer):
+            qa, qg = layer.qa, layer.qg
+            if qa is None or qg is None or qa.dtype != torch.float32 or qg.dtype != torch.float32:
+                return None
+            if layer.prediv_eigenvalues:
+                if layer.dgda is None or layer.dgda.dtype != torch.float32:
+                    return None
+            elif layer.dg is None or layer.da is None:
+                return None
+            return ('eigen', wm, bg, qa, qg)
+        if isinstance(layer, KFACInverseLayer):
+            a_inv, g_inv = layer.a_inv, layer.g_inv
+            if a_inv is None or g_inv is None or a_inv.dtype != torch.float32 \
+                    or g_inv.dtype != torch.float32:
+                return None
+            # (F + damping I)^-1 is symmetric: a column-major result (e.g.
+            # from cholesky_inverse) is used through its transpose
+            a_inv = a_inv if a_inv.stride(1) == 1 else a_inv.t()
+            g_inv = g_inv if g_inv.stride(1) == 1 else g_inv.t()
+            if a_inv.stride(1) != 1 or g_inv.stride(1) != 1:
+                return None
+            return ('inverse', wm, bg, a_inv, g_inv)
+        return None
+
+    def prepare(self, layers: list, damping: float) -> bool:
+        lib = native()
+        if lib is None or not layers or not grouped_gemm_enabled():
+            return False
+        ops = []
+        for layer in layers:
+            o = self._operands(layer)
+            if o is None:
+                return False
+            ops.append(o)
+        t = [[] for _ in range(4)]  # per table: list of operand tuples
+        key = [damping]
+        for layer, (kind, wm, bg, fa, fg) in zip(layers, ops):
+            g, a = fg.shape[0], fa.shape[0]
+            dev = fa.device
+            t1 = layer._buf('_tmp1', (g, a), torch.float32, dev) if kind == 'eigen' \
+                else self._inv_tmp(layer, (g, a), dev)
+            out = layer._grad_buffer(dev)
+            if tuple(out.shape) != (g, a):
+                return False
+            key.append((kind, wm.data_ptr(), None if bg is None else bg.data_ptr(),
+                        fa.data_ptr(), fg.data_ptr(), t1.data_ptr(), out.data_ptr(), g, a))
+            # T1: [Wg | bg] @ QA  (or A^-1)
+            t[0].append((wm, bg, fa, t1, None, None, None, 0.0))
+            if kind == 'eigen':
+                t2 = layer._buf('_tmp2', (g, a), torch.float32, dev)
+                key.append((t2.data_ptr(), layer.prediv_eigenvalues,
+                            None if layer.dgda is None else layer.dgda.data_ptr(),
+                            None if layer.dg is None else layer.dg.data_ptr(),
+                            None if layer.da is None else layer.da.data_ptr()))
+                if layer.prediv_eigenvalues:
+                    t[1].append((fg, None, t1, t2, layer.dgda, None, None, 0.0))
+                else:
+                    t[1].append((fg, None, t1, t2, None, layer.dg, layer.da, float(damping)))
+                t[2].append((fg, None, t2, t1, None, None, None, 0.0))
+                t[3].append((t1, None, fa, out, None, None, None, 0.0))
+            else:
+                t[2].append((fg, None, t1, out, None, None, None, 0.0))
+        key_t = tuple(key)
+        if key_t != self._key:
+            flags = [(True, False), (False, False), (True, False), (True, True)]
+            tables = []
+            for rows, (akc, bkc) in zip(t, flags):
+                if not rows:
+                    tables.append(None)
+                    continue
+                cols = list(zip(*rows))
+                tab, tiles = lib.build_gemm_table(
+                    list(cols[0]), list(cols[1]), list(cols[2]), list(cols[3]),
+                    list(cols[4]), list(cols[5]), list(cols[6]), list(cols[7]), akc, bkc,
+                )
+                tables.append((tab, len(rows), tiles, akc, bkc))
+            self._tables = tables
+            self._key = key_t
+        self._layers = layers
+        return True
+
+    @staticmethod
+    def _inv_tmp(layer: Any, shape: tuple[int, int], dev: torch.device) -> torch.Tensor:
+        t = getattr(layer, '_gtmp', None)
+        if t is None or tuple(t.shape) != shape or t.device != dev:
+            t = torch.empty(shape, dtype=torch.float32, device=dev)
+            layer._gtmp = t
+        return t
+
+    def launch(self) -> None:
+        lib = native()
+        for entry in self._tables:
+            if entry is not None:
+                tab, n, tiles, akc, bkc = entry
+                lib.gemm3_grouped(tab, n, tiles, akc, bkc)
+
+    def run(self, layers: list, damping: float) -> bool:
+        """prepare + launch; sets each layer's ``grad`` to its buffer."""
+        if not self.prepare(layers, damping):
+            return False
+        self.launch()
+        for layer in layers:
+            layer.grad = layer._grad_buf
         return True
