@@ -36,11 +36,12 @@ from distributed_kfac_pytorch_amd import tracing  # noqa: E402
 from distributed_kfac_pytorch_amd.models.resnet import get_model  # noqa: E402
 
 # The reference publishes no number.  Measured on MI355X: the
-# upstream kfac_pytorch package, same config, 1 GPU (it cannot run
-# channels_last weights, so NCHW): 728.91 img/s (profiles/
-# bench_reference_impl_mi355x_1gpu.json).  For N GPUs the comparison point is
-# the reference's linear-scaling upper bound N * 728.91.
-REFERENCE_IMG_S_PER_GPU = 728.91
+# upstream kfac_pytorch package, same config and harness (MIOpen find,
+# foreach SGD), 1 GPU (it cannot run channels_last weights, so NCHW):
+# 729.89 img/s (profiles/bench_reference_impl_mi355x_1gpu_r1b.json; 728.91
+# in the first measurement).  For N GPUs the comparison point is the
+# reference's linear-scaling upper bound N * 729.89.
+REFERENCE_IMG_S_PER_GPU = 729.89
 
 
 def parse_args() -> argparse.Namespace:
