@@ -26,6 +26,16 @@ import os
 import sys
 import time
 
+# MIOpen tuning database shipped with the repo (miopen_db/, built by
+# tools/gpu_tune_miopen.sh with MIOpen find over this benchmark's
+# convolutions, channels_last and NCHW): with cudnn.benchmark off, MIOpen's
+# immediate mode picks the recorded fastest solution for every conv instead
+# of re-running a noisy find in each process.  Must be set before MIOpen
+# initialises; an explicit MIOPEN_USER_DB_PATH wins.
+_MIOPEN_DB = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'miopen_db')
+if os.path.isdir(_MIOPEN_DB):
+    os.environ.setdefault('MIOPEN_USER_DB_PATH', _MIOPEN_DB)
+
 import torch
 import torch.distributed as dist
 
@@ -36,12 +46,13 @@ from distributed_kfac_pytorch_amd import tracing  # noqa: E402
 from distributed_kfac_pytorch_amd.models.resnet import get_model  # noqa: E402
 
 # The reference publishes no number.  Measured on MI355X: the
-# upstream kfac_pytorch package, same config and harness (MIOpen find,
-# foreach SGD), 1 GPU (it cannot run channels_last weights, so NCHW):
-# 729.89 img/s (profiles/bench_reference_impl_mi355x_1gpu_r1b.json; 728.91
-# in the first measurement).  For N GPUs the comparison point is the
-# reference's linear-scaling upper bound N * 729.89.
-REFERENCE_IMG_S_PER_GPU = 729.89
+# upstream kfac_pytorch package, same config and harness (shipped MIOpen
+# db, foreach SGD, zero_grad(set_to_none=True)), 1 GPU (it cannot run
+# channels_last weights, so NCHW): 753.96 img/s
+# (profiles/bench_reference_impl_mi355x_1gpu_r1c.json; 728.91 and 729.89
+# under the earlier harness settings).  For N GPUs the comparison point is
+# the reference's linear-scaling upper bound N * 753.96.
+REFERENCE_IMG_S_PER_GPU = 753.96
 
 
 def parse_args() -> argparse.Namespace:
@@ -66,8 +77,12 @@ def parse_args() -> argparse.Namespace:
     p.add_argument('--no-channels-last', action='store_true')
     p.add_argument('--fp32', action='store_true', help='disable bf16 autocast')
     p.add_argument('--phase-timing', action='store_true')
-    p.add_argument('--cudnn-benchmark', type=int, default=1,
-                   help='MIOpen find (benchmark mode) for the model convolutions')
+    p.add_argument('--grad-set-to-none', type=int, default=1,
+                   help='zero_grad(set_to_none=...): 1 lets autograd hand its gradient '
+                        'buffers to .grad (no accumulate kernels)')
+    p.add_argument('--cudnn-benchmark', type=int, default=0,
+                   help='1: MIOpen find in every process (noisy); 0: immediate mode '
+                        'with the shipped tuning db (miopen_db/)')
     p.add_argument('--profile-mark', action='store_true',
                    help='bracket the timed steps with marker kernels (rocprof windows)')
     p.add_argument('--lr', type=float, default=0.0125)
@@ -165,7 +180,7 @@ def run(args: argparse.Namespace, use_kfac: bool, rank: int, world: int,
     amp = not args.fp32
 
     def step() -> None:
-        opt.zero_grad(set_to_none=False)
+        opt.zero_grad(set_to_none=bool(args.grad_set_to_none))
         with torch.autocast('cuda', dtype=torch.bfloat16, enabled=amp):
             loss = crit(model(x), y)
         loss.backward()
@@ -203,6 +218,10 @@ def run(args: argparse.Namespace, use_kfac: bool, rank: int, world: int,
     if precond is not None and args.impl == 'native':
         out['kfac_layers'] = len(precond._layers)
         out['kfac_steps_end'] = precond.steps
+        g = getattr(precond, '_graphs', None)
+        if g is not None:
+            out['graph_replays'] = g.replays
+            out['graph_captures'] = g.captures
         mem = precond.memory_usage()
         out['kfac_memory_mb'] = round(mem['total'] / 1e6, 1)
     del model, opt, precond

@@ -332,6 +332,7 @@ std::tuple<at::Tensor, int64_t> build_layer_table(
     const int64_t rows = p.size(0), cols = p.size(1);
     const int64_t wcols = cols - (hb ? 1 : 0);
     TORCH_CHECK(w.numel() == rows * wcols, "layer ", i, ": weight grad size");
+    TORCH_CHECK(rows * cols < (int64_t(1) << 31), "layer ", i, ": too many elements for the multi-tensor kernels");
     kfac::LayerDesc d{};
     d.p = p.data_ptr<float>();
     d.w = w.data_ptr();
@@ -364,7 +365,8 @@ std::tuple<at::Tensor, int64_t> build_layer_table(
 
 void kl_dot_multi(const at::Tensor& table, int64_t nlayers,
                   int64_t total_blocks, at::Tensor& acc) {
-  TORCH_CHECK(acc.scalar_type() == at::kDouble);
+  TORCH_CHECK(acc.scalar_type() == at::kDouble && acc.numel() == 256 && acc.is_contiguous(),
+              "kl_dot_multi: acc must be 256 contiguous fp64 partial sums");
   c10::hip::HIPGuardMasqueradingAsCUDA g(acc.device());
   kfac::kl_dot_multi((const kfac::LayerDesc*)table.data_ptr(), (int)nlayers,
                      total_blocks, acc.data_ptr<double>(), cur_stream());
@@ -372,7 +374,7 @@ void kl_dot_multi(const at::Tensor& table, int64_t nlayers,
 
 void kl_finalize_dev(at::Tensor& acc, const at::Tensor& params,
                      at::Tensor& scale) {
-  TORCH_CHECK(acc.scalar_type() == at::kDouble &&
+  TORCH_CHECK(acc.scalar_type() == at::kDouble && acc.numel() == 256 &&
               params.scalar_type() == at::kFloat &&
               scale.scalar_type() == at::kFloat);
   c10::hip::HIPGuardMasqueradingAsCUDA g(acc.device());
@@ -520,7 +522,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("kl_dot_multi", &kl_dot_multi);
   m.def("kl_finalize_dev", &kl_finalize_dev);
   m.def("apply_multi", &apply_multi);
-  m.def("rocsolver_eigh", &rocsolver_eigh, py::arg("A"), py::arg("algo") = 0,
+  // GIL released: several host threads can each drive rocSOLVER on their
+  // own stream (rocSOLVER's syevd blocks its calling thread internally)
+  m.def("rocsolver_eigh", &rocsolver_eigh, py::call_guard<py::gil_scoped_release>(),
+        py::arg("A"), py::arg("algo") = 0,
         py::arg("max_sweeps") = 100, py::arg("tol") = 1e-7);
   m.def("build_gemm_table", &build_gemm_table);
   m.def("gemm3_grouped", &gemm3_grouped);

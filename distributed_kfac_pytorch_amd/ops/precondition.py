@@ -156,7 +156,7 @@ class MultiLayerApply:
 
     def _buffers(self, device: torch.device) -> None:
         if self._acc is None or self._acc.device != device:
-            self._acc = torch.zeros(1, dtype=torch.float64, device=device)
+            self._acc = torch.zeros(256, dtype=torch.float64, device=device)  # KL partial sums
             self._scale = torch.ones(1, dtype=torch.float32, device=device)
             self._params = torch.zeros(2, dtype=torch.float32, device=device)
             self._param_vals = None
