@@ -22,6 +22,8 @@ MI355X-specific behaviour:
 """
 from __future__ import annotations
 
+import os
+
 from typing import Callable
 
 import torch
@@ -252,7 +254,7 @@ class KFACBaseLayer:
         self.a_factor = self._allreduce()(
             self.a_factor,
             average=True,
-            symmetric=self.symmetric_factors and self.symmetry_aware,
+            symmetric=self._pack_factors(),
             group=group,
         )
 
@@ -263,9 +265,26 @@ class KFACBaseLayer:
         self.g_factor = self._allreduce()(
             self.g_factor,
             average=True,
-            symmetric=self.symmetric_factors and self.symmetry_aware,
+            symmetric=self._pack_factors(),
             group=group,
         )
+
+    def _pack_factors(self) -> bool:
+        """Reduce only the upper triangle of the factors.
+
+        The reference packs only with ``symmetry_aware=True``
+        (``kfac/layers/base.py:281-335``).  Here the factors are exactly
+        symmetric by construction (the SYRK kernel writes the lower triangle
+        as the mirror; the CPU path symmetrises), so reducing the triangle and
+        mirroring gives bit-identical results with half the bytes on the
+        wire -- done whenever the module's factors are symmetric
+        (``KFAC_PACK_FACTORS=0`` restores the reference behaviour).
+        """
+        if not self.symmetric_factors:
+            return False
+        if os.environ.get('KFAC_PACK_FACTORS', '1') == '0':
+            return self.symmetry_aware
+        return True
 
     def reset_batch(self) -> None:
         self._a_batch = None
