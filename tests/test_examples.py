@@ -105,3 +105,13 @@ def test_language_model_cli(nproc):
                   '--register-embeddings', '--skip-layers', 'decoder', 'self_attn',
                   '--strategy', 'mem_opt', '--backend', 'gloo', '--no-cuda'], nproc)
     assert [line['epoch'] for line in lines] == [1, 2]
+
+
+def test_gpt_neox_cli_tp(tmp_path):
+    lines = _run(['examples/torch_gpt_neox.py', '--mp', '2', '--steps', '4', '--seq-len', '16',
+                  '--micro-batch', '2', '--factor-update-steps', '1', '--inv-update-steps', '2',
+                  '--log-interval', '2', '--no-cuda', '--backend', 'gloo',
+                  '--factor-checkpoint-dir', str(tmp_path)], nproc=4)
+    assert [line['step'] for line in lines if 'step' in line] == [2, 4]
+    assert lines[-1]['tokens_per_s'] > 0
+    assert len(list(tmp_path.iterdir())) == 8  # one factor file per TP layer
