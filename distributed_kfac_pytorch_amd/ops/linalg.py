@@ -19,13 +19,17 @@ degenerate eigenspaces); K-FAC only uses them through ``Q f(D) Q^T``, which
 is invariant to that freedom.
 
 Environment knobs: ``KFAC_EIGH`` = auto | torch | syevd | syevj | syevdj
-(force one algorithm for n > 64), ``KFAC_EIGH_STREAMS`` (default 4),
+(force one algorithm for n > 64), ``KFAC_EIGH_STREAMS`` (lanes, default 8),
+``KFAC_EIGH_THREADS`` (0: issue every lane from the calling thread),
+``KFAC_EIGH_SPLIT_N`` (factors at least this large are solved one per job),
 ``KFAC_JACOBI_SWEEPS`` / ``KFAC_JACOBI_TOL`` (small-n kernel).
 """
 from __future__ import annotations
 
+import logging
 import os
 from collections import defaultdict
+from typing import Any
 
 import torch
 
@@ -39,6 +43,7 @@ _ALGOS = {'syevd': 0, 'syevj': 1, 'syevdj': 2}
 # largest n sent to the LDS Jacobi kernel (its hard limit is jacobi_max_n())
 JACOBI_MAX_N = int(os.environ.get('KFAC_JACOBI_MAX_N', '64'))
 
+logger = logging.getLogger(__name__)
 _streams: list[torch.cuda.Stream] = []
 
 
@@ -48,7 +53,7 @@ def jacobi_max_n() -> int:
 
 
 def _side_streams(device: torch.device) -> list[torch.cuda.Stream]:
-    n = int(os.environ.get('KFAC_EIGH_STREAMS', '4'))
+    n = int(os.environ.get('KFAC_EIGH_STREAMS', '8'))
     global _streams
     if len(_streams) < n or _streams[0].device != device:
         _streams = [torch.cuda.Stream(device=device) for _ in range(n)]
@@ -108,31 +113,98 @@ def eigh_many(
                 for k, i in enumerate(idxs):
                     out[i] = (evals[k], evecs[k])
         else:
-            main = torch.cuda.current_stream(dev)
-            ready = torch.cuda.Event()
-            ready.record(main)
-            streams = _side_streams(dev)
-            # longest buckets first, round-robin over the side streams
-            order = sorted(gpu, key=lambda kv: -_bucket_cost(kv[0][0], len(kv[1])))
-            loads = [0.0] * len(streams)
-            results = {}
-            for key, idxs in order:
-                j = loads.index(min(loads))
-                loads[j] += _bucket_cost(key[0], len(idxs))
-                s = streams[j]
-                s.wait_event(ready)
-                with torch.cuda.stream(s):
-                    results[key] = _gpu_bucket(stacks[key])
-            for s in streams:
-                main.wait_stream(s)
-            for key, idxs in gpu:
-                evals, evecs = results[key]
-                for k, i in enumerate(idxs):
-                    out[i] = (evals[k], evecs[k])
-                # tensors produced on side streams are consumed on main
-                evals.record_stream(main)
-                evecs.record_stream(main)
+            for i, r in _launch_jobs(gpu, stacks, dev).items():
+                out[i] = r
     return [o for o in out if o is not None]
+
+
+def _jobs(gpu: list) -> list[tuple[tuple, list[int], int, int]]:
+    """Split the size buckets into solver jobs ``(key, idxs, lo, hi)``.
+    By default every bucket is one batched call: rocSOLVER's strided-batched
+    kernels cover all matrices of a bucket per launch, which measured faster
+    than one job per matrix even with threaded lanes (ResNet-50 mix on
+    MI355X: 410 ms batched vs 564 ms split at n >= 1024, 8 lanes).  Factors
+    with n >= ``KFAC_EIGH_SPLIT_N`` become one job each."""
+    split_n = int(os.environ.get('KFAC_EIGH_SPLIT_N', '1000000'))
+    jobs = []
+    for key, idxs in gpu:
+        if key[0] >= split_n and key[0] > JACOBI_MAX_N:
+            jobs += [(key, idxs, k, k + 1) for k in range(len(idxs))]
+        else:
+            jobs.append((key, idxs, 0, len(idxs)))
+    return jobs
+
+
+def _run_lane(stream: torch.cuda.Stream, jobs: list, stacks: dict) -> list:
+    with torch.cuda.stream(stream):
+        return [_gpu_bucket(stacks[key][lo:hi]) for key, _, lo, hi in jobs]
+
+
+def _launch_jobs(
+    gpu: list,
+    stacks: dict,
+    dev: torch.device,
+) -> dict[int, tuple[torch.Tensor, torch.Tensor]]:
+    """Run the solver jobs on ``KFAC_EIGH_STREAMS`` lanes (LPT on n^3), one
+    host thread per lane, and join the lanes back into the current stream.
+
+    rocSOLVER's syevd is a one-stage tridiagonalisation that issues ~5 tiny
+    kernels per column (~22k launches and ~110 ms of dependent small kernels
+    for n = 4608: profiles/rocprof_eigh4608_syevd_stats.csv).  Issued from
+    one thread the call is bound by host enqueue rate, so buckets on
+    different streams barely overlap (ResNet-50 mix: 4 streams 530 ms vs 1
+    stream 573 ms).  The native call releases the GIL, so one thread per
+    lane enqueues the independent chains concurrently and the GPU runs them
+    side by side (same mix: 410 ms with 8 threaded lanes vs 506-516 ms from
+    one thread; tools/eigh_lanes_probe.py).  (rocSOLVER's syevd cannot be captured into a HIP graph:
+    it fails with rocblas_status_internal_error under stream capture.)
+    """
+    main = torch.cuda.current_stream(dev)
+    ready = torch.cuda.Event()
+    ready.record(main)
+    streams = _side_streams(dev)
+    jobs = sorted(_jobs(gpu), key=lambda j: -_bucket_cost(j[0][0], j[3] - j[2]))
+    lanes: list[list] = [[] for _ in streams]
+    loads = [0.0] * len(streams)
+    for job in jobs:
+        k = loads.index(min(loads))
+        loads[k] += _bucket_cost(job[0][0], job[3] - job[2])
+        lanes[k].append(job)
+    active = [(s, ln) for s, ln in zip(streams, lanes) if ln]
+    for s, _ in active:
+        s.wait_event(ready)
+    if len(active) > 1 and _threads_enabled():
+        pool = _executor(len(active))
+        futs = [pool.submit(_run_lane, s, ln, stacks) for s, ln in active]
+        results = [f.result() for f in futs]
+    else:
+        results = [_run_lane(s, ln, stacks) for s, ln in active]
+    out: dict[int, tuple[torch.Tensor, torch.Tensor]] = {}
+    for (s, ln), res in zip(active, results):
+        main.wait_stream(s)
+        for (key, idxs, lo, hi), (evals, evecs) in zip(ln, res):
+            # produced on a lane stream, consumed on the main stream
+            evals.record_stream(main)
+            evecs.record_stream(main)
+            for k in range(hi - lo):
+                out[idxs[lo + k]] = (evals[k], evecs[k])
+    return out
+
+
+def _threads_enabled() -> bool:
+    return os.environ.get('KFAC_EIGH_THREADS', '1') != '0'
+
+
+_pool: Any = None
+
+
+def _executor(n: int) -> Any:
+    global _pool
+    if _pool is None or _pool._max_workers < n:
+        from concurrent.futures import ThreadPoolExecutor
+
+        _pool = ThreadPoolExecutor(max_workers=n, thread_name_prefix='kfac-eigh')
+    return _pool
 
 
 def eigh(mat: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
