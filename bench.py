@@ -43,6 +43,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 import distributed_kfac_pytorch_amd as kfac  # noqa: E402
 from distributed_kfac_pytorch_amd import tracing  # noqa: E402
+from distributed_kfac_pytorch_amd.graphs import GraphedTrainStep  # noqa: E402
 from distributed_kfac_pytorch_amd.models.resnet import get_model  # noqa: E402
 
 # The reference publishes no number.  Measured on MI355X: the
@@ -80,6 +81,11 @@ def parse_args() -> argparse.Namespace:
     p.add_argument('--grad-set-to-none', type=int, default=1,
                    help='zero_grad(set_to_none=...): 1 lets autograd hand its gradient '
                         'buffers to .grad (no accumulate kernels)')
+    p.add_argument('--graphs', type=int, default=1,
+                   help='1: replay each step kind from a captured HIP graph '
+                        '(distributed_kfac_pytorch_amd.graphs.GraphedTrainStep; '
+                        'single-rank jobs only, second-order update steps stay '
+                        'eager); 0: every step eager')
     p.add_argument('--cudnn-benchmark', type=int, default=0,
                    help='1: MIOpen find in every process (noisy); 0: immediate mode '
                         'with the shipped tuning db (miopen_db/)')
@@ -179,11 +185,26 @@ def run(args: argparse.Namespace, use_kfac: bool, rank: int, world: int,
     crit = torch.nn.CrossEntropyLoss(label_smoothing=0.1)
     amp = not args.fp32
 
-    def step() -> None:
-        opt.zero_grad(set_to_none=bool(args.grad_set_to_none))
-        with torch.autocast('cuda', dtype=torch.bfloat16, enabled=amp):
+    use_graphs = bool(args.graphs) and args.impl == 'native' and world == 1
+
+    def forward_backward() -> torch.Tensor:
+        # no autocast weight cache: it cannot be replayed from a graph
+        with torch.autocast('cuda', dtype=torch.bfloat16, enabled=amp,
+                            cache_enabled=not use_graphs):
             loss = crit(model(x), y)
         loss.backward()
+        return loss
+
+    runner = None
+    if use_graphs:
+        runner = GraphedTrainStep(forward_backward, opt, precond)
+
+    def step() -> None:
+        if runner is not None:
+            runner()
+            return
+        opt.zero_grad(set_to_none=bool(args.grad_set_to_none))
+        forward_backward()
         if precond is not None:
             precond.step()
         opt.step()
@@ -215,6 +236,9 @@ def run(args: argparse.Namespace, use_kfac: bool, rank: int, world: int,
         }
         out['phase_counts'] = timer.counts()
         tracing.enable_phase_timing(False)
+    if runner is not None:
+        out['step_graphs'] = {'replays': runner.replays, 'captures': runner.captures,
+                              'eager_steps': runner.eager_steps}
     if precond is not None and args.impl == 'native':
         out['kfac_layers'] = len(precond._layers)
         out['kfac_steps_end'] = precond.steps
@@ -280,7 +304,9 @@ def main() -> None:
         line['kfac_overhead_ms'] = round(
             res['ms_per_step'] - base['ms_per_step'], 3,
         )
-    for k in ('phase_ms_per_step', 'phase_counts', 'kfac_layers',
+    if base is not None and 'step_graphs' in base:
+        line['sgd_step_graphs'] = base['step_graphs']
+    for k in ('phase_ms_per_step', 'phase_counts', 'kfac_layers', 'step_graphs',
               'kfac_memory_mb', 'kfac_steps_end'):
         if k in res:
             line[k] = res[k]

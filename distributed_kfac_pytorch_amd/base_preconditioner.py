@@ -164,6 +164,10 @@ class StepGraphs:
             return False
         if ordered[0][1].module.device.type != 'cuda':
             return False
+        if torch.cuda.is_current_stream_capturing():
+            # inside a whole-step capture (graphs.GraphedTrainStep): the
+            # eager launches are recorded into the outer graph
+            return False
         bcast = pre._assignment.broadcast_gradients()
         key = self._key(pre, ordered, bcast)
         if key is None:

@@ -103,16 +103,17 @@ def eigh_many(
             out[i] = (evals[k], evecs[k])
     if gpu:
         dev = gpu[0][0][1]
-        stacks = {
-            key: torch.stack([mats[i].to(torch.float32) for i in idxs])
-            for key, idxs in gpu
-        }
-        if not use_native(*stacks.values()):
+        if not use_native(*[mats[idxs[0]] for _, idxs in gpu]):
             for key, idxs in gpu:
-                evals, evecs = torch.linalg.eigh(stacks[key])
+                evals, evecs = torch.linalg.eigh(
+                    torch.stack([mats[i].to(torch.float32) for i in idxs]))
                 for k, i in enumerate(idxs):
                     out[i] = (evals[k], evecs[k])
         else:
+            stacks = {
+                key: torch.stack([mats[i].to(torch.float32) for i in idxs])
+                for key, idxs in gpu
+            }
             for i, r in _launch_jobs(gpu, stacks, dev).items():
                 out[i] = r
     return [o for o in out if o is not None]
@@ -155,9 +156,18 @@ def _launch_jobs(
     different streams barely overlap (ResNet-50 mix: 4 streams 530 ms vs 1
     stream 573 ms).  The native call releases the GIL, so one thread per
     lane enqueues the independent chains concurrently and the GPU runs them
-    side by side (same mix: 410 ms with 8 threaded lanes vs 506-516 ms from
-    one thread; tools/eigh_lanes_probe.py).  (rocSOLVER's syevd cannot be captured into a HIP graph:
-    it fails with rocblas_status_internal_error under stream capture.)
+    side by side.  Measured on the ResNet-50 mix (tools/eigh_lanes_probe.py,
+    profiles/eigh_lanes_mi355x.jsonl): 410 ms with 8 threaded lanes vs
+    506-516 ms from one thread on one box, 412 vs 419 ms on another -- the
+    floor is the 3 x 4608 bucket alone (242 ms).
+
+    HIP graphs do not remove this bound: syevd fails under stream capture
+    (it synchronises the host internally), and its stages captured one by
+    one (sytrd, then stedc + ormtr; possible only with rocBLAS's hipBLASLt
+    backend disabled) replay no faster than they run eagerly (3 x 4608:
+    sytrd 165 ms eager / 169 ms replayed; profiles/
+    eigh_rocsolver_stages_capture.jsonl) -- the reduction is a chain of
+    dependent tiny kernels on the GPU as well.
     """
     main = torch.cuda.current_stream(dev)
     ready = torch.cuda.Event()

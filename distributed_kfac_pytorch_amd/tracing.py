@@ -173,9 +173,12 @@ def phase_timer() -> PhaseTimer | None:
 
 @contextlib.contextmanager
 def phase(name: str) -> Iterator[None]:
-    """Record a K-FAC phase on the global timer (no-op when disabled)."""
+    """Record a K-FAC phase on the global timer (no-op when disabled, and
+    while a HIP graph is being captured: event timing is not capturable)."""
     timer = _PHASE_TIMER
-    if timer is None:
+    if timer is None or (
+        torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+    ):
         yield
     else:
         with timer.phase(name):

@@ -128,6 +128,26 @@ def test_eigh_many_mixed_sizes(cuda):
         assert (recon - m).abs().max().item() < 1e-4 * m.abs().max().item()
 
 
+def test_eigh_many_rocsolver_sizes(cuda):
+    """Mixed mid-size factors through the threaded rocSOLVER lanes: the
+    eigenpairs must match a float64 reference."""
+    torch.manual_seed(3)
+    mats = []
+    for n in (512, 480, 440, 300, 260, 1024, 900):
+        x = torch.randn(n, 2 * n, device=cuda)
+        mats.append(x @ x.t() / (2 * n) + 1e-3 * torch.eye(n, device=cuda))
+    res = linalg.eigh_many(mats)
+    for m, (d, q) in zip(mats, res):
+        n = m.shape[0]
+        assert d.shape == (n,) and q.shape == (n, n)
+        ref = torch.linalg.eigvalsh(m.double())
+        assert (d.double() - ref).abs().max().item() < 1e-5 * ref.abs().max().item()
+        recon = q @ torch.diag(d) @ q.t()
+        assert (recon - m).abs().max().item() < 1e-5 * m.abs().max().item()
+        eye = torch.eye(n, device=cuda)
+        assert (q.t() @ q - eye).abs().max().item() < 1e-4
+
+
 def test_precondition_epilogues(cuda):
     g, a = 48, 97
     v = torch.randn(g, a, device=cuda)

@@ -44,8 +44,8 @@ def main() -> None:
         s = make(n, cnt, dev)
         mats += [s[i].contiguous() for i in range(cnt)]
     ref = [torch.linalg.eigvalsh(m.double()) for m in mats]
-    configs = [('0', '4', '100000'), ('1', '4', '100000'), ('1', '8', '100000'),
-               ('1', '13', '100000'), ('1', '6', '100000'), ('0', '4', '100000')]
+    configs = [('1', '8', '100000'), ('0', '8', '100000'),
+               ('1', '4', '100000'), ('1', '8', '1024')]
     for threads, streams, split in configs:
         os.environ['KFAC_EIGH_THREADS'] = threads
         os.environ['KFAC_EIGH_STREAMS'] = streams
