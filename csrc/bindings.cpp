@@ -315,9 +315,40 @@ std::vector<at::Tensor> jacobi_eigh(const at::Tensor& A, int64_t max_sweeps,
 // Build the device descriptor table for a list of layers.  Returns
 // (table [uint8 on device], total_blocks).  The caller caches the table
 // while the tensors' storages are unchanged.
-std::tuple<at::Tensor, int64_t> build_layer_table(
+// Upload a host-built descriptor table.  `host` is an optional pinned byte
+// buffer owned by the caller (preallocated outside any HIP-graph capture);
+// the copy is a plain hipMemcpyAsync on the current stream, so when the
+// table is built inside a capture it becomes a graph node that re-reads
+// `host` on every replay.  Without `host` a pinned staging tensor is
+// allocated here (not possible while capturing).
+std::tuple<at::Tensor, at::Tensor> upload_table(
+    const void* data, int64_t nbytes, const at::Device& device,
+    const c10::optional<at::Tensor>& host) {
+  at::Tensor cpu;
+  if (host.has_value() && host->numel() >= nbytes) {
+    cpu = *host;
+    TORCH_CHECK(cpu.is_pinned() && cpu.scalar_type() == at::kByte && cpu.is_contiguous(),
+                "table staging must be a pinned contiguous byte tensor");
+  } else {
+    cpu = at::empty({std::max<int64_t>(nbytes, 1)},
+                    at::TensorOptions().dtype(at::kByte).pinned_memory(true));
+  }
+  std::memcpy(cpu.data_ptr(), data, nbytes);
+  auto dev_t = at::empty({std::max<int64_t>(nbytes, 1)},
+                         at::TensorOptions().dtype(at::kByte).device(device));
+  C10_HIP_CHECK(hipMemcpyAsync(dev_t.data_ptr(), cpu.data_ptr(), nbytes,
+                               hipMemcpyHostToDevice, cur_stream()));
+  return {dev_t, cpu};
+}
+
+// Returns (device table, block count, pinned host staging).  The host copy
+// is returned so the caller keeps it alive: when the table is built inside a
+// HIP-graph capture the H2D copy becomes a graph node that re-reads it on
+// every replay.
+std::tuple<at::Tensor, int64_t, at::Tensor> build_layer_table(
     const std::vector<at::Tensor>& ps, const std::vector<at::Tensor>& ws,
-    const std::vector<c10::optional<at::Tensor>>& bs) {
+    const std::vector<c10::optional<at::Tensor>>& bs,
+    const c10::optional<at::Tensor>& host_buf) {
   TORCH_CHECK(ps.size() == ws.size() && ps.size() == bs.size());
   std::vector<kfac::LayerDesc> host(ps.size());
   int64_t blocks = 0;
@@ -353,14 +384,11 @@ std::tuple<at::Tensor, int64_t> build_layer_table(
     host[i] = d;
   }
   const int64_t nbytes = (int64_t)(host.size() * sizeof(kfac::LayerDesc));
-  at::Tensor dev_t;
+  at::Tensor dev_t, cpu;
   if (!ps.empty()) {
-    auto cpu = at::empty({std::max<int64_t>(nbytes, 1)},
-                         at::TensorOptions().dtype(at::kByte).pinned_memory(true));
-    std::memcpy(cpu.data_ptr(), host.data(), nbytes);
-    dev_t = cpu.to(ps[0].device(), /*non_blocking=*/true);
+    std::tie(dev_t, cpu) = upload_table(host.data(), nbytes, ps[0].device(), host_buf);
   }
-  return {dev_t, blocks};
+  return {dev_t, blocks, cpu};
 }
 
 void kl_dot_multi(const at::Tensor& table, int64_t nlayers,
@@ -411,14 +439,17 @@ bool vec_ok(const at::Tensor& t) {
 //   b_kc: Bs[i] is the stored [N, K] (logical B = Bs^T), else [K, N].
 // Optional epilogue scale: Ss[i] [M, N] or dgs[i] [M] with das[i] [N].
 // Layers are sorted by K (descending) so long tiles are dispatched first.
-std::tuple<at::Tensor, int64_t> build_gemm_table(
+// Returns (device table, tile count, pinned host staging) -- see
+// build_layer_table for why the host copy is returned.
+std::tuple<at::Tensor, int64_t, at::Tensor> build_gemm_table(
     const std::vector<at::Tensor>& As,
     const std::vector<c10::optional<at::Tensor>>& A_extras,
     const std::vector<at::Tensor>& Bs, const std::vector<at::Tensor>& Cs,
     const std::vector<c10::optional<at::Tensor>>& Ss,
     const std::vector<c10::optional<at::Tensor>>& dgs,
     const std::vector<c10::optional<at::Tensor>>& das,
-    const std::vector<double>& dampings, bool a_kc, bool b_kc) {
+    const std::vector<double>& dampings, bool a_kc, bool b_kc,
+    const c10::optional<at::Tensor>& host_buf) {
   const size_t n = As.size();
   TORCH_CHECK(A_extras.size() == n && Bs.size() == n && Cs.size() == n &&
               Ss.size() == n && dgs.size() == n && das.size() == n &&
@@ -480,14 +511,12 @@ std::tuple<at::Tensor, int64_t> build_gemm_table(
     tiles += (int64_t)((d.M + 127) / 128) * d.tiles_n;
   }
   TORCH_CHECK(tiles < (1LL << 30));
-  at::Tensor dev_t;
+  at::Tensor dev_t, cpu;
   if (n > 0) {
     const int64_t nbytes = (int64_t)(n * sizeof(kfac::GemmDesc));
-    auto cpu = at::empty({nbytes}, at::TensorOptions().dtype(at::kByte).pinned_memory(true));
-    std::memcpy(cpu.data_ptr(), host.data(), nbytes);
-    dev_t = cpu.to(Cs[0].device(), /*non_blocking=*/true);
+    std::tie(dev_t, cpu) = upload_table(host.data(), nbytes, Cs[0].device(), host_buf);
   }
-  return {dev_t, tiles};
+  return {dev_t, tiles, cpu};
 }
 
 void gemm3_grouped(const at::Tensor& table, int64_t nlayers, int64_t total_tiles,
@@ -518,7 +547,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fill_identity", &fill_identity);
   m.def("jacobi_eigh", &jacobi_eigh);
   m.def("jacobi_max_n", &kfac::jacobi_max_n);
-  m.def("build_layer_table", &build_layer_table);
+  m.def("build_layer_table", &build_layer_table, py::arg("ps"), py::arg("ws"),
+        py::arg("bs"), py::arg("host") = py::none());
   m.def("kl_dot_multi", &kl_dot_multi);
   m.def("kl_finalize_dev", &kl_finalize_dev);
   m.def("apply_multi", &apply_multi);
@@ -527,7 +557,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rocsolver_eigh", &rocsolver_eigh, py::call_guard<py::gil_scoped_release>(),
         py::arg("A"), py::arg("algo") = 0,
         py::arg("max_sweeps") = 100, py::arg("tol") = 1e-7);
-  m.def("build_gemm_table", &build_gemm_table);
+  m.def("build_gemm_table", &build_gemm_table, py::arg("As"), py::arg("A_extras"),
+        py::arg("Bs"), py::arg("Cs"), py::arg("Ss"), py::arg("dgs"), py::arg("das"),
+        py::arg("dampings"), py::arg("a_kc"), py::arg("b_kc"),
+        py::arg("host") = py::none());
   m.def("gemm3_grouped", &gemm3_grouped);
   m.attr("arch") = "gfx950";
 }

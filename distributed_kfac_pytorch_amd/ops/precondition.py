@@ -133,6 +133,61 @@ def apply_grad_(
         wgrad.copy_(src.reshape(rows, -1).reshape(wgrad.shape))
 
 
+class _TableCache:
+    """Small LRU of device descriptor tables keyed by operand addresses,
+    with the pinned host staging buffers they are uploaded from.
+
+    A table built inside a HIP-graph capture (``graphs.GraphedTrainStep``:
+    the captured backward produces gradients at new addresses) is uploaded
+    by a captured H2D copy that re-reads its staging buffer on every replay,
+    so each entry owns its staging buffers until evicted.  Pinned memory
+    cannot be allocated while a capture is running, so the buffers are
+    allocated the first time they are needed outside a capture and recycled
+    after that.  Each captured step kind keeps its own entry; the size bound
+    only stops eager training with fresh gradient tensors every step from
+    growing the cache.
+    """
+
+    SLOT_BYTES = 1 << 16  # >= 500 layers of descriptors per table
+
+    def __init__(self, size: int = 8, slots_per_entry: int = 1) -> None:
+        self.size = size
+        self.per = slots_per_entry
+        self._d: dict = {}
+        self._free: list[torch.Tensor] = []
+
+    def get(self, key: tuple) -> Any:
+        v = self._d.pop(key, None)
+        if v is not None:
+            self._d[key] = v
+            return v[0]
+        return None
+
+    def reserve(self) -> list[torch.Tensor | None]:
+        """Staging buffers for one new entry (None: let the builder
+        allocate, which is only possible outside a capture)."""
+        while len(self._d) >= self.size:
+            _, (_, slots) = self._pop_oldest()
+            self._free += [t for t in slots if t is not None]
+        capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+        if not capturing and torch.cuda.is_available():
+            # top up so that a later capture never has to allocate
+            while len(self._free) < self.per * self.size:
+                self._free.append(torch.empty(self.SLOT_BYTES, dtype=torch.uint8, pin_memory=True))
+        out: list[torch.Tensor | None] = []
+        for _ in range(self.per):
+            out.append(self._free.pop() if self._free else None)
+        return out
+
+    def _pop_oldest(self) -> tuple:
+        k = next(iter(self._d))
+        return k, self._d.pop(k)
+
+    def put(self, key: tuple, value: Any, slots: list) -> Any:
+        self._d[key] = (value, slots)
+        return value
+
+
 class MultiLayerApply:
     """KL clip + gradient write for all layers in three native launches.
 
@@ -148,6 +203,7 @@ class MultiLayerApply:
         self._key: tuple | None = None
         self._table: torch.Tensor | None = None
         self._blocks = 0
+        self._tables = _TableCache(slots_per_entry=1)
         self._acc: torch.Tensor | None = None
         self._scale: torch.Tensor | None = None
         self._params: torch.Tensor | None = None
@@ -205,7 +261,12 @@ class MultiLayerApply:
             ))
         key_t = tuple(key)
         if key_t != self._key:
-            self._table, self._blocks = lib.build_layer_table(ps, ws, bs)
+            entry = self._tables.get(key_t)
+            if entry is None:
+                slots = self._tables.reserve()
+                entry = self._tables.put(
+                    key_t, lib.build_layer_table(ps, ws, bs, slots[0]), slots)
+            self._table, self._blocks, _ = entry
             self._key = key_t
         self._n = len(ps)
         self._buffers(ps[0].device)
@@ -263,6 +324,7 @@ class GroupedPrecondition:
     def __init__(self) -> None:
         self._key: tuple | None = None
         self._tables: list = []
+        self._cache = _TableCache(slots_per_entry=4)
 
     @staticmethod
     def _operands(layer: Any) -> tuple | None:
@@ -349,18 +411,23 @@ class GroupedPrecondition:
                 t[2].append((fg, None, t1, out, None, None, None, 0.0))
         key_t = tuple(key)
         if key_t != self._key:
-            flags = [(True, False), (False, False), (True, False), (True, True)]
-            tables = []
-            for rows, (akc, bkc) in zip(t, flags):
-                if not rows:
-                    tables.append(None)
-                    continue
-                cols = list(zip(*rows))
-                tab, tiles = lib.build_gemm_table(
-                    list(cols[0]), list(cols[1]), list(cols[2]), list(cols[3]),
-                    list(cols[4]), list(cols[5]), list(cols[6]), list(cols[7]), akc, bkc,
-                )
-                tables.append((tab, len(rows), tiles, akc, bkc))
+            tables = self._cache.get(key_t)
+            if tables is None:
+                flags = [(True, False), (False, False), (True, False), (True, True)]
+                slots = self._cache.reserve()
+                tables = []
+                for rows, (akc, bkc), slot in zip(t, flags, slots):
+                    if not rows:
+                        tables.append(None)
+                        continue
+                    cols = list(zip(*rows))
+                    tab, tiles, host = lib.build_gemm_table(
+                        list(cols[0]), list(cols[1]), list(cols[2]), list(cols[3]),
+                        list(cols[4]), list(cols[5]), list(cols[6]), list(cols[7]), akc, bkc,
+                        slot,
+                    )
+                    tables.append((tab, len(rows), tiles, akc, bkc, host))
+                self._cache.put(key_t, tables, slots)
             self._tables = tables
             self._key = key_t
         self._layers = layers
@@ -378,7 +445,7 @@ class GroupedPrecondition:
         lib = native()
         for entry in self._tables:
             if entry is not None:
-                tab, n, tiles, akc, bkc = entry
+                tab, n, tiles, akc, bkc, _ = entry
                 lib.gemm3_grouped(tab, n, tiles, akc, bkc)
 
     def run(self, layers: list, damping: float) -> bool:

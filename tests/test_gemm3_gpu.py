@@ -59,7 +59,7 @@ def test_grouped_gemm_layouts(cuda, a_kc, b_kc):
         dgs.append(dg)
         das.append(da)
         damps.append(damp)
-    table, tiles = lib.build_gemm_table(As, extras, Bs, Cs, Ss, dgs, das, damps, a_kc, b_kc)
+    table, tiles, _ = lib.build_gemm_table(As, extras, Bs, Cs, Ss, dgs, das, damps, a_kc, b_kc)
     lib.gemm3_grouped(table, len(As), tiles, a_kc, b_kc)
     torch.cuda.synchronize()
     for (m, n, k), C, ref in zip(SHAPES, Cs, refs):
@@ -77,7 +77,7 @@ def test_grouped_gemm_strided_operands(cuda):
     A = base_a[:, :129]      # lda 133
     B = base_b[:129, :77]    # ldb 90 (n-contig)
     C = torch.empty(70, 77, device=cuda)
-    table, tiles = lib.build_gemm_table([A], [None], [B], [C], [None], [None], [None], [0.0],
+    table, tiles, _ = lib.build_gemm_table([A], [None], [B], [C], [None], [None], [None], [0.0],
                                         True, False)
     lib.gemm3_grouped(table, 1, tiles, True, False)
     ref = A.double() @ B.double()

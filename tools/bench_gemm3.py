@@ -43,7 +43,7 @@ def main() -> None:
     tabs = []
     for rows, (akc, bkc) in zip(T, flags):
         cols = list(zip(*rows))
-        tab, tiles = lib.build_gemm_table(*[list(c) for c in cols], akc, bkc)
+        tab, tiles, _ = lib.build_gemm_table(*[list(c) for c in cols], akc, bkc)
         tabs.append((tab, len(rows), tiles, akc, bkc))
 
     def run(i: int | None = None) -> None:

@@ -45,7 +45,7 @@ def main() -> None:
         mats += [s[i].contiguous() for i in range(cnt)]
     ref = [torch.linalg.eigvalsh(m.double()) for m in mats]
     configs = [('1', '8', '100000'), ('0', '8', '100000'),
-               ('1', '4', '100000'), ('1', '8', '1024')]
+               ('1', '8', '4608'), ('1', '12', '4608'), ('1', '12', '2304')]
     for threads, streams, split in configs:
         os.environ['KFAC_EIGH_THREADS'] = threads
         os.environ['KFAC_EIGH_STREAMS'] = streams

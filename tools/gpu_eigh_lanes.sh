@@ -1,4 +1,4 @@
-# eigh threaded-lane probe (tools/eigh_lanes_probe.py) + eigh GPU tests
+# eigh threaded-lane probe (tools/eigh_lanes_probe.py)
 set -o pipefail
 R="$GRAFT_REPO_ROOT"
 mkdir -p "$R/gpurun_out"
