@@ -27,7 +27,7 @@ void scale_copy(int dtype, const void* src, void* dst, int64_t n, float scale,
 int64_t syrk_workspace_splits(int64_t N, int64_t D);
 void syrk(int in_dtype, const void* x, int64_t N, int64_t K, int64_t ldx,
           bool bias, float* C, int64_t D, int64_t ldc, float alpha,
-          float beta, int splits, hipStream_t s);
+          float beta, int splits, hipStream_t s, const ConvGeom* geom = nullptr);
 // im2col.hip
 void im2col_nhwc(int dtype, const void* x, int64_t B, int64_t H, int64_t W,
                  int64_t C, int64_t sB, int64_t sH, int64_t sW, int kh, int kw,
@@ -159,6 +159,43 @@ void syrk(const at::Tensor& x, at::Tensor& C, bool bias, double alpha,
   kfac::syrk(dtype_tag(x), x.data_ptr(), N, K, ldx, bias,
              C.data_ptr<float>(), D, C.stride(0), (float)alpha, (float)beta,
              sp, cur_stream());
+}
+
+// C[D,D] = beta*C + alpha * P^T P with P the (implicit) patch matrix of an
+// NHWC conv input x [B, C, H, W] (channels_last strides), columns in natural
+// (kh, kw, c) order, plus the bias ones column.  The patches are read from x
+// inside the SYRK tile loader (K-HIP-2: no im2col buffer).
+void syrk_conv(const at::Tensor& x, at::Tensor& C, int64_t kh, int64_t kw,
+               int64_t sh, int64_t sw, int64_t ph, int64_t pw, bool bias,
+               double alpha, double beta, int64_t splits) {
+  check_cuda(x, "x");
+  check_cuda(C, "C");
+  TORCH_CHECK(x.dim() == 4, "x must be [B, C, H, W]");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat,
+              "syrk_conv input must be bf16 or fp32");
+  const int64_t B = x.size(0), Cin = x.size(1), H = x.size(2), W = x.size(3);
+  const int64_t vec = x.scalar_type() == at::kFloat ? 4 : 8;  // elements per 16 B
+  TORCH_CHECK(x.stride(1) == 1, "syrk_conv needs channels_last input (channel stride 1)");
+  TORCH_CHECK(Cin % vec == 0 && x.stride(0) % vec == 0 && x.stride(2) % vec == 0 &&
+                  x.stride(3) % vec == 0 &&
+                  (reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0,
+              "syrk_conv: channel count and strides must allow 16-byte loads");
+  TORCH_CHECK(C.scalar_type() == at::kFloat && C.dim() == 2 && C.size(0) == C.size(1) &&
+              C.stride(1) == 1, "syrk_conv output must be fp32 square, unit column stride");
+  const int64_t OH = (H + 2 * ph - kh) / sh + 1, OW = (W + 2 * pw - kw) / sw + 1;
+  TORCH_CHECK(OH > 0 && OW > 0, "syrk_conv: empty output");
+  const int64_t K = Cin * kh * kw;
+  const int64_t D = K + (bias ? 1 : 0);
+  TORCH_CHECK(C.size(0) == D, "C must be [C*kh*kw + bias]^2");
+  const int64_t N = B * OH * OW;
+  TORCH_CHECK(H < (1 << 30) && W < (1 << 30) && OH * OW < (1LL << 31));
+  kfac::ConvGeom g{x.stride(0), x.stride(2), x.stride(3), (int32_t)H, (int32_t)W,
+                   (int32_t)Cin, (int32_t)kw, (int32_t)sh, (int32_t)sw,
+                   (int32_t)ph, (int32_t)pw, (int32_t)OH, (int32_t)OW};
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  int sp = splits > 0 ? (int)splits : (int)kfac::syrk_workspace_splits(N, D);
+  kfac::syrk(dtype_tag(x), x.data_ptr(), N, K, /*ldx=*/K, bias, C.data_ptr<float>(), D,
+             C.stride(0), (float)alpha, (float)beta, sp, cur_stream(), &g);
 }
 
 // --------------------------------------------------------------- im2col
@@ -539,6 +576,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("syrk", &syrk, py::arg("x"), py::arg("C"), py::arg("bias"),
         py::arg("alpha"), py::arg("beta"), py::arg("splits") = 0);
   m.def("syrk_default_splits", &kfac::syrk_workspace_splits);
+  m.def("syrk_conv", &syrk_conv, py::arg("x"), py::arg("C"), py::arg("kh"), py::arg("kw"),
+        py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("bias"),
+        py::arg("alpha"), py::arg("beta"), py::arg("splits") = 0);
   m.def("im2col", &im2col);
   m.def("eigen_scale", &eigen_scale);
   m.def("kl_dot", &kl_dot);

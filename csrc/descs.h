@@ -31,4 +31,12 @@ struct GemmDesc {
   int32_t vec;  // bit0: A float4 loads ok, bit1: B float4 loads ok
 };
 
+// syrk.hip implicit-im2col mode: the SYRK input rows are the patches of an
+// NHWC conv input, columns in natural (kh, kw, c) order, read straight from
+// the activation (the patch matrix is never materialised)
+struct ConvGeom {
+  int64_t sB, sH, sW;  // element strides of the input (channel stride 1)
+  int32_t H, W, C, kw, sh, sw, ph, pw, OH, OW;
+};
+
 }  // namespace kfac

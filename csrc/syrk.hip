@@ -22,6 +22,7 @@
 // (8 consecutive k per lane) come from ds_read_b64_tr_b16 (bf16) or plain
 // ds_read_b32 (fp32, v_mfma_f32_32x32x2_f32: exact fp32 products).
 #include "common.h"
+#include "descs.h"
 
 namespace kfac {
 
@@ -173,6 +174,174 @@ struct Staging<float> {
   }
 };
 
+// ---- implicit im2col (K-HIP-2).  A patch row r = (b, oh, ow) and a column
+// chunk at k = (i*kw + j)*C + c (C % chunk == 0, so a chunk never straddles
+// two taps) read the 16 contiguous bytes at x[b, oh*sh-ph+i, ow*sw-pw+j,
+// c..] (zeros outside the image).  Column decode is done once per block.
+struct ColTap {
+  int c, i, j;
+  int bias_chunk;  // 1: the chunk lies at/after column K (bias column / pad)
+  int64_t col;
+};
+
+__device__ __forceinline__ ColTap decode_col(int64_t col, int64_t K, const ConvGeom& g) {
+  ColTap t;
+  t.col = col;
+  if (col >= K) {
+    t.bias_chunk = 1;
+    t.c = t.i = t.j = 0;
+    return t;
+  }
+  const int tap = (int)(col / g.C);
+  t.c = (int)(col - (int64_t)tap * g.C);
+  t.i = tap / g.kw;
+  t.j = tap - t.i * g.kw;
+  t.bias_chunk = 0;
+  return t;
+}
+
+// row -> (b, oh*sh - ph, ow*sw - pw); b < 0 marks a row past the end
+struct RowPos {
+  int64_t b;
+  int ih0, iw0;
+};
+
+__device__ __forceinline__ RowPos decode_row(int64_t row, int64_t row_end, const ConvGeom& g) {
+  RowPos p;
+  if (row >= row_end) {
+    p.b = -1;
+    p.ih0 = p.iw0 = 0;
+    return p;
+  }
+  const int64_t ohw = (int64_t)g.OH * g.OW;
+  p.b = row / ohw;
+  const int rem = (int)(row - p.b * ohw);
+  const int oh = rem / g.OW;
+  const int ow = rem - oh * g.OW;
+  p.ih0 = oh * g.sh - g.ph;
+  p.iw0 = ow * g.sw - g.pw;
+  return p;
+}
+
+// element offset of a chunk, or -1 when it is zero (padding / past the end)
+__device__ __forceinline__ int64_t patch_offset(const RowPos& p, const ColTap& t, const ConvGeom& g) {
+  if (p.b < 0 || t.bias_chunk) return -1;
+  const int ih = p.ih0 + t.i, iw = p.iw0 + t.j;
+  if (ih < 0 || ih >= g.H || iw < 0 || iw >= g.W) return -1;
+  return p.b * g.sB + (int64_t)ih * g.sH + (int64_t)iw * g.sW + t.c;
+}
+
+template <typename TIn>
+struct PatchStaging;
+
+template <>
+struct PatchStaging<bf16_t> {
+  v8i16 r[2][2];
+  ColTap ti, tj;
+
+  __device__ __forceinline__ void init(int64_t c0i, int64_t c0j, int64_t K, const ConvGeom& g) {
+    const int chunk = threadIdx.x & 15;
+    ti = decode_col(c0i + chunk * 8, K, g);
+    tj = decode_col(c0j + chunk * 8, K, g);
+  }
+
+  __device__ __forceinline__ static v8i16 chunk_of(const uint16_t* X, const RowPos& p,
+                                                   const ColTap& t, const ConvGeom& g,
+                                                   int64_t K, bool bias) {
+    v8i16 v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = 0;
+    if (p.b >= 0 && t.bias_chunk) {
+      if (bias && t.col == K) v[0] = (short)0x3F80;  // bf16(1.0)
+      return v;
+    }
+    const int64_t off = patch_offset(p, t, g);
+    if (off >= 0) v = *reinterpret_cast<const v8i16*>(X + off);
+    return v;
+  }
+
+  __device__ __forceinline__ void load(const void* Xv, int64_t, int64_t n0, int64_t row_end,
+                                       int64_t K, bool bias, bool, int64_t, int64_t,
+                                       bool diag, const ConvGeom& g) {
+    const uint16_t* X = (const uint16_t*)Xv;
+    const int rloc = threadIdx.x >> 4;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const RowPos pos = decode_row(n0 + rloc + 16 * p, row_end, g);
+      r[0][p] = chunk_of(X, pos, ti, g, K, bias);
+      if (!diag) r[1][p] = chunk_of(X, pos, tj, g, K, bias);
+    }
+  }
+
+  __device__ __forceinline__ void store(short* Li, short* Lj, bool diag) {
+    const int t = threadIdx.x;
+    const int chunk = t & 15, rloc = t >> 4;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      *reinterpret_cast<v8i16*>(Li + (rloc + 16 * p) * LDS_W16 + chunk * 8) = r[0][p];
+      if (!diag)
+        *reinterpret_cast<v8i16*>(Lj + (rloc + 16 * p) * LDS_W16 + chunk * 8) = r[1][p];
+    }
+  }
+};
+
+template <>
+struct PatchStaging<float> {
+  float4 r[2][4];
+  ColTap ti, tj;
+
+  __device__ __forceinline__ void init(int64_t c0i, int64_t c0j, int64_t K, const ConvGeom& g) {
+    const int chunk = threadIdx.x & 31;
+    ti = decode_col(c0i + chunk * 4, K, g);
+    tj = decode_col(c0j + chunk * 4, K, g);
+  }
+
+  __device__ __forceinline__ static float4 chunk_of(const float* X, const RowPos& p,
+                                                    const ColTap& t, const ConvGeom& g,
+                                                    int64_t K, bool bias) {
+    if (p.b >= 0 && t.bias_chunk)
+      return make_float4((bias && t.col == K) ? 1.f : 0.f, 0.f, 0.f, 0.f);
+    const int64_t off = patch_offset(p, t, g);
+    if (off >= 0) return *reinterpret_cast<const float4*>(X + off);
+    return make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+
+  __device__ __forceinline__ void load(const void* Xv, int64_t, int64_t n0, int64_t row_end,
+                                       int64_t K, bool bias, bool, int64_t, int64_t,
+                                       bool diag, const ConvGeom& g) {
+    const float* X = (const float*)Xv;
+    const int rloc = threadIdx.x >> 5;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const RowPos pos = decode_row(n0 + rloc + 8 * p, row_end, g);
+      r[0][p] = chunk_of(X, pos, ti, g, K, bias);
+      if (!diag) r[1][p] = chunk_of(X, pos, tj, g, K, bias);
+    }
+  }
+
+  __device__ __forceinline__ void store(float* Li, float* Lj, bool diag) {
+    const int t = threadIdx.x;
+    const int chunk = t & 31, rloc = t >> 5;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      *reinterpret_cast<float4*>(Li + (rloc + 8 * p) * LDS_W32 + chunk * 4) = r[0][p];
+      if (!diag)
+        *reinterpret_cast<float4*>(Lj + (rloc + 8 * p) * LDS_W32 + chunk * 4) = r[1][p];
+    }
+  }
+};
+
+// dense mode: the existing Staging with the common load signature
+template <typename TIn>
+struct DenseStaging : Staging<TIn> {
+  __device__ __forceinline__ void init(int64_t, int64_t, int64_t, const ConvGeom&) {}
+  __device__ __forceinline__ void load(const void* X, int64_t ldx, int64_t n0, int64_t row_end,
+                                       int64_t K, bool bias, bool vec_ok, int64_t c0i,
+                                       int64_t c0j, bool diag, const ConvGeom&) {
+    Staging<TIn>::load(X, ldx, n0, row_end, K, bias, vec_ok, c0i, c0j, diag);
+  }
+};
+
 // bf16 operand fragment for a 32-wide column block `cb` at k offset `kk`:
 // lane l gets X[k = kk + 8h + j][col = cb + (l & 31)], j = 0..7, h = l >> 5,
 // via two ds_read_b64_tr_b16 (4 k-rows each).
@@ -191,12 +360,12 @@ __device__ __forceinline__ v8bf16 frag_bf16(const short* L, int cb, int kk) {
   return __builtin_bit_cast(v8bf16, c);
 }
 
-template <typename TIn>
+template <typename TIn, typename Stage>
 __global__ void __launch_bounds__(NT)
 syrk_kernel(const void* __restrict__ X, int64_t N, int64_t K, int64_t ldx,
             int bias, float* __restrict__ C, int64_t D, int64_t ldc,
             float alpha, float beta, int T, int splits, int64_t rows_per_split,
-            int vec_ok) {
+            int vec_ok, ConvGeom geom) {
   using LT = typename std::conditional<std::is_same<TIn, float>::value, float,
                                        short>::type;
   constexpr int LW = std::is_same<TIn, float>::value ? LDS_W32 : LDS_W16;
@@ -227,10 +396,11 @@ syrk_kernel(const void* __restrict__ X, int64_t N, int64_t K, int64_t ldx,
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
 
-  Staging<TIn> st;
+  Stage st;
+  st.init(c0i, c0j, K, geom);
   const int64_t ntiles = n_end > n_begin ? ceil_div(n_end - n_begin, BK) : 0;
   if (ntiles > 0) {
-    st.load(X, ldx, n_begin, n_end, K, bias, vec_ok, c0i, c0j, diag);
+    st.load(X, ldx, n_begin, n_end, K, bias, vec_ok, c0i, c0j, diag, geom);
     st.store((decltype(&lds[0]))Li, (decltype(&lds[0]))Lj, diag);
     __syncthreads();
   }
@@ -238,7 +408,7 @@ syrk_kernel(const void* __restrict__ X, int64_t N, int64_t K, int64_t ldx,
     const bool more = kt + 1 < ntiles;
     if (more)
       st.load(X, ldx, n_begin + (kt + 1) * BK, n_end, K, bias, vec_ok, c0i,
-              c0j, diag);
+              c0j, diag, geom);
     if constexpr (std::is_same<TIn, float>::value) {
       const int h = l >> 5, r = l & 31;
 #pragma unroll
@@ -371,9 +541,11 @@ int64_t syrk_workspace_splits(int64_t N, int64_t D) {
   return splits;
 }
 
+// geom == nullptr: X is a dense [N, K] matrix (row stride ldx); otherwise
+// X is an NHWC conv input and its rows are the conv patches (implicit im2col)
 void syrk(int in_dtype, const void* x, int64_t N, int64_t K, int64_t ldx,
           bool bias, float* C, int64_t D, int64_t ldc, float alpha,
-          float beta, int splits, hipStream_t s) {
+          float beta, int splits, hipStream_t s, const ConvGeom* geom) {
   if (D <= 0) return;
   const int T = (int)ceil_div(D, BM);
   const int64_t tiles = (int64_t)T * (T + 1) / 2;
@@ -385,18 +557,29 @@ void syrk(int in_dtype, const void* x, int64_t N, int64_t K, int64_t ldx,
   }
   const dim3 grid((unsigned)(tiles * splits));
   const float beta_k = splits > 1 ? 1.f : beta;
+  const ConvGeom g = geom != nullptr ? *geom : ConvGeom{};
   if (in_dtype == kF32) {
     const int vec_ok = ((ldx & 3) == 0) &&
                        ((reinterpret_cast<uintptr_t>(x) & 15) == 0);
-    syrk_kernel<float><<<grid, dim3(NT), 0, s>>>(
-        x, N, K, ldx, bias ? 1 : 0, C, D, ldc, alpha, beta_k, T, splits,
-        rows_per_split, vec_ok);
+    if (geom != nullptr)
+      syrk_kernel<float, PatchStaging<float>><<<grid, dim3(NT), 0, s>>>(
+          x, N, K, ldx, bias ? 1 : 0, C, D, ldc, alpha, beta_k, T, splits,
+          rows_per_split, vec_ok, g);
+    else
+      syrk_kernel<float, DenseStaging<float>><<<grid, dim3(NT), 0, s>>>(
+          x, N, K, ldx, bias ? 1 : 0, C, D, ldc, alpha, beta_k, T, splits,
+          rows_per_split, vec_ok, g);
   } else {
     const int vec_ok = ((ldx & 7) == 0) &&
                        ((reinterpret_cast<uintptr_t>(x) & 15) == 0);
-    syrk_kernel<bf16_t><<<grid, dim3(NT), 0, s>>>(
-        x, N, K, ldx, bias ? 1 : 0, C, D, ldc, alpha, beta_k, T, splits,
-        rows_per_split, vec_ok);
+    if (geom != nullptr)
+      syrk_kernel<bf16_t, PatchStaging<bf16_t>><<<grid, dim3(NT), 0, s>>>(
+          x, N, K, ldx, bias ? 1 : 0, C, D, ldc, alpha, beta_k, T, splits,
+          rows_per_split, vec_ok, g);
+    else
+      syrk_kernel<bf16_t, DenseStaging<bf16_t>><<<grid, dim3(NT), 0, s>>>(
+          x, N, K, ldx, bias ? 1 : 0, C, D, ldc, alpha, beta_k, T, splits,
+          rows_per_split, vec_ok, g);
   }
   if (splits > 1) {
     const unsigned t = (unsigned)ceil_div(D, 32);

@@ -294,6 +294,16 @@ class Conv2dModuleHelper(ModuleHelper):
             a = a.contiguous(memory_format=torch.channels_last)
         return a
 
+    def _dense_view(self, a: torch.Tensor) -> bool:
+        """1x1 / stride 1 / no padding on NHWC: the patch matrix is a free
+        view of the input (plain SYRK, see factor_ops.conv_patches)."""
+        return (
+            self.kernel == (1, 1)
+            and self.stride == (1, 1)
+            and self.padding == (0, 0)
+            and factor_ops.is_channels_last(a)
+        )
+
     def accumulate_a_factor(
         self,
         a: torch.Tensor,
@@ -302,6 +312,19 @@ class Conv2dModuleHelper(ModuleHelper):
         beta: float = 0.0,
     ) -> None:
         a = self._prepare_input(a)
+        if (
+            self.natural_order or self.kernel == (1, 1)
+        ) and not self._dense_view(a):
+            oh, ow = factor_ops.conv_out_hw(a.shape[2], a.shape[3], self.kernel,
+                                            self.stride, self.padding)
+            n = max(a.shape[0] * oh * ow, 1)
+            if factor_ops.conv_cov_accumulate_(
+                out, a, self.kernel, self.stride, self.padding,
+                bias=self.has_bias(),
+                alpha=alpha / (n * float(oh * ow) ** 2),
+                beta=beta,
+            ):
+                return
         patches, spatial = factor_ops.conv_patches(
             a,
             self.kernel,

@@ -65,6 +65,41 @@ def cov_accumulate_(
     return out
 
 
+def conv_cov_accumulate_(
+    out: torch.Tensor,
+    x: torch.Tensor,
+    kernel: tuple[int, int],
+    stride: tuple[int, int],
+    padding: tuple[int, int],
+    *,
+    bias: bool = False,
+    alpha: float = 1.0,
+    beta: float = 0.0,
+) -> bool:
+    """Implicit-im2col SYRK (K-HIP-2): ``out = beta*out + alpha*P^T P`` with
+    ``P`` the natural-order (kh, kw, c) patch matrix of the NHWC conv input
+    ``x``, computed without materialising ``P`` (the SYRK tile loader reads
+    the patches from ``x``).  Returns False when the fast path does not
+    apply (CPU, NCHW input, dtype, channel count not a multiple of one
+    16-byte vector); the caller then builds the patch matrix explicitly."""
+    if not (use_native(x, out) and out.dtype == torch.float32 and is_channels_last(x)):
+        return False
+    if x.dtype not in (torch.bfloat16, torch.float32):
+        return False
+    vec = 4 if x.dtype == torch.float32 else 8
+    st = x.stride()
+    if (
+        x.shape[1] % vec
+        or any(v % vec for v in (st[0], st[2], st[3]))
+        or x.data_ptr() % 16
+        or out.stride(1) != 1
+    ):
+        return False
+    native().syrk_conv(x, out, kernel[0], kernel[1], stride[0], stride[1],
+                       padding[0], padding[1], bias, float(alpha), float(beta))
+    return True
+
+
 def identity_(out: torch.Tensor) -> torch.Tensor:
     """Fill a square matrix with the identity (factor initialisation)."""
     if use_native(out) and out.dtype == torch.float32 and out.stride(1) == 1:

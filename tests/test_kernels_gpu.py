@@ -100,6 +100,51 @@ def test_triu_roundtrip(cuda, n, dtype):
     assert torch.allclose(out, 0.5 * a)
 
 
+def _natural_patches(x: torch.Tensor, k, s, p) -> torch.Tensor:
+    """Reference (kh, kw, c)-order patch matrix of an NCHW-logical input."""
+    b, c, h, w = x.shape
+    xp = torch.nn.functional.pad(x, (p[1], p[1], p[0], p[0]))
+    u = xp.unfold(2, k[0], s[0]).unfold(3, k[1], s[1])  # [B, C, OH, OW, kh, kw]
+    oh, ow = u.shape[2], u.shape[3]
+    return u.permute(0, 2, 3, 4, 5, 1).reshape(b * oh * ow, k[0] * k[1] * c), oh * ow
+
+
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize('cfg', [
+    # (B, C, H, W, kernel, stride, padding, bias)
+    (4, 16, 14, 14, (3, 3), (1, 1), (1, 1), False),
+    (2, 64, 15, 13, (3, 3), (2, 2), (1, 1), True),
+    (3, 32, 16, 16, (1, 1), (2, 2), (0, 0), False),
+    (2, 8, 9, 11, (5, 3), (1, 2), (2, 0), True),
+    (2, 136, 7, 7, (3, 3), (1, 1), (1, 1), False),
+])
+def test_syrk_conv_implicit_im2col(cuda, cfg, dtype):
+    b, c, h, w, k, s, p, bias = cfg
+    torch.manual_seed(sum(cfg[:4]))
+    x = torch.randn(b, c, h, w, device=cuda).to(dtype).contiguous(
+        memory_format=torch.channels_last)
+    pm, spatial = _natural_patches(x.double(), k, s, p)
+    if bias:
+        pm = torch.cat([pm, pm.new_ones(pm.shape[0], 1)], 1)
+    d = pm.shape[1]
+    alpha, beta = 0.7 / pm.shape[0], 0.25
+    c0 = torch.randn(d, d, device=cuda, dtype=torch.float64)
+    c0 = (c0 + c0.t()).float()
+    ref = beta * c0.double() + alpha * (pm.t() @ pm)
+    out = c0.clone()
+    assert factors.conv_cov_accumulate_(out, x, k, s, p, bias=bias, alpha=alpha, beta=beta)
+    tol = 1e-5 if dtype == torch.float32 else 1e-4
+    assert (out.double() - ref).abs().max().item() <= tol * ref.abs().max().item()
+    assert torch.equal(out, out.t())
+
+
+def test_syrk_conv_rejects_unaligned_channels(cuda):
+    x = torch.randn(2, 3, 8, 8, device=cuda).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    out = torch.zeros(27, 27, device=cuda)
+    assert not factors.conv_cov_accumulate_(out, x, (3, 3), (1, 1), (1, 1))
+
+
 @pytest.mark.parametrize('n', [2, 10, 33, 64, 100, 128])
 def test_jacobi_eigh(cuda, n):
     torch.manual_seed(n)
