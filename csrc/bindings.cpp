@@ -75,6 +75,10 @@ void gemm3_grouped(const GemmDesc* table, int nlayers, int total_tiles,
 // solver.cpp
 std::vector<at::Tensor> rocsolver_eigh(at::Tensor A, int64_t algo,
                                        int64_t max_sweeps, double tol);
+int64_t sytrd_max_n();
+std::vector<at::Tensor> sytrd_reduce(std::vector<at::Tensor> stacks);
+std::vector<at::Tensor> tridiag_eigvecs(at::Tensor A, at::Tensor d, at::Tensor e,
+                                        at::Tensor tau);
 
 namespace {
 
@@ -594,6 +598,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("apply_multi", &apply_multi);
   // GIL released: several host threads can each drive rocSOLVER on their
   // own stream (rocSOLVER's syevd blocks its calling thread internally)
+  m.def("sytrd_max_n", &sytrd_max_n);
+  m.def("sytrd_reduce", &sytrd_reduce, py::call_guard<py::gil_scoped_release>());
+  m.def("tridiag_eigvecs", &tridiag_eigvecs, py::call_guard<py::gil_scoped_release>());
   m.def("rocsolver_eigh", &rocsolver_eigh, py::call_guard<py::gil_scoped_release>(),
         py::arg("A"), py::arg("algo") = 0,
         py::arg("max_sweeps") = 100, py::arg("tol") = 1e-7);

@@ -39,4 +39,17 @@ struct ConvGeom {
   int32_t H, W, C, kw, sh, sw, ph, pw, OH, OW;
 };
 
+// sytrd.hip: one matrix of a batched mixed-size tridiagonalisation
+struct SytrdDesc {
+  float* A;      // [n][n] row-major, full symmetric on entry
+  float* Wt;     // [NB][n] panel W, row j = column j of LAPACK's W
+  float* d;      // [n]
+  float* e;      // [n-1]
+  float* tau;    // [n-1]
+  float* part1;  // [SY_MAXCH][SY_P1] col-step partials
+  float* part2;  // [SY_MAXROWBLK] symv partial w.v
+  float* sc;     // [2]: tau, v scale of the last reflector
+  int32_t n, pad;
+};
+
 }  // namespace kfac

@@ -17,6 +17,8 @@
 #include <rocblas/rocblas.h>
 #include <rocsolver/rocsolver.h>
 
+#include "descs.h"
+
 #include <mutex>
 #include <unordered_map>
 #include <vector>
@@ -109,4 +111,127 @@ std::vector<at::Tensor> rocsolver_eigh(at::Tensor A, int64_t algo,
                   resid.data_ptr<float>(), ints.data_ptr<int>() + batch,
                   (int)max_sweeps, (float)tol, (int)batch));
   return {W, A.transpose(1, 2)};
+}
+
+// ---------------------------------------------------------------------------
+// Large-n tier built on the native batched tridiagonalisation (sytrd.hip):
+// sytrd_reduce() reduces every matrix of every bucket in ONE launch chain
+// (in place: reflectors in the rows of A, d / e / tau out), then
+// tridiag_eigvecs() finishes one bucket with rocSOLVER stedc (divide and
+// conquer on T, eigenvectors of T) + ormtr (Z = Q Z_T), i.e. exactly the
+// second half of syevd.  Buckets can be finished on different streams.
+namespace kfac {
+int sytrd_nb();
+int sytrd_max_n();
+int sytrd_p1();
+int sytrd_maxch();
+int sytrd_maxrowblk();
+void sytrd_batched(const SytrdDesc* descs_dev, const int* ns, int batch,
+                   hipStream_t stream);
+}  // namespace kfac
+
+int64_t sytrd_max_n() { return kfac::sytrd_max_n(); }
+
+// stacks: list of [cnt, n, n] fp32 contiguous symmetric (overwritten).
+// Returns [d, e, tau] per stack, each [cnt, n] fp32.
+std::vector<at::Tensor> sytrd_reduce(std::vector<at::Tensor> stacks) {
+  TORCH_CHECK(!stacks.empty());
+  const auto opts = stacks[0].options();
+  c10::hip::HIPGuardMasqueradingAsCUDA g(stacks[0].device());
+  hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+  const int NB = kfac::sytrd_nb(), P1 = kfac::sytrd_p1();
+  std::vector<at::Tensor> outs;
+  std::vector<int> ns;
+  int64_t scratch = 0;
+  for (auto& A : stacks) {
+    TORCH_CHECK(A.is_cuda() && A.scalar_type() == at::kFloat && A.dim() == 3 &&
+                A.size(1) == A.size(2) && A.is_contiguous());
+    TORCH_CHECK(A.size(1) <= kfac::sytrd_max_n(), "sytrd supports n <= ",
+                kfac::sytrd_max_n());
+    const int64_t cnt = A.size(0), n = A.size(1);
+    for (int64_t b = 0; b < cnt; ++b) ns.push_back((int)n);
+    scratch += cnt * ((int64_t)NB * n + (int64_t)kfac::sytrd_maxch() * P1 +
+                      kfac::sytrd_maxrowblk() + 4);
+  }
+  const int batch = (int)ns.size();
+  if (batch == 0) return outs;
+  auto work = at::empty({std::max<int64_t>(scratch, 1)}, opts);
+  float* wp = work.data_ptr<float>();
+  auto host = at::empty({(int64_t)(batch * sizeof(kfac::SytrdDesc))},
+                        at::TensorOptions().dtype(at::kByte).pinned_memory(true));
+  auto* descs = reinterpret_cast<kfac::SytrdDesc*>(host.data_ptr());
+  int idx = 0;
+  for (auto& A : stacks) {
+    const int64_t cnt = A.size(0), n = A.size(1);
+    auto d = at::empty({cnt, n}, opts), e = at::zeros({cnt, n}, opts),
+         tau = at::zeros({cnt, n}, opts);
+    for (int64_t b = 0; b < cnt; ++b) {
+      kfac::SytrdDesc& D = descs[idx++];
+      D.A = A.data_ptr<float>() + b * n * n;
+      D.d = d.data_ptr<float>() + b * n;
+      D.e = e.data_ptr<float>() + b * n;
+      D.tau = tau.data_ptr<float>() + b * n;
+      D.Wt = wp;
+      wp += (int64_t)NB * n;
+      D.part1 = wp;
+      wp += (int64_t)kfac::sytrd_maxch() * P1;
+      D.part2 = wp;
+      wp += kfac::sytrd_maxrowblk();
+      D.sc = wp;
+      wp += 4;
+      D.n = (int)n;
+      D.pad = 0;
+    }
+    outs.push_back(d);
+    outs.push_back(e);
+    outs.push_back(tau);
+  }
+  auto dev = at::empty({host.numel()}, opts.dtype(at::kByte));
+  dev.copy_(host, /*non_blocking=*/true);
+  kfac::sytrd_batched(reinterpret_cast<const kfac::SytrdDesc*>(dev.data_ptr()),
+                      ns.data(), batch, s);
+  return outs;
+}
+
+// A: [cnt, n, n] reduced by sytrd_reduce (reflectors); d, e, tau from it.
+// Returns (evals [cnt, n] ascending, evecs [cnt, n, n], eigenvectors in
+// columns).
+std::vector<at::Tensor> tridiag_eigvecs(at::Tensor A, at::Tensor d, at::Tensor e,
+                                        at::Tensor tau) {
+  TORCH_CHECK(A.is_cuda() && A.dim() == 3 && A.is_contiguous());
+  const int64_t cnt = A.size(0), n = A.size(1);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(A.device());
+  hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+  auto Z = at::empty({cnt, n, n}, A.options());
+  auto info = at::empty({std::max<int64_t>(cnt, 1)}, A.options().dtype(at::kInt));
+  if (cnt == 0 || n == 0) return {d, Z.transpose(1, 2)};
+  HandleState& st = handle_for(s);
+  auto run = [&](int64_t b) -> rocblas_status {
+    float* Ab = A.data_ptr<float>() + b * n * n;
+    float* Zb = Z.data_ptr<float>() + b * n * n;
+    rocblas_status r = rocsolver_sstedc(st.handle, rocblas_evect_tridiagonal, (int)n,
+                                        d.data_ptr<float>() + b * n,
+                                        e.data_ptr<float>() + b * n, Zb, (int)n,
+                                        info.data_ptr<int>() + b);
+    if (r != rocblas_status_success && r != rocblas_status_size_unchanged &&
+        r != rocblas_status_size_increased)
+      return r;
+    rocblas_status r2 = rocsolver_sormtr(st.handle, rocblas_side_left, rocblas_fill_lower,
+                                         rocblas_operation_none, (int)n, (int)n, Ab,
+                                         (int)n, tau.data_ptr<float>() + b * n, Zb,
+                                         (int)n);
+    return r2;
+  };
+  size_t need = 0;
+  ROCBLAS_OK(rocblas_start_device_memory_size_query(st.handle));
+  run(0);
+  ROCBLAS_OK(rocblas_stop_device_memory_size_query(st.handle, &need));
+  if (!st.workspace.defined() || (size_t)st.workspace.numel() < need) {
+    st.workspace = at::empty({(int64_t)std::max<size_t>(need, 1)},
+                             A.options().dtype(at::kByte));
+    ROCBLAS_OK(rocblas_set_workspace(st.handle, st.workspace.data_ptr(),
+                                     (size_t)st.workspace.numel()));
+  }
+  for (int64_t b = 0; b < cnt; ++b) ROCBLAS_OK(run(b));
+  return {d, Z.transpose(1, 2)};
 }

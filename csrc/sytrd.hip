@@ -1,0 +1,349 @@
+// K-HIP-3 (large-n tier): batched blocked Householder tridiagonalisation of
+// symmetric fp32 matrices of MIXED sizes, A = Q T Q^T, Q = H_0 H_1 ... H_{n-2}.
+//
+// Why: rocSOLVER's syevd reduces one matrix at a time with ~5 dependent
+// tiny kernels per column (profiles/rocprof_eigh4608_syevd_stats.csv: 13k
+// launches of latrd_* / larfg per 4608 matrix, 55 ms each; the ResNet-50
+// factor mix spends ~300 ms of its ~400 ms eigen refresh there, and more
+// HIP streams / hardware queues do not overlap the chains:
+// profiles/eigh_lanes_hwq_mi355x.jsonl).  Here EVERY large factor a rank owns
+// advances one column per launch pair, so the whole mix costs
+// 2 * max(n) launches instead of ~5 * sum(n):
+//
+//   col  (k): finalise column k-1 (normalise its reflector, apply the
+//             -tau/2 (w.v) v correction to W), update row k with the
+//             panel's V W^T + W V^T, write d[k], and the larfg / W^T x /
+//             V^T x partial sums of row k (one workgroup per 256 entries);
+//   symv (k): every workgroup re-reduces those partials (beta, tau, v
+//             scale, t1 = W^T v, t2 = V^T v), stages v in LDS and computes 8
+//             rows of w = tau (A22 v - V t1 - W t2) plus partial w.v;
+//   per NB=32 columns: a finalise-only col step and the rank-2NB trailing
+//             update A22 -= V W^T + W V^T (64x64 LDS tiles, full square so the
+//             trailing matrix stays symmetric and the symv reads whole rows).
+//
+// Storage is row-major and the math is LAPACK's slatrd / ssytrd with
+// uplo = 'L' on the transpose: reflector k (v[k+1] = 1 implicit,
+// v[k+2:n] stored) lives in ROW k, which is exactly LAPACK's column-major
+// lower layout, so rocSOLVER's stedc + ormtr finish the eigensolve
+// (csrc/solver.cpp).  The algorithm is checked step for step on the CPU by
+// tools/sytrd_proto.py.  Replaces the reference's torch.linalg.eigh
+// (kfac/layers/eigen.py:294-347) for n >= KFAC_SYTRD_MIN_N.
+#include "common.h"
+#include "descs.h"
+
+namespace kfac {
+
+constexpr int SY_NB = 32;                 // panel width
+constexpr int SY_T = 256;                 // threads per block
+constexpr int SY_P1 = 2 * SY_NB + 4;      // partial stride: xn2, dW[NB], dV[NB]
+constexpr int SY_ROWS = 8;                // symv rows per workgroup (2 per wave)
+constexpr int SY_MAXN = 8192;             // v staged in LDS (32 KiB)
+constexpr int SY_MAXCH = SY_MAXN / SY_T;  // col-step chunks
+constexpr int SY_MAXROWBLK = SY_MAXN / SY_ROWS;
+
+int sytrd_nb() { return SY_NB; }
+int sytrd_max_n() { return SY_MAXN; }
+int sytrd_p1() { return SY_P1; }
+int sytrd_maxch() { return SY_MAXCH; }
+int sytrd_maxrowblk() { return SY_MAXROWBLK; }
+
+namespace {
+
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_reduce_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  float s = 0.f;
+#pragma unroll
+  for (int t = 0; t < SY_T / 64; ++t) s += red[t];
+  return s;
+}
+
+// col step for column k of panel p (i = k - p).  fin_only: only finalise
+// column k-1 (panel end).  grid (chunks, batch).
+__global__ void __launch_bounds__(SY_T) sytrd_col_kernel(
+    const SytrdDesc* __restrict__ descs, int k, int p, int fin_only) {
+  const SytrdDesc D = descs[blockIdx.y];
+  const int n = D.n;
+  if (k >= n) return;
+  const int r0 = k + blockIdx.x * SY_T;
+  if (r0 >= n) return;
+  const int i = k - p;
+  const int r = r0 + threadIdx.x;
+  const bool act = r < n;
+  __shared__ float red[SY_T / 64];
+  __shared__ float cW[SY_NB], cV[SY_NB];
+  __shared__ float wred[SY_T / 64][SY_P1];
+
+  float alpha2 = 0.f, sprev = 0.f;
+  if (i > 0) {
+    // partial w.v of column k-1: rows k..n-1 in blocks of SY_ROWS
+    const int cnt = (int)ceil_div(n - k, SY_ROWS);
+    float s = 0.f;
+    for (int t = threadIdx.x; t < cnt; t += SY_T) s += D.part2[t];
+    s = block_sum(s, red);
+    const float tp = D.sc[0];
+    sprev = D.sc[1];
+    alpha2 = -0.5f * tp * s;
+  }
+  if ((int)threadIdx.x < i && !fin_only) {
+    const int j = threadIdx.x;
+    float w = D.Wt[(int64_t)j * n + k];
+    float v;
+    if (j == i - 1) {
+      w += alpha2;  // finalised W[k, i-1]; V_{i-1}[k] = 1 (implicit)
+      v = 1.f;
+    } else {
+      v = D.A[(int64_t)(p + j) * n + k];
+    }
+    cW[j] = w;
+    cV[j] = v;
+  }
+  __syncthreads();
+
+  float vprev = 0.f, wprev = 0.f;
+  if (act && i > 0) {
+    vprev = (r == k) ? 1.f : D.A[(int64_t)(k - 1) * n + r] * sprev;
+    if (r > k) D.A[(int64_t)(k - 1) * n + r] = vprev;
+    wprev = D.Wt[(int64_t)(i - 1) * n + r] + alpha2 * vprev;
+    // W[k, i-1] is finalised by every block on its own (cW above) and not
+    // read again by later col / symv steps: writing it here would race with
+    // those reads.  The panel-end trailing update does read it (r = q).
+    if (r > k || fin_only) D.Wt[(int64_t)(i - 1) * n + r] = wprev;
+  }
+  if (fin_only) return;
+
+  float vj[SY_NB], wj[SY_NB];
+  float a = 0.f;
+  if (act) {
+    a = D.A[(int64_t)k * n + r];
+#pragma unroll
+    for (int j = 0; j < SY_NB; ++j) {
+      if (j < i) {
+        if (j == i - 1) {
+          vj[j] = vprev;
+          wj[j] = wprev;
+        } else {
+          vj[j] = D.A[(int64_t)(p + j) * n + r];
+          wj[j] = D.Wt[(int64_t)j * n + r];
+        }
+        a -= vj[j] * cW[j] + wj[j] * cV[j];
+      }
+    }
+    D.A[(int64_t)k * n + r] = a;
+    if (r == k) D.d[k] = a;
+  }
+  if (k == n - 1) return;  // last diagonal entry: no reflector
+  // partial sums over the reflector tail x = a[k+2:n]
+  const float x = (act && r >= k + 2) ? a : 0.f;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  float s0 = wave_reduce_sum(x * x);
+  if (l == 0) wred[w][0] = s0;
+#pragma unroll
+  for (int j = 0; j < SY_NB; ++j) {
+    if (j < i) {
+      float sw = wave_reduce_sum(x != 0.f ? wj[j] * x : 0.f);
+      float sv = wave_reduce_sum(x != 0.f ? vj[j] * x : 0.f);
+      if (l == 0) {
+        wred[w][1 + j] = sw;
+        wred[w][1 + SY_NB + j] = sv;
+      }
+    }
+  }
+  __syncthreads();
+  const int nval = 1 + 2 * SY_NB;
+  for (int t = threadIdx.x; t < nval; t += SY_T) {
+    const int j = (t - 1) % SY_NB;
+    if (t > 0 && j >= i) continue;
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < SY_T / 64; ++q) s += wred[q][t];
+    D.part1[(int64_t)blockIdx.x * SY_P1 + t] = s;
+  }
+}
+
+// symv step for column k (k <= n-2).  grid (row blocks, batch).
+__global__ void __launch_bounds__(SY_T) sytrd_symv_kernel(
+    const SytrdDesc* __restrict__ descs, int k, int p) {
+  const SytrdDesc D = descs[blockIdx.y];
+  const int n = D.n;
+  if (k >= n - 1) return;
+  const int row0 = k + 1 + blockIdx.x * SY_ROWS;
+  if (row0 >= n) return;
+  const int i = k - p;
+  const int m = n - k - 1;  // length of v (rows/cols k+1..n-1)
+  __shared__ float sv[SY_MAXN];
+  __shared__ float tot[SY_P1];
+  __shared__ float t1[SY_NB], t2[SY_NB];
+  __shared__ float red[SY_T / 64];
+  __shared__ float scal[3];
+
+  // reduce the col-step partials of column k
+  const int nch = (int)ceil_div(n - k, SY_T);
+  for (int t = threadIdx.x; t < 1 + 2 * SY_NB; t += SY_T) {
+    const int j = (t - 1) % SY_NB;
+    if (t > 0 && j >= i) continue;
+    float s = 0.f;
+    for (int c = 0; c < nch; ++c) s += D.part1[(int64_t)c * SY_P1 + t];
+    tot[t] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float alpha = D.A[(int64_t)k * n + k + 1];
+    const float xn2 = tot[0];
+    float tau_k, beta, scale;
+    if (xn2 == 0.f) {
+      tau_k = 0.f;
+      beta = alpha;
+      scale = 0.f;
+    } else {
+      beta = -copysignf(sqrtf(alpha * alpha + xn2), alpha);
+      tau_k = (beta - alpha) / beta;
+      scale = 1.f / (alpha - beta);
+    }
+    scal[0] = tau_k;
+    scal[1] = scale;
+    if (blockIdx.x == 0) {
+      D.e[k] = beta;
+      D.tau[k] = tau_k;
+      D.sc[0] = tau_k;
+      D.sc[1] = scale;
+    }
+  }
+  __syncthreads();
+  const float tau_k = scal[0], scale = scal[1];
+  if ((int)threadIdx.x < i) {
+    const int j = threadIdx.x;
+    t1[j] = D.Wt[(int64_t)j * n + k + 1] + scale * tot[1 + j];
+    t2[j] = D.A[(int64_t)(p + j) * n + k + 1] + scale * tot[1 + SY_NB + j];
+  }
+  const float* arow = D.A + (int64_t)k * n + k + 1;
+  for (int c = threadIdx.x; c < m; c += SY_T) sv[c] = c == 0 ? 1.f : arow[c] * scale;
+  __syncthreads();
+
+  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+  float pd = 0.f;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int r = row0 + wv * 2 + h;
+    if (r >= n) break;
+    const float* ar = D.A + (int64_t)r * n + k + 1;
+    float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
+    int c = l;
+    for (; c + 192 < m; c += 256) {
+      acc0 += ar[c] * sv[c];
+      acc1 += ar[c + 64] * sv[c + 64];
+      acc2 += ar[c + 128] * sv[c + 128];
+      acc3 += ar[c + 192] * sv[c + 192];
+    }
+    for (; c < m; c += 64) acc0 += ar[c] * sv[c];
+    float y = wave_reduce_sum((acc0 + acc1) + (acc2 + acc3));
+    float corr = 0.f;
+    if (l < i) corr = D.A[(int64_t)(p + l) * n + r] * t1[l];
+    else if (l >= 32 && l - 32 < i) corr = D.Wt[(int64_t)(l - 32) * n + r] * t2[l - 32];
+    corr = wave_reduce_sum(corr);
+    const float wr = tau_k * (y - corr);
+    if (l == 0) {
+      D.Wt[(int64_t)i * n + r] = wr;
+      pd += wr * sv[r - k - 1];
+    }
+  }
+  pd = block_sum(pd, red);
+  if (threadIdx.x == 0) D.part2[blockIdx.x] = pd;
+}
+
+// trailing update A[q:,q:] -= V W^T + W V^T for the panel [p, q).
+// grid (col tiles, row tiles, batch), 64x64 tiles, 16x16 threads x 4x4.
+__global__ void __launch_bounds__(SY_T) sytrd_syr2k_kernel(
+    const SytrdDesc* __restrict__ descs, int q, int p) {
+  const SytrdDesc D = descs[blockIdx.z];
+  const int n = D.n;
+  if (q >= n) return;
+  const int r0 = q + blockIdx.y * 64, c0 = q + blockIdx.x * 64;
+  if (r0 >= n || c0 >= n) return;
+  const int mw = q - p;
+  __shared__ float Vr[SY_NB][64], Wr[SY_NB][64], Vc[SY_NB][64], Wc[SY_NB][64];
+  for (int t = threadIdx.x; t < SY_NB * 64; t += SY_T) {
+    const int j = t >> 6, x = t & 63;
+    float vr = 0.f, wr = 0.f, vc = 0.f, wc = 0.f;
+    if (j < mw) {
+      const int r = r0 + x, c = c0 + x;
+      if (r < n) {
+        vr = (r == p + j + 1) ? 1.f : D.A[(int64_t)(p + j) * n + r];
+        wr = D.Wt[(int64_t)j * n + r];
+      }
+      if (c < n) {
+        vc = (c == p + j + 1) ? 1.f : D.A[(int64_t)(p + j) * n + c];
+        wc = D.Wt[(int64_t)j * n + c];
+      }
+    }
+    Vr[j][x] = vr;
+    Wr[j][x] = wr;
+    Vc[j][x] = vc;
+    Wc[j][x] = wc;
+  }
+  __syncthreads();
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  float acc[4][4] = {};
+  for (int j = 0; j < mw; ++j) {
+    float vr[4], wr[4], vc[4], wc[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      vr[a] = Vr[j][ty * 4 + a];
+      wr[a] = Wr[j][ty * 4 + a];
+      vc[a] = Vc[j][tx + 16 * a];
+      wc[a] = Wc[j][tx + 16 * a];
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc[a][b] += vr[a] * wc[b] + wr[a] * vc[b];
+  }
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const int r = r0 + ty * 4 + a;
+    if (r >= n) continue;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int c = c0 + tx + 16 * b;
+      if (c < n) D.A[(int64_t)r * n + c] -= acc[a][b];
+    }
+  }
+}
+
+}  // namespace
+
+// Host driver: descs is a device table of `batch` descriptors, ns the host
+// copy of their sizes.  Issues 2 launches per column of the largest matrix
+// plus 2 per panel, all on `stream`, no host sync.
+void sytrd_batched(const SytrdDesc* descs_dev, const int* ns, int batch,
+                   hipStream_t stream) {
+  int maxn = 0;
+  for (int b = 0; b < batch; ++b) maxn = ns[b] > maxn ? ns[b] : maxn;
+  if (maxn <= 0) return;
+  for (int p = 0; p < maxn; p += SY_NB) {
+    const int q = (p + SY_NB < maxn) ? p + SY_NB : maxn;
+    for (int k = p; k < q; ++k) {
+      const int rem = maxn - k;
+      hipLaunchKernelGGL(sytrd_col_kernel, dim3((unsigned)ceil_div(rem, SY_T), batch),
+                         dim3(SY_T), 0, stream, descs_dev, k, p, 0);
+      if (k < maxn - 1) {
+        hipLaunchKernelGGL(sytrd_symv_kernel,
+                           dim3((unsigned)ceil_div(rem - 1, SY_ROWS), batch),
+                           dim3(SY_T), 0, stream, descs_dev, k, p);
+      }
+    }
+    if (q < maxn) {
+      const int rem = maxn - q;
+      hipLaunchKernelGGL(sytrd_col_kernel, dim3((unsigned)ceil_div(rem, SY_T), batch),
+                         dim3(SY_T), 0, stream, descs_dev, q, p, 1);
+      const unsigned tiles = (unsigned)ceil_div(rem, 64);
+      hipLaunchKernelGGL(sytrd_syr2k_kernel, dim3(tiles, tiles, batch), dim3(SY_T), 0,
+                         stream, descs_dev, q, p);
+    }
+  }
+}
+
+}  // namespace kfac

@@ -6,7 +6,14 @@ sizes (all K-FAC factors a rank owns) with as little latency as possible:
 * matrices are bucketed by size; each bucket is ONE batched call;
 * n <= 64: the LDS-resident parallel Jacobi kernel (csrc/eigh_jacobi.hip),
   one matrix per workgroup;
-* larger n: direct batched rocSOLVER ``syevd`` calls from C++
+* with ``KFAC_EIGH=sytrd``, n >= ``KFAC_SYTRD_MIN_N``: the native batched
+  tridiagonalisation (csrc/sytrd.hip): every such factor of every bucket
+  advances one column per launch pair in ONE chain, then each matrix is
+  finished by rocSOLVER ``stedc`` + ``ormtr`` (the second half of syevd) on
+  the lanes below.  Opt-in: on MI355X it is correct to ~1e-6 but not yet
+  faster than syevd on the ResNet-50 factor mix (526 vs 397 ms; the stedc +
+  ormtr tail alone sums to ~330 ms, profiles/eigh_sytrd_mi355x.jsonl);
+* other n: direct batched rocSOLVER ``syevd`` calls from C++
   (csrc/solver.cpp) which, unlike ``torch.linalg.eigh``, never synchronise
   the host;
 * the buckets run concurrently on a small pool of HIP streams (joined back
@@ -19,7 +26,8 @@ degenerate eigenspaces); K-FAC only uses them through ``Q f(D) Q^T``, which
 is invariant to that freedom.
 
 Environment knobs: ``KFAC_EIGH`` = auto | torch | syevd | syevj | syevdj
-(force one algorithm for n > 64), ``KFAC_EIGH_STREAMS`` (lanes, default 8),
+(force one algorithm for n > 64; sytrd = native tridiagonalisation tier),
+``KFAC_SYTRD_MIN_N`` (smallest n for the sytrd tier), ``KFAC_EIGH_STREAMS`` (lanes, default 8),
 ``KFAC_EIGH_THREADS`` (0: issue every lane from the calling thread),
 ``KFAC_EIGH_SPLIT_N`` (factors at least this large are solved one per job),
 ``KFAC_JACOBI_SWEEPS`` / ``KFAC_JACOBI_TOL`` (small-n kernel).
@@ -42,6 +50,12 @@ _ALGOS = {'syevd': 0, 'syevj': 1, 'syevdj': 2}
 # n above which auto picks syevd over syevj (Jacobi sweeps are O(n^3) each)
 # largest n sent to the LDS Jacobi kernel (its hard limit is jacobi_max_n())
 JACOBI_MAX_N = int(os.environ.get('KFAC_JACOBI_MAX_N', '64'))
+
+
+def sytrd_min_n() -> int:
+    """Smallest factor dimension sent to the native tridiagonalisation."""
+    return int(os.environ.get('KFAC_SYTRD_MIN_N', '512'))
+
 
 logger = logging.getLogger(__name__)
 _streams: list[torch.cuda.Stream] = []
@@ -76,6 +90,8 @@ def _gpu_bucket(stack: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
     if n <= JACOBI_MAX_N:
         return lib.jacobi_eigh(stack.contiguous(), JACOBI_SWEEPS, JACOBI_TOL)
     algo = _algo_for(n)
+    if algo == 'sytrd':  # below KFAC_SYTRD_MIN_N
+        algo = 'syevd'
     if algo == 'torch':
         return torch.linalg.eigh(stack)
     evals, evecs = lib.rocsolver_eigh(stack.contiguous(), _ALGOS[algo], 100, 1e-7)
@@ -117,6 +133,13 @@ def eigh_many(
             for i, r in _launch_jobs(gpu, stacks, dev).items():
                 out[i] = r
     return [o for o in out if o is not None]
+
+
+def _use_sytrd(n: int) -> bool:
+    if os.environ.get('KFAC_EIGH', 'auto') != 'sytrd' or n < sytrd_min_n():
+        return False
+    lib = native()
+    return lib is not None and n <= int(lib.sytrd_max_n())
 
 
 def _jobs(gpu: list) -> list[tuple[tuple, list[int], int, int]]:
@@ -173,6 +196,12 @@ def _launch_jobs(
     ready = torch.cuda.Event()
     ready.record(main)
     streams = _side_streams(dev)
+    big = [(k, v) for k, v in gpu if _use_sytrd(k[0])]
+    rest = [(k, v) for k, v in gpu if not _use_sytrd(k[0])]
+    out: dict[int, tuple[torch.Tensor, torch.Tensor]] = {}
+    if big:
+        out.update(_launch_sytrd(big, rest, stacks, main, ready, streams))
+        return out
     jobs = sorted(_jobs(gpu), key=lambda j: -_bucket_cost(j[0][0], j[3] - j[2]))
     lanes: list[list] = [[] for _ in streams]
     loads = [0.0] * len(streams)
@@ -189,7 +218,6 @@ def _launch_jobs(
         results = [f.result() for f in futs]
     else:
         results = [_run_lane(s, ln, stacks) for s, ln in active]
-    out: dict[int, tuple[torch.Tensor, torch.Tensor]] = {}
     for (s, ln), res in zip(active, results):
         main.wait_stream(s)
         for (key, idxs, lo, hi), (evals, evecs) in zip(ln, res):
@@ -198,6 +226,89 @@ def _launch_jobs(
             evecs.record_stream(main)
             for k in range(hi - lo):
                 out[idxs[lo + k]] = (evals[k], evecs[k])
+    return out
+
+
+def _sytrd_lane(stream: torch.cuda.Stream, keys: list, stacks: dict) -> list:
+    with torch.cuda.stream(stream):
+        return native().sytrd_reduce([stacks[k] for k in keys])
+
+
+def _tridiag_lane(stream: torch.cuda.Stream, jobs: list, stacks: dict,
+                  red: dict) -> list:
+    with torch.cuda.stream(stream):
+        res = []
+        for key, _, lo, hi in jobs:
+            d, e, tau = red[key]
+            for t in (d, e, tau):  # allocated on lane 0, read here
+                t.record_stream(stream)
+            res.append(native().tridiag_eigvecs(
+                stacks[key][lo:hi], d[lo:hi], e[lo:hi], tau[lo:hi]))
+        return res
+
+
+def _launch_sytrd(
+    big: list,
+    rest: list,
+    stacks: dict,
+    main: torch.cuda.Stream,
+    ready: torch.cuda.Event,
+    streams: list[torch.cuda.Stream],
+) -> dict[int, tuple[torch.Tensor, torch.Tensor]]:
+    """Large buckets: ONE native tridiagonalisation chain on lane 0 while the
+    other lanes run the small buckets' syevd; then every large matrix is
+    finished (stedc + ormtr) as its own job, LPT over all lanes."""
+    for s in streams:
+        s.wait_event(ready)
+    keys = [k for k, _ in big]
+    small_jobs = sorted(_jobs(rest), key=lambda j: -_bucket_cost(j[0][0], j[3] - j[2]))
+    lanes: list[list] = [[] for _ in streams[1:]]
+    loads = [0.0] * len(lanes)
+    for job in small_jobs:
+        k = loads.index(min(loads))
+        loads[k] += _bucket_cost(job[0][0], job[3] - job[2])
+        lanes[k].append(job)
+    active = [(s, ln) for s, ln in zip(streams[1:], lanes) if ln]
+    if _threads_enabled() and active:
+        pool = _executor(len(active) + 1)
+        fut_red = pool.submit(_sytrd_lane, streams[0], keys, stacks)
+        futs = [pool.submit(_run_lane, s, ln, stacks) for s, ln in active]
+        flat = fut_red.result()
+        results = [f.result() for f in futs]
+    else:
+        flat = _sytrd_lane(streams[0], keys, stacks)
+        results = [_run_lane(s, ln, stacks) for s, ln in active]
+    red = {k: tuple(flat[3 * i:3 * i + 3]) for i, k in enumerate(keys)}
+    reduced = torch.cuda.Event()
+    reduced.record(streams[0])
+    # phase 2: per-matrix stedc + ormtr jobs over every lane
+    tjobs = [(key, idxs, b, b + 1) for key, idxs in big for b in range(len(idxs))]
+    tjobs.sort(key=lambda j: -_bucket_cost(j[0][0], 1))
+    tl: list[list] = [[] for _ in streams]
+    tload = [0.0] * len(streams)
+    for job in tjobs:
+        k = tload.index(min(tload))
+        tload[k] += _bucket_cost(job[0][0], 1)
+        tl[k].append(job)
+    tactive = [(s, ln) for s, ln in zip(streams, tl) if ln]
+    for s, _ in tactive:
+        s.wait_event(reduced)
+    if _threads_enabled() and len(tactive) > 1:
+        pool = _executor(len(tactive))
+        tf = [pool.submit(_tridiag_lane, s, ln, stacks, red) for s, ln in tactive]
+        tres = [f.result() for f in tf]
+    else:
+        tres = [_tridiag_lane(s, ln, stacks, red) for s, ln in tactive]
+    out: dict[int, tuple[torch.Tensor, torch.Tensor]] = {}
+    for (s, ln), res in list(zip(active, results)) + list(zip(tactive, tres)):
+        main.wait_stream(s)
+        for (key, idxs, lo, hi), (evals, evecs) in zip(ln, res):
+            evals.record_stream(main)
+            evecs.record_stream(main)
+            for k in range(hi - lo):
+                out[idxs[lo + k]] = (evals[k], evecs[k])
+    for k in keys:
+        stacks[k].record_stream(streams[0])
     return out
 
 

@@ -44,13 +44,25 @@ def main() -> None:
         s = make(n, cnt, dev)
         mats += [s[i].contiguous() for i in range(cnt)]
     ref = [torch.linalg.eigvalsh(m.double()) for m in mats]
-    configs = [('1', '8', '100000'), ('0', '8', '100000'),
-               ('1', '8', '4608'), ('1', '12', '4608'), ('1', '12', '2304')]
-    for threads, streams, split in configs:
+    # PROBE_CONFIGS="threads:streams:split_n,..." overrides the default list
+    spec = os.environ.get('PROBE_CONFIGS')
+    if spec:
+        configs = [tuple(c.split(':')) for c in spec.split(',')]
+    else:
+        configs = [('1', '8', '100000'), ('0', '8', '100000'),
+                   ('1', '8', '4608'), ('1', '12', '4608'), ('1', '12', '2304')]
+    for cfg in configs:
+        threads, streams, split = cfg[:3]
+        mode = cfg[3] if len(cfg) > 3 else 'auto'
+        min_n = cfg[4] if len(cfg) > 4 else '512'
         os.environ['KFAC_EIGH_THREADS'] = threads
         os.environ['KFAC_EIGH_STREAMS'] = streams
         os.environ['KFAC_EIGH_SPLIT_N'] = split
-        row = {'mix': 'resnet50', 'threads': threads, 'streams': streams, 'split_n': split}
+        os.environ['KFAC_EIGH'] = mode
+        os.environ['KFAC_SYTRD_MIN_N'] = min_n
+        row = {'mix': 'resnet50', 'threads': threads, 'streams': streams, 'split_n': split,
+               'eigh': mode, 'sytrd_min_n': min_n,
+               'hw_queues': os.environ.get('GPU_MAX_HW_QUEUES', 'default')}
         row['ms'] = round(timed(lambda: linalg.eigh_many(mats), 2), 1)
         got = linalg.eigh_many(mats)
         row['max_rel_eval_err'] = max(
