@@ -76,6 +76,8 @@ void gemm3_grouped(const GemmDesc* table, int nlayers, int total_tiles,
 std::vector<at::Tensor> rocsolver_eigh(at::Tensor A, int64_t algo,
                                        int64_t max_sweeps, double tol);
 int64_t sytrd_max_n();
+int64_t spd_lds_max_n();
+at::Tensor spd_inverse(at::Tensor F, double damping);
 std::vector<at::Tensor> sytrd_reduce(std::vector<at::Tensor> stacks);
 std::vector<at::Tensor> tridiag_eigvecs(at::Tensor A, at::Tensor d, at::Tensor e,
                                         at::Tensor tau);
@@ -599,6 +601,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   // GIL released: several host threads can each drive rocSOLVER on their
   // own stream (rocSOLVER's syevd blocks its calling thread internally)
   m.def("sytrd_max_n", &sytrd_max_n);
+  m.def("spd_lds_max_n", &spd_lds_max_n);
+  m.def("spd_inverse", &spd_inverse, py::call_guard<py::gil_scoped_release>());
   m.def("sytrd_reduce", &sytrd_reduce, py::call_guard<py::gil_scoped_release>());
   m.def("tridiag_eigvecs", &tridiag_eigvecs, py::call_guard<py::gil_scoped_release>());
   m.def("rocsolver_eigh", &rocsolver_eigh, py::call_guard<py::gil_scoped_release>(),

@@ -235,3 +235,33 @@ std::vector<at::Tensor> tridiag_eigvecs(at::Tensor A, at::Tensor d, at::Tensor e
   for (int64_t b = 0; b < cnt; ++b) ROCBLAS_OK(run(b));
   return {d, Z.transpose(1, 2)};
 }
+
+// ---------------------------------------------------------------------------
+// K-HIP-5 batched damped SPD inverse (csrc/spdinv.hip): F [cnt, n, n] fp32
+// symmetric -> (F + damping I)^-1, exactly symmetric, no host sync; one
+// workgroup per matrix, Gauss-Jordan in LDS (n <= spd_lds_max_n()).  Larger
+// factors are inverted one at a time by the caller (ops/linalg.py): the
+// strided-batched rocSOLVER potrf + potri path returned sporadic NaN rows on
+// MI355X (ROCm 7.2), so it is not offered here.
+namespace kfac {
+int spd_lds_max_n();
+void spd_inverse_lds(const float* F, float* X, int n, int batch, int64_t strideF,
+                     int64_t strideX, float damping, hipStream_t s);
+}  // namespace kfac
+
+int64_t spd_lds_max_n() { return kfac::spd_lds_max_n(); }
+
+at::Tensor spd_inverse(at::Tensor F, double damping) {
+  TORCH_CHECK(F.is_cuda() && F.scalar_type() == at::kFloat && F.dim() == 3 &&
+              F.size(1) == F.size(2) && F.is_contiguous());
+  const int64_t cnt = F.size(0), n = F.size(1);
+  TORCH_CHECK(n <= kfac::spd_lds_max_n(), "spd_inverse supports n <= ",
+              kfac::spd_lds_max_n());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(F.device());
+  hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+  auto X = at::empty_like(F);
+  if (cnt == 0 || n == 0) return X;
+  kfac::spd_inverse_lds(F.data_ptr<float>(), X.data_ptr<float>(), (int)n, (int)cnt,
+                        n * n, n * n, (float)damping, s);
+  return X;
+}

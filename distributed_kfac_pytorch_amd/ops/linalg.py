@@ -333,20 +333,57 @@ def eigh(mat: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
     return eigh_many([mat])[0]
 
 
+def inverse_many(mats: list[torch.Tensor], damping: float) -> list[torch.Tensor]:
+    """``(F + damping I)^-1`` for every symmetric factor, fp32, batched by
+    size: n <= ``spd_lds_max_n()`` in ONE launch per size (K-HIP-5,
+    csrc/spdinv.hip: Gauss-Jordan in LDS, one workgroup per matrix), larger
+    n one Cholesky + ``cholesky_inverse`` per matrix.  No host
+    synchronisation; the results are exactly symmetric.  CPU tensors use
+    the PyTorch math.
+
+    Batched Cholesky is avoided for n > 176: on MI355X (ROCm 7.2 rocSOLVER)
+    the strided-batched potrf + potri path returned sporadic NaN rows
+    (csrc/solver.cpp ``spd_inverse``) and torch's batched ``cholesky_ex``
+    returned wrong inverses and then faulted (tools/spd_dbg.py)."""
+    out: list[torch.Tensor | None] = [None] * len(mats)
+    buckets: dict[tuple[int, torch.device], list[int]] = defaultdict(list)
+    for i, m in enumerate(mats):
+        buckets[(m.shape[0], m.device)].append(i)
+    for (_, dev), idxs in buckets.items():
+        n = mats[idxs[0]].shape[0]
+        if dev.type == 'cuda' and use_native(mats[idxs[0]]):
+            stack = torch.stack([mats[i].to(torch.float32) for i in idxs])
+            if n <= int(native().spd_lds_max_n()):
+                inv = native().spd_inverse(stack, float(damping))
+            else:
+                inv = torch.stack([_damped_inverse_torch(m, damping) for m in stack])
+                inv = 0.5 * (inv + inv.transpose(-1, -2))
+            for k, i in enumerate(idxs):
+                out[i] = inv[k]
+        else:
+            for i in idxs:
+                out[i] = _damped_inverse_torch(mats[i], damping)
+    return [o for o in out if o is not None]
+
+
 def damped_inverse(mat: torch.Tensor, damping: float) -> torch.Tensor:
     """``(mat + damping*I)^-1`` computed in fp32 (reference inverse.py:
-    185-212).  The damped factor is SPD, so a Cholesky factorisation plus
-    ``cholesky_inverse`` replaces the general LU inverse (half the flops, no
-    pivoting); if the factorisation fails (indefinite input) it falls back
-    to ``torch.linalg.inv`` (checked on CPU only; on the GPU the check
-    would be a host sync)."""
+    185-212); single-matrix wrapper around ``inverse_many``."""
+    return inverse_many([mat], damping)[0]
+
+
+def _damped_inverse_torch(mat: torch.Tensor, damping: float) -> torch.Tensor:
+    """PyTorch math: the damped factor is SPD, so a Cholesky factorisation
+    plus ``cholesky_inverse`` replaces the general LU inverse (half the
+    flops, no pivoting); if the factorisation fails (indefinite input) it
+    falls back to ``torch.linalg.inv``."""
     a = mat.to(torch.float32)
-    a = a + damping * torch.eye(a.shape[0], dtype=a.dtype, device=a.device)
+    a = a + damping * torch.eye(a.shape[-1], dtype=a.dtype, device=a.device)
     chol, info = torch.linalg.cholesky_ex(a)
     if a.is_cuda:
-        # No host sync on the GPU path: a damped K-FAC factor is SPD by
-        # construction (PSD running average + damping * I).
+        # no host sync on the GPU: a damped K-FAC factor is SPD by
+        # construction (PSD running average + damping * I)
         return torch.cholesky_inverse(chol)
-    if int(info) != 0:
+    if bool((info != 0).any()):
         return torch.linalg.inv(a)
     return torch.cholesky_inverse(chol)

@@ -255,6 +255,34 @@ def test_eigh_many_sytrd_tier(cuda, monkeypatch, sizes):
         _check_eigpairs(m, d, q)
 
 
+@pytest.mark.parametrize('n', [1, 7, 64, 129, 176, 177, 300, 640])
+def test_spd_inverse(cuda, n):
+    """K-HIP-5: LDS Gauss-Jordan (n <= 176) and batched Cholesky (larger n)
+    damped inverses vs a float64 reference; exactly symmetric."""
+    torch.manual_seed(n)
+    b, damping = 3, 1e-2
+    x = torch.randn(b, n, 2 * n, device=cuda)
+    f = x @ x.transpose(1, 2) / (2 * n)
+    got = torch.stack(linalg.inverse_many(list(f), damping))
+    eye = torch.eye(n, device=cuda, dtype=torch.float64)
+    ref = torch.linalg.inv(f.double() + damping * eye)
+    err = (got.double() - ref).abs().max().item()
+    assert err < 2e-4 * ref.abs().max().item(), err
+    assert torch.equal(got, got.transpose(1, 2))
+
+
+def test_inverse_many_mixed(cuda):
+    mats = []
+    for n in (10, 10, 200, 33):
+        x = torch.randn(n, 3 * n, device=cuda)
+        mats.append(x @ x.t() / (3 * n))
+    res = linalg.inverse_many(mats, 0.003)
+    for m, inv in zip(mats, res):
+        n = m.shape[0]
+        ident = (m.double() + 0.003 * torch.eye(n, device=cuda, dtype=torch.float64)) @ inv.double()
+        assert (ident - torch.eye(n, device=cuda, dtype=torch.float64)).abs().max().item() < 1e-3
+
+
 def test_precondition_epilogues(cuda):
     g, a = 48, 97
     v = torch.randn(g, a, device=cuda)
