@@ -197,7 +197,10 @@ class StepGraphs:
             side.wait_stream(torch.cuda.current_stream())
             lanes = [] if grouped else self._lanes(workers)
             with torch.cuda.stream(side):
-                with torch.cuda.graph(g, stream=side):
+                # thread_local: only this thread is barred from unsafe HIP
+                # calls while capturing -- RCCL's watchdog thread keeps
+                # querying its events (multi-rank jobs)
+                with torch.cuda.graph(g, stream=side, capture_error_mode='thread_local'):
                     if grouped:
                         pre._grouped.launch()
                     # otherwise fork: independent per-layer GEMM chains run as
