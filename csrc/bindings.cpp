@@ -70,6 +70,17 @@ void apply_multi(const LayerDesc* descs, int nlayers, int64_t total_blocks,
 int gemm3_grid(int total_tiles);
 void gemm3_grouped(const GemmDesc* table, int nlayers, int total_tiles,
                    bool a_kc, bool b_kc, hipStream_t s);
+// bnact.hip
+void bn_partition(int64_t M, int C, int64_t* rows_per_block, int* nblk);
+int bn_max_c();
+void bn_forward(const uint16_t* x, const uint16_t* res, const float* weight,
+                const float* bias, float* running_mean, float* running_var,
+                int64_t* num_batches, float momentum, float eps, int relu, int64_t M,
+                int C, float* part, float* stats, uint16_t* y, hipStream_t s);
+void bn_backward(const uint16_t* x, const uint16_t* dy, const uint16_t* y,
+                 const float* weight, const float* stats, int relu, int64_t M, int C,
+                 float* part, float* coef, float* dweight, float* dbias, uint16_t* dx,
+                 uint16_t* dres, hipStream_t s);
 }  // namespace kfac
 
 // solver.cpp
@@ -574,6 +585,98 @@ void gemm3_grouped(const at::Tensor& table, int64_t nlayers, int64_t total_tiles
 
 }  // namespace
 
+
+// ------------------------------------------------------------ fused BN
+namespace {
+bool bn_ok(const at::Tensor& t) {
+  return t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.dim() == 4 &&
+         t.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+         (reinterpret_cast<uintptr_t>(t.data_ptr()) % 16) == 0;
+}
+const float* opt_f(const c10::optional<at::Tensor>& t) {
+  return t.has_value() && t->defined() ? t->data_ptr<float>() : nullptr;
+}
+}  // namespace
+
+bool bn_act_supported(const at::Tensor& x) {
+  if (!bn_ok(x)) return false;
+  const int64_t C = x.size(1);
+  return C % 8 == 0 && C <= kfac::bn_max_c();
+}
+
+// x: [N, C, H, W] channels_last bf16.  Returns (y, stats[4, C] fp32).
+std::vector<at::Tensor> bn_act_forward(const at::Tensor& x,
+                                       const c10::optional<at::Tensor>& residual,
+                                       const c10::optional<at::Tensor>& weight,
+                                       const c10::optional<at::Tensor>& bias,
+                                       const c10::optional<at::Tensor>& running_mean,
+                                       const c10::optional<at::Tensor>& running_var,
+                                       const c10::optional<at::Tensor>& num_batches,
+                                       double momentum, double eps, bool relu) {
+  TORCH_CHECK(bn_act_supported(x), "bn_act_forward: unsupported input");
+  const int64_t C = x.size(1), M = x.numel() / C;
+  const bool has_res = residual.has_value() && residual->defined();
+  if (has_res) {
+    TORCH_CHECK(bn_ok(*residual) && residual->sizes() == x.sizes(), "residual layout");
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  int64_t rpb;
+  int nblk;
+  kfac::bn_partition(M, (int)C, &rpb, &nblk);
+  auto fopts = x.options().dtype(at::kFloat);
+  auto part = at::empty({(int64_t)nblk * 2 * C}, fopts);
+  auto stats = at::empty({4, C}, fopts);
+  auto y = at::empty_like(x, at::MemoryFormat::ChannelsLast);
+  int64_t* nb = nullptr;
+  if (num_batches.has_value() && num_batches->defined()) {
+    TORCH_CHECK(num_batches->scalar_type() == at::kLong && num_batches->is_cuda());
+    nb = num_batches->data_ptr<int64_t>();
+  }
+  float* rm = running_mean.has_value() && running_mean->defined()
+                  ? running_mean->data_ptr<float>() : nullptr;
+  float* rv = running_var.has_value() && running_var->defined()
+                  ? running_var->data_ptr<float>() : nullptr;
+  kfac::bn_forward(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                   has_res ? reinterpret_cast<const uint16_t*>(residual->data_ptr()) : nullptr,
+                   opt_f(weight), opt_f(bias), rm, rv, nb, (float)momentum, (float)eps,
+                   relu ? 1 : 0, M, (int)C, part.data_ptr<float>(), stats.data_ptr<float>(),
+                   reinterpret_cast<uint16_t*>(y.data_ptr()), cur_stream());
+  return {y, stats};
+}
+
+// Returns (dx, dweight, dbias, dresidual-or-undefined).
+std::vector<at::Tensor> bn_act_backward(const at::Tensor& x, const at::Tensor& dy,
+                                        const at::Tensor& y,
+                                        const c10::optional<at::Tensor>& weight,
+                                        const at::Tensor& stats, bool relu,
+                                        bool has_res) {
+  TORCH_CHECK(bn_act_supported(x) && stats.is_contiguous());
+  const int64_t C = x.size(1), M = x.numel() / C;
+  at::Tensor g = dy;
+  if (!bn_ok(g)) g = dy.to(at::kBFloat16).contiguous(at::MemoryFormat::ChannelsLast);
+  TORCH_CHECK(bn_ok(y));
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  int64_t rpb;
+  int nblk;
+  kfac::bn_partition(M, (int)C, &rpb, &nblk);
+  auto fopts = x.options().dtype(at::kFloat);
+  auto part = at::empty({(int64_t)nblk * 2 * C}, fopts);
+  auto coef = at::empty({3, C}, fopts);
+  auto dw = at::empty({C}, fopts), db = at::empty({C}, fopts);
+  auto dx = at::empty_like(x, at::MemoryFormat::ChannelsLast);
+  at::Tensor dres;
+  if (has_res) dres = at::empty_like(x, at::MemoryFormat::ChannelsLast);
+  kfac::bn_backward(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                    reinterpret_cast<const uint16_t*>(g.data_ptr()),
+                    reinterpret_cast<const uint16_t*>(y.data_ptr()), opt_f(weight),
+                    stats.data_ptr<float>(), relu ? 1 : 0, M, (int)C,
+                    part.data_ptr<float>(), coef.data_ptr<float>(), dw.data_ptr<float>(),
+                    db.data_ptr<float>(), reinterpret_cast<uint16_t*>(dx.data_ptr()),
+                    has_res ? reinterpret_cast<uint16_t*>(dres.data_ptr()) : nullptr,
+                    cur_stream());
+  return {dx, dw, db, dres};
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "MI355X (gfx950) HIP kernels for distributed K-FAC";
   m.def("triu_pack", &triu_pack);
@@ -601,6 +704,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   // GIL released: several host threads can each drive rocSOLVER on their
   // own stream (rocSOLVER's syevd blocks its calling thread internally)
   m.def("sytrd_max_n", &sytrd_max_n);
+  m.def("bn_act_supported", &bn_act_supported);
+  m.def("bn_act_forward", &bn_act_forward);
+  m.def("bn_act_backward", &bn_act_backward);
   m.def("spd_lds_max_n", &spd_lds_max_n);
   m.def("spd_inverse", &spd_inverse, py::call_guard<py::gil_scoped_release>());
   m.def("sytrd_reduce", &sytrd_reduce, py::call_guard<py::gil_scoped_release>());

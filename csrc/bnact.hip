@@ -1,0 +1,379 @@
+// Fused training-mode BatchNorm2d (+ residual add) (+ ReLU) for NHWC bf16
+// activations, forward and backward, for the ResNet models.
+//
+// Why: in a ResNet-50 step at batch 32 on MI355X the BatchNorm family is
+// the largest non-conv cost: MIOpen's 3 forward + 3 backward BN kernels,
+// ~2 MIOpen tensor-op kernels, a separate ReLU forward and backward, the
+// residual add and the num_batches_tracked increment come to ~4.7 ms of a
+// 9.3 ms busy step (profiles/rocprof_steady_sgd_r1_final.txt) for what is
+// a few memory passes over each activation.  Here one BN layer is
+//   forward : stats partials -> finalize (running stats, counter, scale /
+//             shift) -> apply (x*scale + shift [+ residual], ReLU, bf16)
+//   backward: partials of dz = dy*(y > 0) and dz*(x - mean) -> finalize
+//             (dgamma, dbeta, dx coefficients) -> apply (dx [, d residual])
+// All passes move 16 B (8 channels of bf16) per thread per access, rows are
+// [N*H*W, C] with C % 8 == 0.  Statistics accumulate in fp32 per workgroup
+// and in fp64 across workgroups (E[x^2] - E[x]^2 in fp64 does not cancel).
+// Semantics follow torch.nn.functional.batch_norm (training=True): biased
+// variance to normalise, unbiased variance into running_var, momentum
+// update, num_batches_tracked += 1.
+#include "common.h"
+
+namespace kfac {
+
+namespace {
+
+constexpr int BN_T = 256;
+constexpr int BN_FIN_CH = 32;  // channels per finalize block
+constexpr int BN_FIN_L = 16;   // lanes splitting the partial blocks
+constexpr int BN_FIN_T = BN_FIN_CH * BN_FIN_L;
+
+typedef unsigned short us8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void load8(const uint16_t* p, float* v) {
+  const uint4 u = *reinterpret_cast<const uint4*>(p);
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(w[i] << 16);
+    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+
+__device__ __forceinline__ void store8(uint16_t* p, const float* v) {
+  uint4 u;
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    w[i] = (uint32_t)f32_to_bf16_bits(v[2 * i]) |
+           ((uint32_t)f32_to_bf16_bits(v[2 * i + 1]) << 16);
+  u.x = w[0];
+  u.y = w[1];
+  u.z = w[2];
+  u.w = w[3];
+  *reinterpret_cast<uint4*>(p) = u;
+}
+
+// Per-block channel partial sums.  mode 0 (forward): s0 = sum x,
+// s1 = sum x^2.  mode 1 (backward): dz = dy * (y > 0 | !relu),
+// s0 = sum dz, s1 = sum dz * (x - mean).
+template <int MODE>
+__global__ void __launch_bounds__(BN_T) bn_partial_kernel(
+    const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
+    const uint16_t* __restrict__ y, const float* __restrict__ mean, int relu,
+    int64_t M, int C, int64_t rows_per_block, float* __restrict__ part) {
+  extern __shared__ float sh[];  // [2][RPI][C]
+  const int tpr = C / 8;
+  const int rpi = BN_T / tpr;
+  const int cg = threadIdx.x % tpr, rs = threadIdx.x / tpr;
+  const int c0 = cg * 8;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  int64_t r1 = r0 + rows_per_block;
+  if (r1 > M) r1 = M;
+  float s0[8] = {}, s1[8] = {};
+  float mu[8] = {};
+  if (MODE == 1 && rs < rpi) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) mu[i] = mean[c0 + i];
+  }
+  if (rs < rpi) {
+    // U rows per iteration with independent loads: keeps enough 16-B loads
+    // in flight per thread to stream at HBM rate from ~400 workgroups
+    constexpr int U = MODE == 0 ? 8 : 4;
+    for (int64_t rb = r0 + rs; rb < r1; rb += U * (int64_t)rpi) {
+      float a[U][8], g[U][8], o[U][8];
+      bool ok[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t r = rb + (int64_t)u * rpi;
+        ok[u] = r < r1;
+        if (ok[u]) {
+          const int64_t off = r * C + c0;
+          load8(x + off, a[u]);
+          if (MODE == 1) {
+            load8(dy + off, g[u]);
+            if (relu) load8(y + off, o[u]);
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (!ok[u]) continue;
+        if (MODE == 0) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            s0[i] += a[u][i];
+            s1[i] += a[u][i] * a[u][i];
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const float gi = (!relu || o[u][i] > 0.f) ? g[u][i] : 0.f;
+            s0[i] += gi;
+            s1[i] += gi * (a[u][i] - mu[i]);
+          }
+        }
+      }
+    }
+  }
+  float* sh0 = sh;
+  float* sh1 = sh + rpi * C;
+  if (rs < rpi) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      sh0[rs * C + c0 + i] = s0[i];
+      sh1[rs * C + c0 + i] = s1[i];
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += BN_T) {
+    float a = 0.f, b = 0.f;
+    for (int q = 0; q < rpi; ++q) {
+      a += sh0[q * C + c];
+      b += sh1[q * C + c];
+    }
+    part[((int64_t)blockIdx.x * 2) * C + c] = a;
+    part[((int64_t)blockIdx.x * 2 + 1) * C + c] = b;
+  }
+}
+
+// fp64 reduction of the partials: 32 channels x 16 lanes per block.
+__device__ __forceinline__ void reduce_parts(const float* __restrict__ part, int nblk, int C,
+                                             int c, double& a, double& b) {
+  __shared__ double ra[BN_FIN_L][BN_FIN_CH], rb[BN_FIN_L][BN_FIN_CH];
+  const int lane = threadIdx.x / BN_FIN_CH, cl = threadIdx.x % BN_FIN_CH;
+  double sa = 0.0, sb = 0.0;
+  if (c < C) {
+    // 4 independent loads in flight per step (the finalize is latency bound)
+    int blk = lane;
+    for (; blk + 3 * BN_FIN_L < nblk; blk += 4 * BN_FIN_L) {
+      float va[4], vb[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        va[u] = part[((int64_t)(blk + u * BN_FIN_L) * 2) * C + c];
+        vb[u] = part[((int64_t)(blk + u * BN_FIN_L) * 2 + 1) * C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        sa += (double)va[u];
+        sb += (double)vb[u];
+      }
+    }
+    for (; blk < nblk; blk += BN_FIN_L) {
+      sa += (double)part[((int64_t)blk * 2) * C + c];
+      sb += (double)part[((int64_t)blk * 2 + 1) * C + c];
+    }
+  }
+  ra[lane][cl] = sa;
+  rb[lane][cl] = sb;
+  __syncthreads();
+  a = 0.0;
+  b = 0.0;
+#pragma unroll
+  for (int q = 0; q < BN_FIN_L; ++q) {
+    a += ra[q][cl];
+    b += rb[q][cl];
+  }
+}
+
+// stats[4][C]: mean, invstd, scale, shift
+__global__ void __launch_bounds__(BN_FIN_T) bn_fwd_finalize_kernel(
+    const float* __restrict__ part, int nblk, int64_t M, int C,
+    const float* __restrict__ weight, const float* __restrict__ bias,
+    float* __restrict__ running_mean, float* __restrict__ running_var,
+    int64_t* __restrict__ num_batches, float momentum, float eps,
+    float* __restrict__ stats) {
+  const int c = blockIdx.x * BN_FIN_CH + threadIdx.x % BN_FIN_CH;
+  double s, q;
+  reduce_parts(part, nblk, C, c, s, q);
+  if (threadIdx.x >= BN_FIN_CH || c >= C) return;
+  const double mean = s / (double)M;
+  double var = q / (double)M - mean * mean;
+  if (var < 0.0) var = 0.0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float w = weight ? weight[c] : 1.f;
+  const float b = bias ? bias[c] : 0.f;
+  const float scale = w * invstd;
+  stats[c] = (float)mean;
+  stats[C + c] = invstd;
+  stats[2 * C + c] = scale;
+  stats[3 * C + c] = b - (float)mean * scale;
+  if (running_mean) {
+    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
+    const double unb = M > 1 ? var * (double)M / (double)(M - 1) : var;
+    running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unb;
+  }
+  if (num_batches && c == 0) num_batches[0] += 1;
+}
+
+// Apply passes: each thread owns one 8-channel group for the whole launch
+// (per-channel constants in registers, no index division) and streams 4
+// rows per iteration with independent 16-B loads.
+__global__ void __launch_bounds__(BN_T) bn_fwd_apply_kernel(
+    const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
+    const float* __restrict__ stats, int relu, int64_t M, int C,
+    uint16_t* __restrict__ y) {
+  const int tpr = C / 8;
+  const int rpi = BN_T / tpr;
+  const int cg = threadIdx.x % tpr, rs = threadIdx.x / tpr;
+  if (rs >= rpi) return;
+  const int c0 = cg * 8;
+  float sc[8], sf[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    sc[i] = stats[2 * C + c0 + i];
+    sf[i] = stats[3 * C + c0 + i];
+  }
+  const int64_t step = (int64_t)gridDim.x * 4 * rpi;
+  for (int64_t rb = (int64_t)blockIdx.x * 4 * rpi + rs; rb < M; rb += step) {
+    float a[4][8], r[4][8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t row = rb + (int64_t)u * rpi;
+      if (row < M) {
+        load8(x + row * C + c0, a[u]);
+        if (res) load8(res + row * C + c0, r[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t row = rb + (int64_t)u * rpi;
+      if (row >= M) continue;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float o = a[u][i] * sc[i] + sf[i];
+        if (res) o += r[u][i];
+        a[u][i] = relu ? fmaxf(o, 0.f) : o;
+      }
+      store8(y + row * C + c0, a[u]);
+    }
+  }
+}
+
+// coef[3][C]: k1, k2, k3 with dx = k1*dz + k2 + k3*(x - mean)
+__global__ void __launch_bounds__(BN_FIN_T) bn_bwd_finalize_kernel(
+    const float* __restrict__ part, int nblk, int64_t M, int C,
+    const float* __restrict__ weight, const float* __restrict__ stats,
+    float* __restrict__ dweight, float* __restrict__ dbias, float* __restrict__ coef) {
+  const int c = blockIdx.x * BN_FIN_CH + threadIdx.x % BN_FIN_CH;
+  double sdz, sdzx;
+  reduce_parts(part, nblk, C, c, sdz, sdzx);
+  if (threadIdx.x >= BN_FIN_CH || c >= C) return;
+  const double invstd = stats[C + c];
+  const double w = weight ? weight[c] : 1.0;
+  if (dweight) dweight[c] = (float)(sdzx * invstd);
+  if (dbias) dbias[c] = (float)sdz;
+  const double k1 = w * invstd;
+  coef[c] = (float)k1;
+  coef[C + c] = (float)(-k1 * sdz / (double)M);
+  coef[2 * C + c] = (float)(-k1 * invstd * invstd * sdzx / (double)M);
+}
+
+__global__ void __launch_bounds__(BN_T) bn_bwd_apply_kernel(
+    const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
+    const uint16_t* __restrict__ y, const float* __restrict__ stats,
+    const float* __restrict__ coef, int relu, int64_t M, int C,
+    uint16_t* __restrict__ dx, uint16_t* __restrict__ dres) {
+  const int tpr = C / 8;
+  const int rpi = BN_T / tpr;
+  const int cg = threadIdx.x % tpr, rs = threadIdx.x / tpr;
+  if (rs >= rpi) return;
+  const int c0 = cg * 8;
+  float mu[8], k1[8], k2[8], k3[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    mu[i] = stats[c0 + i];
+    k1[i] = coef[c0 + i];
+    k2[i] = coef[C + c0 + i];
+    k3[i] = coef[2 * C + c0 + i];
+  }
+  const int64_t step = (int64_t)gridDim.x * 4 * rpi;
+  for (int64_t rb = (int64_t)blockIdx.x * 4 * rpi + rs; rb < M; rb += step) {
+    float a[4][8], g[4][8], o[4][8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t row = rb + (int64_t)u * rpi;
+      if (row < M) {
+        const int64_t off = row * C + c0;
+        load8(x + off, a[u]);
+        load8(dy + off, g[u]);
+        if (relu) load8(y + off, o[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t row = rb + (int64_t)u * rpi;
+      if (row >= M) continue;
+      const int64_t off = row * C + c0;
+      if (relu) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) g[u][i] = o[u][i] > 0.f ? g[u][i] : 0.f;
+      }
+      if (dres) store8(dres + off, g[u]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a[u][i] = k1[i] * g[u][i] + k2[i] + k3[i] * (a[u][i] - mu[i]);
+      store8(dx + off, a[u]);
+    }
+  }
+}
+
+int apply_grid(int64_t M, int C) {
+  const int rpi = BN_T / (C / 8);
+  int64_t g = ceil_div(M, 4 * (int64_t)rpi);
+  return (int)(g < 4096 ? (g > 0 ? g : 1) : 4096);
+}
+
+}  // namespace
+
+// rows per partial block and block count for [M, C]
+void bn_partition(int64_t M, int C, int64_t* rows_per_block, int* nblk) {
+  // ~400 workgroups on the big activations (8 / 4 rows of loads in flight
+  // per thread keep HBM busy; few partials keep the finalize short), at
+  // least 32 rows and one full unrolled iteration per workgroup
+  const int rpi = BN_T / (C / 8);
+  int64_t r = ceil_div(M, 400);
+  if (r < (int64_t)rpi * 8) r = (int64_t)rpi * 8;
+  if (r < 32) r = 32;
+  *rows_per_block = r;
+  *nblk = (int)ceil_div(M, r);
+}
+
+int bn_max_c() { return 8 * BN_T; }
+
+void bn_forward(const uint16_t* x, const uint16_t* res, const float* weight,
+                const float* bias, float* running_mean, float* running_var,
+                int64_t* num_batches, float momentum, float eps, int relu, int64_t M,
+                int C, float* part, float* stats, uint16_t* y, hipStream_t s) {
+  int64_t rpb;
+  int nblk;
+  bn_partition(M, C, &rpb, &nblk);
+  const int rpi = BN_T / (C / 8);
+  const size_t shm = (size_t)2 * rpi * C * sizeof(float);
+  hipLaunchKernelGGL(bn_partial_kernel<0>, dim3(nblk), dim3(BN_T), shm, s, x, nullptr,
+                     nullptr, nullptr, 0, M, C, rpb, part);
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((unsigned)ceil_div(C, BN_FIN_CH)),
+                     dim3(BN_FIN_T), 0, s, part, nblk, M, C, weight, bias, running_mean,
+                     running_var, num_batches, momentum, eps, stats);
+  hipLaunchKernelGGL(bn_fwd_apply_kernel, dim3(apply_grid(M, C)), dim3(BN_T), 0, s, x,
+                     res, stats, relu, M, C, y);
+}
+
+void bn_backward(const uint16_t* x, const uint16_t* dy, const uint16_t* y,
+                 const float* weight, const float* stats, int relu, int64_t M, int C,
+                 float* part, float* coef, float* dweight, float* dbias, uint16_t* dx,
+                 uint16_t* dres, hipStream_t s) {
+  int64_t rpb;
+  int nblk;
+  bn_partition(M, C, &rpb, &nblk);
+  const int rpi = BN_T / (C / 8);
+  const size_t shm = (size_t)2 * rpi * C * sizeof(float);
+  hipLaunchKernelGGL(bn_partial_kernel<1>, dim3(nblk), dim3(BN_T), shm, s, x, dy, y,
+                     stats, relu, M, C, rpb, part);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((unsigned)ceil_div(C, BN_FIN_CH)),
+                     dim3(BN_FIN_T), 0, s, part, nblk, M, C, weight, stats, dweight, dbias,
+                     coef);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(apply_grid(M, C)), dim3(BN_T), 0, s, x,
+                     dy, y, stats, coef, relu, M, C, dx, dres);
+}
+
+}  // namespace kfac

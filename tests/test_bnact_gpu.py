@@ -1,0 +1,92 @@
+"""Fused BatchNorm (+ residual) (+ ReLU) kernels (csrc/bnact.hip) vs the
+PyTorch fp32 math on the same bf16 inputs."""
+from __future__ import annotations
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from distributed_kfac_pytorch_amd.ops import bnact
+
+pytestmark = pytest.mark.gpu
+
+
+def _cl(t: torch.Tensor) -> torch.Tensor:
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+@pytest.mark.parametrize('shape', [(4, 64, 14, 14), (2, 256, 7, 9), (3, 2048, 4, 4),
+                                   (2, 16, 5, 5), (2, 24, 3, 3), (8, 128, 28, 28)])
+@pytest.mark.parametrize('relu', [True, False])
+@pytest.mark.parametrize('residual', [True, False])
+def test_bn_act_matches_reference(cuda, shape, relu, residual):
+    torch.manual_seed(sum(shape))
+    n, c, h, w = shape
+    x = _cl((torch.randn(shape, device=cuda) * 2 + 0.5).to(torch.bfloat16))
+    res = _cl(torch.randn(shape, device=cuda).to(torch.bfloat16)) if residual else None
+    dy = _cl(torch.randn(shape, device=cuda).to(torch.bfloat16))
+    bn = bnact.BatchNormAct2d(c).to(cuda)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+    ref_bn = torch.nn.BatchNorm2d(c).to(cuda)
+    ref_bn.load_state_dict(bn.state_dict())
+    assert bnact._fusable(bn, x, res)
+
+    xa = x.clone().requires_grad_(True)
+    ra = res.clone().requires_grad_(True) if residual else None
+    y = bn.act(xa, residual=ra, relu=relu)
+    y.backward(dy)
+
+    xr = x.float().requires_grad_(True)
+    rr = res.float().requires_grad_(True) if residual else None
+    yr = ref_bn(xr)
+    if residual:
+        yr = yr + rr
+    if relu:
+        yr = F.relu(yr)
+    yr.backward(dy.float())
+
+    assert y.dtype == torch.bfloat16 and y.is_contiguous(memory_format=torch.channels_last)
+    tol = 2e-2
+    assert (y.float() - yr).abs().max().item() <= tol * yr.abs().max().item() + 1e-2
+    gx = xr.grad.abs().max().item()
+    assert (xa.grad.float() - xr.grad).abs().max().item() <= tol * gx + 1e-3
+    assert torch.allclose(bn.weight.grad, ref_bn.weight.grad, rtol=1e-2, atol=1e-2)
+    assert torch.allclose(bn.bias.grad, ref_bn.bias.grad, rtol=1e-2, atol=1e-2)
+    if residual:
+        assert (ra.grad.float() - rr.grad).abs().max().item() <= 1e-2 * rr.grad.abs().max().item() + 1e-3
+    assert torch.allclose(bn.running_mean, ref_bn.running_mean, rtol=1e-4, atol=1e-5)
+    assert torch.allclose(bn.running_var, ref_bn.running_var, rtol=1e-4, atol=1e-5)
+    assert int(bn.num_batches_tracked) == int(ref_bn.num_batches_tracked) == 1
+
+
+def test_resnet50_fused_vs_unfused(cuda, monkeypatch):
+    """Whole ResNet-50 fwd+bwd: the fused-BN bf16 run must be at least about
+    as close to an fp32 run of the same weights as the PyTorch / MIOpen bf16
+    run is (the fused path rounds bn(x) + residual once, in fp32, instead of
+    rounding the BN output and the sum separately)."""
+    from distributed_kfac_pytorch_amd.models.resnet import resnet50
+
+    torch.manual_seed(0)
+    base = resnet50(num_classes=10).to(cuda).to(memory_format=torch.channels_last)
+    x = _cl(torch.randn(4, 3, 64, 64, device=cuda))
+    y = torch.randint(0, 10, (4,), device=cuda)
+    runs = {}
+    for name, fused, amp in (('fp32', '0', False), ('fused', '1', True), ('miopen', '0', True)):
+        model = resnet50(num_classes=10).to(cuda).to(memory_format=torch.channels_last)
+        model.load_state_dict(base.state_dict())
+        monkeypatch.setenv('KFAC_FUSED_BN', fused)
+        with torch.autocast('cuda', dtype=torch.bfloat16, enabled=amp):
+            loss = F.cross_entropy(model(x), y)
+        loss.backward()
+        runs[name] = (loss.item(), model.fc.weight.grad.clone(), model)
+    lr, fr, _ = runs['fp32']
+    dl_f = abs(runs['fused'][0] - lr)
+    dl_m = abs(runs['miopen'][0] - lr)
+    assert dl_f <= 1.5 * dl_m + 2e-2 * abs(lr), (dl_f, dl_m)
+    df = (runs['fused'][1] - fr).abs().max().item()
+    dm = (runs['miopen'][1] - fr).abs().max().item()
+    assert df <= 1.5 * dm + 1e-2 * fr.abs().max().item(), (df, dm)
+    nb = [b for n, b in runs['fused'][2].named_buffers() if n.endswith('num_batches_tracked')]
+    assert nb and all(int(b) == 1 for b in nb)
