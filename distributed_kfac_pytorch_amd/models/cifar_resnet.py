@@ -12,6 +12,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from distributed_kfac_pytorch_amd.ops.bnact import BatchNormAct2d
+
 __all__ = [
     'CifarResNet',
     'resnet20',
@@ -41,17 +43,18 @@ class _Block(nn.Module):
     def __init__(self, cin: int, cout: int, stride: int = 1) -> None:
         super().__init__()
         self.conv1 = nn.Conv2d(cin, cout, 3, stride=stride, padding=1, bias=False)
-        self.bn1 = nn.BatchNorm2d(cout)
+        self.bn1 = BatchNormAct2d(cout)
         self.conv2 = nn.Conv2d(cout, cout, 3, padding=1, bias=False)
-        self.bn2 = nn.BatchNorm2d(cout)
+        self.bn2 = BatchNormAct2d(cout)
         self.shortcut: nn.Module = nn.Identity()
         if stride != 1 or cin != cout:
             self.shortcut = _ShortcutA((cout - cin) // 2)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        y = F.relu(self.bn1(self.conv1(x)))
-        y = self.bn2(self.conv2(y))
-        return F.relu(y + self.shortcut(x))
+        # BN (+ shortcut) + ReLU: one fused native op in bf16 channels_last
+        # training (ops/bnact.py), the same math through PyTorch otherwise
+        y = self.bn1.act(self.conv1(x))
+        return self.bn2.act(self.conv2(y), residual=self.shortcut(x))
 
 
 class CifarResNet(nn.Module):
@@ -59,7 +62,7 @@ class CifarResNet(nn.Module):
         super().__init__()
         self.in_planes = 16
         self.conv1 = nn.Conv2d(3, 16, 3, padding=1, bias=False)
-        self.bn1 = nn.BatchNorm2d(16)
+        self.bn1 = BatchNormAct2d(16)
         self.layer1 = self._stage(16, num_blocks[0], 1)
         self.layer2 = self._stage(32, num_blocks[1], 2)
         self.layer3 = self._stage(64, num_blocks[2], 2)
@@ -76,7 +79,7 @@ class CifarResNet(nn.Module):
         return nn.Sequential(*mods)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        x = F.relu(self.bn1(self.conv1(x)))
+        x = self.bn1.act(self.conv1(x))
         x = self.layer3(self.layer2(self.layer1(x)))
         x = F.adaptive_avg_pool2d(x, 1).flatten(1)
         return self.linear(x)
