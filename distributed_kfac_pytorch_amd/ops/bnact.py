@@ -30,6 +30,9 @@ def _enabled() -> bool:
 
 
 class _BNActFunction(torch.autograd.Function):
+    """Python reference wrapper of the same kernels (tests compare the C++
+    autograd node ``native().bn_act`` against it)."""
+
     @staticmethod
     def forward(  # type: ignore[override]
         ctx: Any,
@@ -72,7 +75,8 @@ class _BNActFunction(torch.autograd.Function):
 
 
 def _fusable(bn: nn.BatchNorm2d, x: torch.Tensor, residual: torch.Tensor | None) -> bool:
-    if not (_enabled() and bn.training and bn.track_running_stats and bn.momentum is not None):
+    if not (_enabled() and bn.training and bn.track_running_stats and bn.momentum is not None
+            and bn.affine):
         return False
     if not x.is_cuda or x.dtype != torch.bfloat16:
         return False
@@ -95,9 +99,11 @@ def bn_act(
 ) -> torch.Tensor:
     """``relu(bn(x) + residual)`` (ReLU / residual optional)."""
     if _fusable(bn, x, residual):
-        return _BNActFunction.apply(
-            x, bn.weight, bn.bias, bn.running_mean, bn.running_var,
-            bn.num_batches_tracked, residual, relu, float(bn.momentum), float(bn.eps),
+        # C++ autograd node (csrc/bindings.cpp BNActFn): no Python in the
+        # forward or backward of the layer
+        return native().bn_act(
+            x, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var,
+            bn.num_batches_tracked, float(bn.momentum), float(bn.eps), relu,
         )
     y = bn(x)
     if residual is not None:

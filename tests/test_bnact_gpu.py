@@ -90,3 +90,28 @@ def test_resnet50_fused_vs_unfused(cuda, monkeypatch):
     assert df <= 1.5 * dm + 1e-2 * fr.abs().max().item(), (df, dm)
     nb = [b for n, b in runs['fused'][2].named_buffers() if n.endswith('num_batches_tracked')]
     assert nb and all(int(b) == 1 for b in nb)
+
+
+def test_cpp_node_matches_python_function(cuda):
+    """The C++ autograd node (native().bn_act) and the Python Function
+    wrapper run the same kernels: identical outputs and gradients."""
+    from distributed_kfac_pytorch_amd.ops._native import native
+
+    torch.manual_seed(1)
+    shape = (4, 128, 9, 9)
+    x = _cl(torch.randn(shape, device=cuda).to(torch.bfloat16))
+    res = _cl(torch.randn(shape, device=cuda).to(torch.bfloat16))
+    dy = _cl(torch.randn(shape, device=cuda).to(torch.bfloat16))
+    outs = []
+    for use_cpp in (True, False):
+        bn = bnact.BatchNormAct2d(128).to(cuda)
+        xa, ra = x.clone().requires_grad_(True), res.clone().requires_grad_(True)
+        args = (bn.running_mean, bn.running_var, bn.num_batches_tracked)
+        if use_cpp:
+            y = native().bn_act(xa, bn.weight, bn.bias, ra, *args, 0.1, 1e-5, True)
+        else:
+            y = bnact._BNActFunction.apply(xa, bn.weight, bn.bias, *args, ra, True, 0.1, 1e-5)
+        y.backward(dy)
+        outs.append((y, xa.grad, ra.grad, bn.weight.grad, bn.bias.grad, bn.running_var))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
