@@ -16,6 +16,7 @@ in every script (``examples/torch_cifar10_resnet.py:29-283``,
 from __future__ import annotations
 
 import argparse
+import atexit
 import datetime
 import os
 import random
@@ -92,6 +93,13 @@ def resolve_precision(args: argparse.Namespace) -> None:
         args.grad_scaler = None
 
 
+def _shutdown() -> None:
+    """Tear the process group down at exit (RCCL warns about leaked
+    communicators otherwise)."""
+    if dist.is_available() and dist.is_initialized():
+        dist.destroy_process_group()
+
+
 def init_distributed(args: argparse.Namespace) -> None:
     """Initialise the process group and the device of this rank.
 
@@ -118,6 +126,7 @@ def init_distributed(args: argparse.Namespace) -> None:
             kw['device_id'] = args.device
         dist.init_process_group(args.backend, init_method='env://',
                                 timeout=datetime.timedelta(minutes=30), **kw)
+        atexit.register(_shutdown)
     args.rank = dist.get_rank()
     args.world_size = dist.get_world_size()
     if args.verbose is None:
