@@ -503,11 +503,30 @@ std::tuple<at::Tensor, int64_t, at::Tensor> build_gemm_table(
     const std::vector<c10::optional<at::Tensor>>& dgs,
     const std::vector<c10::optional<at::Tensor>>& das,
     const std::vector<double>& dampings, bool a_kc, bool b_kc,
-    const c10::optional<at::Tensor>& host_buf) {
+    const c10::optional<at::Tensor>& host_buf,
+    const std::vector<c10::optional<at::Tensor>>& A_hls,
+    const std::vector<c10::optional<at::Tensor>>& B_hls) {
   const size_t n = As.size();
   TORCH_CHECK(A_extras.size() == n && Bs.size() == n && Cs.size() == n &&
               Ss.size() == n && dgs.size() == n && das.size() == n &&
               dampings.size() == n);
+  TORCH_CHECK(A_hls.empty() || A_hls.size() == n, "gemm3: A_hls size");
+  TORCH_CHECK(B_hls.empty() || B_hls.size() == n, "gemm3: B_hls size");
+  // pre-split operand: [rows, cols / 4, 8] bf16 (hi x4, lo x4 per group of
+  // 4 elements) matching a contiguous fp32 operand with cols % 4 == 0
+  auto hl = [](const c10::optional<at::Tensor>& t, const at::Tensor& op,
+               const uint16_t** h) {
+    *h = nullptr;
+    if (!t.has_value() || !t->defined()) return;
+    check_cuda(*t, "pre-split operand");
+    TORCH_CHECK(op.is_contiguous() && op.size(1) % 4 == 0,
+                "gemm3: pre-split needs a contiguous fp32 operand with cols % 4 == 0");
+    TORCH_CHECK(t->scalar_type() == at::kBFloat16 && t->dim() == 3 && t->is_contiguous() &&
+                    t->size(0) == op.size(0) && t->size(1) == op.size(1) / 4 &&
+                    t->size(2) == 8 && (reinterpret_cast<uintptr_t>(t->data_ptr()) % 16) == 0,
+                "gemm3: pre-split operand must be a contiguous [rows, cols/4, 8] bf16 tensor");
+    *h = reinterpret_cast<const uint16_t*>(t->data_ptr());
+  };
   std::vector<kfac::GemmDesc> host(n);
   for (size_t i = 0; i < n; ++i) {
     const auto& A = As[i];
@@ -554,6 +573,11 @@ std::tuple<at::Tensor, int64_t, at::Tensor> build_gemm_table(
     d.Kmain = (int32_t)Kmain;
     d.tiles_n = (int32_t)((N + 127) / 128);
     d.damping = (float)dampings[i];
+    if (!A_hls.empty()) {
+      hl(A_hls[i], A, &d.Ah);
+      TORCH_CHECK(d.Ah == nullptr || !extra, "gemm3: pre-split A cannot carry an extra column");
+    }
+    if (!B_hls.empty()) hl(B_hls[i], B, &d.Bh);
     d.vec = (vec_ok(A) ? 1 : 0) | (vec_ok(B) ? 2 : 0);
     host[i] = d;
   }
@@ -760,7 +784,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("build_gemm_table", &build_gemm_table, py::arg("As"), py::arg("A_extras"),
         py::arg("Bs"), py::arg("Cs"), py::arg("Ss"), py::arg("dgs"), py::arg("das"),
         py::arg("dampings"), py::arg("a_kc"), py::arg("b_kc"),
-        py::arg("host") = py::none());
+        py::arg("host") = py::none(),
+        py::arg("A_hls") = std::vector<c10::optional<at::Tensor>>(),
+        py::arg("B_hls") = std::vector<c10::optional<at::Tensor>>());
   m.def("gemm3_grouped", &gemm3_grouped);
   m.attr("arch") = "gfx950";
 }

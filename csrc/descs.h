@@ -29,6 +29,12 @@ struct GemmDesc {
   int32_t tiles_n, tile_start;
   float damping;
   int32_t vec;  // bit0: A float4 loads ok, bit1: B float4 loads ok
+  // optional pre-split operands: x = hi + lo (bf16) computed once per
+  // second-order update (the eigenbases are constant between updates),
+  // interleaved per 4 elements in the fp32 operand's layout, so the kernel
+  // stores them to LDS without the per-tile split
+  const uint16_t* Ah;
+  const uint16_t* Bh;
 };
 
 // syrk.hip implicit-im2col mode: the SYRK input rows are the patches of an

@@ -225,6 +225,64 @@ __device__ __forceinline__ void store_mc(const Stage& st, short* Lh, short* Ll) 
   }
 }
 
+// ---- pre-split operands: bf16 hi/lo interleaved per 4 consecutive
+// elements ([h0 h1 h2 h3 l0 l1 l2 l3] = 16 B, the footprint of 4 fp32), so
+// a group is read with the fp32 operand's float4 offsets and lands in a
+// Stage float4 as {hi01, hi23, lo01, lo23}.  Rows / k extents are multiples
+// of 4 (checked on the host), so groups never straddle an edge.
+__device__ __forceinline__ void load_kc_hl(Stage& st, const float* __restrict__ P, int64_t ld,
+                                           int rows, int r0, int kmain, int k0) {
+  const int t = threadIdx.x;
+  const int c = k0 + (t & 7) * 4;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int r = r0 + (t >> 3) + 32 * p;
+    st.r[p] = (r < rows && c < kmain) ? gload4(P + (int64_t)r * ld + c)
+                                      : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+__device__ __forceinline__ void load_mc_hl(Stage& st, const float* __restrict__ P, int64_t ld,
+                                           int cols, int m0, int K, int k0) {
+  const int t = threadIdx.x;
+  const int m = m0 + (t & 31) * 4;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int k = k0 + (t >> 5) + 8 * p;
+    st.r[p] = (k < K && m < cols) ? gload4(P + (int64_t)k * ld + m)
+                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+__device__ __forceinline__ void unpack_hl(const float4 v, v4i16& hi, v4i16& lo) {
+  hi = __builtin_bit_cast(v4i16, make_uint2(__float_as_uint(v.x), __float_as_uint(v.y)));
+  lo = __builtin_bit_cast(v4i16, make_uint2(__float_as_uint(v.z), __float_as_uint(v.w)));
+}
+
+__device__ __forceinline__ void store_kc_hl(const Stage& st, short* Lh, short* Ll) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int r = (t >> 3) + 32 * p;
+    v4i16 h, l;
+    unpack_hl(st.r[p], h, l);
+    *reinterpret_cast<v4i16*>(Lh + r * LDK + (t & 7) * 4) = h;
+    *reinterpret_cast<v4i16*>(Ll + r * LDK + (t & 7) * 4) = l;
+  }
+}
+
+__device__ __forceinline__ void store_mc_hl(const Stage& st, short* Lh, short* Ll) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int k = (t >> 5) + 8 * p;
+    v4i16 h, l;
+    unpack_hl(st.r[p], h, l);
+    *reinterpret_cast<v4i16*>(Lh + k * LDM + (t & 31) * 4) = h;
+    *reinterpret_cast<v4i16*>(Ll + k * LDM + (t & 31) * 4) = l;
+  }
+}
+
 // fragment: lane l gets X[row = base + (l & 31)][k = kk + 8 (l >> 5) + 0..7]
 __device__ __forceinline__ v8bf16 frag_kc(const short* L, int base, int kk) {
   const int l = threadIdx.x & 63;
@@ -276,6 +334,7 @@ gemm3_kernel(const GemmDesc* __restrict__ descs, int nlayers, int total_tiles) {
   const int m0 = (first_m + in_group % gm) * GT;
   const int n0 = (in_group / gm) * GT;
   const bool avec = d.vec & 1, bvec = (d.vec >> 1) & 1;
+  const bool a_hl = d.Ah != nullptr, b_hl = d.Bh != nullptr;
 
   const int w = threadIdx.x >> 6;
   const int l = threadIdx.x & 63;
@@ -302,20 +361,40 @@ gemm3_kernel(const GemmDesc* __restrict__ descs, int nlayers, int total_tiles) {
       }
       return;
     }
-    if constexpr (A_KC) load_kc(sa, d.A, d.A_extra, d.lda, d.M, m0, d.Kmain, k0, avec);
-    else load_mc(sa, d.A, d.lda, d.M, m0, d.K, k0, avec);
-    if constexpr (B_KC) load_kc(sb, d.B, nullptr, d.ldb, d.N, n0, d.K, k0, bvec);
-    else load_mc(sb, d.B, d.ldb, d.N, n0, d.K, k0, bvec);
+    if constexpr (A_KC) {
+      if (a_hl) load_kc_hl(sa, (const float*)d.Ah, d.lda, d.M, m0, d.Kmain, k0);
+      else load_kc(sa, d.A, d.A_extra, d.lda, d.M, m0, d.Kmain, k0, avec);
+    } else {
+      if (a_hl) load_mc_hl(sa, (const float*)d.Ah, d.lda, d.M, m0, d.K, k0);
+      else load_mc(sa, d.A, d.lda, d.M, m0, d.K, k0, avec);
+    }
+    if constexpr (B_KC) {
+      if (b_hl) load_kc_hl(sb, (const float*)d.Bh, d.ldb, d.N, n0, d.K, k0);
+      else load_kc(sb, d.B, nullptr, d.ldb, d.N, n0, d.K, k0, bvec);
+    } else {
+      if (b_hl) load_mc_hl(sb, (const float*)d.Bh, d.ldb, d.N, n0, d.K, k0);
+      else load_mc(sb, d.B, d.ldb, d.N, n0, d.K, k0, bvec);
+    }
   };
   auto store = [&](const Stage& sa, const Stage& sb, short* buf) {
     if constexpr (GEMM3_DIAG == 2) {
       if (sa.r[0].x == 12345.f && sb.r[3].w == 54321.f) buf[threadIdx.x] = 1;
       return;
     }
-    if constexpr (A_KC) store_kc(sa, buf, buf + A_SZ);
-    else store_mc(sa, buf, buf + A_SZ);
-    if constexpr (B_KC) store_kc(sb, buf + 2 * A_SZ, buf + 2 * A_SZ + B_SZ);
-    else store_mc(sb, buf + 2 * A_SZ, buf + 2 * A_SZ + B_SZ);
+    if constexpr (A_KC) {
+      if (a_hl) store_kc_hl(sa, buf, buf + A_SZ);
+      else store_kc(sa, buf, buf + A_SZ);
+    } else {
+      if (a_hl) store_mc_hl(sa, buf, buf + A_SZ);
+      else store_mc(sa, buf, buf + A_SZ);
+    }
+    if constexpr (B_KC) {
+      if (b_hl) store_kc_hl(sb, buf + 2 * A_SZ, buf + 2 * A_SZ + B_SZ);
+      else store_kc(sb, buf + 2 * A_SZ, buf + 2 * A_SZ + B_SZ);
+    } else {
+      if (b_hl) store_mc_hl(sb, buf + 2 * A_SZ, buf + 2 * A_SZ + B_SZ);
+      else store_mc(sb, buf + 2 * A_SZ, buf + 2 * A_SZ + B_SZ);
+    }
   };
   auto compute = [&](const short* cur) {
     const short* Ah = cur;

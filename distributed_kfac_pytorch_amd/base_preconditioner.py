@@ -33,6 +33,7 @@ from typing import Callable
 import torch
 
 from distributed_kfac_pytorch_amd import tracing
+from distributed_kfac_pytorch_amd.graphs import _no_gc
 from distributed_kfac_pytorch_amd.layers.base import KFACBaseLayer
 from distributed_kfac_pytorch_amd.layers.eigen import KFACEigenLayer
 from distributed_kfac_pytorch_amd.layers.inverse import KFACInverseLayer
@@ -196,10 +197,11 @@ class StepGraphs:
             side = torch.cuda.Stream()
             side.wait_stream(torch.cuda.current_stream())
             lanes = [] if grouped else self._lanes(workers)
-            with torch.cuda.stream(side):
+            with _no_gc(), torch.cuda.stream(side):
                 # thread_local: only this thread is barred from unsafe HIP
                 # calls while capturing -- RCCL's watchdog thread keeps
-                # querying its events (multi-rank jobs)
+                # querying its events (multi-rank jobs); no GC: a collected
+                # cycle holding an old graph would destroy it mid-capture
                 with torch.cuda.graph(g, stream=side, capture_error_mode='thread_local'):
                     if grouped:
                         pre._grouped.launch()
@@ -571,6 +573,12 @@ class BaseKFACPreconditioner:
                                 group=self._assignment.grad_worker_group(name),
                             )
             self._tdc.flush_allreduce_buckets()
+            # eigenbases changed: refresh their bf16 hi/lo planes for the
+            # grouped GEMMs now, eagerly (never inside a later graph capture)
+            if pops.presplit_enabled():
+                for name, layer in ordered:
+                    if isinstance(layer, KFACEigenLayer) and self._assignment.is_grad_worker(name):
+                        layer.q_split()
 
         inverse_step = self.steps % self.inv_update_steps == 0
         if self._graphs is None or not self._graphs.run(self, ordered, inverse_step):

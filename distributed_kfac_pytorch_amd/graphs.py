@@ -40,10 +40,13 @@ runner executes every step eagerly.
 """
 from __future__ import annotations
 
+import contextlib
+import gc
 import logging
 from collections import defaultdict
 from typing import Any
 from typing import Callable
+from typing import Iterator
 
 import torch
 import torch.distributed as dist
@@ -52,6 +55,19 @@ from distributed_kfac_pytorch_amd import tracing
 
 logger = logging.getLogger(__name__)
 
+
+
+@contextlib.contextmanager
+def _no_gc() -> Iterator[None]:
+    """Collect now, then keep the cyclic GC off for the block."""
+    gc.collect()
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
 
 class GraphedTrainStep:
     """Run (and graph-capture) a full training step.
@@ -181,7 +197,10 @@ class GraphedTrainStep:
         # ResNet-50 step) into this graph's private pool, where they stay
         # at fixed addresses for every replay.
         self.optimizer.zero_grad(set_to_none=True)
-        with torch.cuda.stream(side):
+        # no Python GC while capturing: collecting an unreachable cycle that
+        # holds an old CUDAGraph would destroy that graph mid-capture, which
+        # HIP forbids (hipErrorStreamCaptureUnsupported -> abort)
+        with _no_gc(), torch.cuda.stream(side):
             with torch.cuda.graph(g, stream=side):
                 loss = self.forward_backward()
                 if p is not None:

@@ -56,6 +56,11 @@ class KFACEigenLayer(KFACBaseLayer):
         self._dgda: torch.Tensor | FutureType | None = None
         self._tmp1: torch.Tensor | None = None
         self._tmp2: torch.Tensor | None = None
+        # bf16 hi/lo planes of QA / QG for the grouped GEMMs (q_split)
+        self._q_version = 0
+        self._split_version = -1
+        self._qa_hl: torch.Tensor | None = None
+        self._qg_hl: torch.Tensor | None = None
 
     # ------------------------------------------------------------ properties
     @property
@@ -66,6 +71,7 @@ class KFACEigenLayer(KFACBaseLayer):
     @qa.setter
     def qa(self, v: torch.Tensor | FutureType | None) -> None:
         self._qa = v
+        self._q_version += 1
 
     @property
     def qg(self) -> torch.Tensor | None:
@@ -75,6 +81,7 @@ class KFACEigenLayer(KFACBaseLayer):
     @qg.setter
     def qg(self, v: torch.Tensor | FutureType | None) -> None:
         self._qg = v
+        self._q_version += 1
 
     @property
     def da(self) -> torch.Tensor | None:
@@ -105,11 +112,51 @@ class KFACEigenLayer(KFACBaseLayer):
 
     def memory_usage(self) -> dict[str, int]:
         sizes = super().memory_usage()
-        sizes['a_inverses'] = _nbytes(self.qa) + _nbytes(self.da)
+        sizes['a_inverses'] = _nbytes(self.qa) + _nbytes(self.da) + _nbytes(self._qa_hl)
         sizes['g_inverses'] = (
-            _nbytes(self.qg) + _nbytes(self.dg) + _nbytes(self.dgda)
+            _nbytes(self.qg) + _nbytes(self.dg) + _nbytes(self.dgda) + _nbytes(self._qg_hl)
         )
         return sizes
+
+    @staticmethod
+    def _split_into(buf: torch.Tensor | None, q: torch.Tensor) -> torch.Tensor:
+        """q = hi + lo with hi = bf16_rn(q), lo = bf16_rn(q - hi) -- exactly
+        the split csrc/gemm3.hip applies per tile -- into a persistent
+        [rows, cols / 4, 8] bf16 buffer (hi x4, lo x4 per group of 4)."""
+        r, c = q.shape
+        shape = (r, c // 4, 8)
+        if buf is None or tuple(buf.shape) != shape or buf.device != q.device:
+            buf = torch.empty(shape, dtype=torch.bfloat16, device=q.device)
+        qv = q.view(r, c // 4, 4)
+        buf[:, :, :4].copy_(qv)
+        buf[:, :, 4:].copy_(qv - buf[:, :, :4].float())
+        return buf
+
+    def q_split(self) -> tuple[torch.Tensor, torch.Tensor] | None:
+        """Pre-split eigenbases for the grouped preconditioning GEMMs.
+
+        The eigenbases change only at second-order updates (or when they
+        are received by broadcast), so they are split into bf16 hi/lo
+        planes once per update instead of in every GEMM tile of every step;
+        the buffers keep their addresses (device tables, captured graphs).
+        """
+        qa, qg = self.qa, self.qg
+        if qa is None or qg is None or qa.dtype != torch.float32 or qg.dtype != torch.float32:
+            return None
+        if not (qa.is_cuda and qa.is_contiguous() and qg.is_contiguous()):
+            return None
+        if qa.shape[1] % 4 or qg.shape[1] % 4:
+            return None
+        if self._split_version != self._q_version or self._qa_hl is None or self._qg_hl is None:
+            if torch.cuda.is_current_stream_capturing():
+                # never allocate / refresh inside a HIP-graph capture (the
+                # buffers would live in the graph's private pool): the GEMMs
+                # split in-kernel until the next eager refresh
+                return None
+            self._qa_hl = self._split_into(self._qa_hl, qa)
+            self._qg_hl = self._split_into(self._qg_hl, qg)
+            self._split_version = self._q_version
+        return self._qa_hl, self._qg_hl
 
     # ------------------------------------------------------------ broadcasts
     def broadcast_a_inv(self, src: int, group: dist.ProcessGroup | None = None) -> None:

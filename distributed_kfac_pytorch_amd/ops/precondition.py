@@ -155,21 +155,33 @@ class _TableCache:
         self.per = slots_per_entry
         self._d: dict = {}
         self._free: list[torch.Tensor] = []
+        # entries a captured graph refers to (its kernels read the device
+        # table, its H2D copy re-reads the staging buffer): never evicted
+        self._sticky: set = set()
+
+    @staticmethod
+    def _capturing() -> bool:
+        return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
 
     def get(self, key: tuple) -> Any:
         v = self._d.pop(key, None)
         if v is not None:
             self._d[key] = v
+            if self._capturing():
+                self._sticky.add(key)
             return v[0]
         return None
 
     def reserve(self) -> list[torch.Tensor | None]:
         """Staging buffers for one new entry (None: let the builder
         allocate, which is only possible outside a capture)."""
-        while len(self._d) >= self.size:
-            _, (_, slots) = self._pop_oldest()
+        while len(self._d) - len(self._sticky) >= self.size:
+            victim = next((k for k in self._d if k not in self._sticky), None)
+            if victim is None:
+                break
+            _, slots = self._d.pop(victim)
             self._free += [t for t in slots if t is not None]
-        capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+        capturing = self._capturing()
         if not capturing and torch.cuda.is_available():
             # top up so that a later capture never has to allocate
             while len(self._free) < self.per * self.size:
@@ -179,12 +191,10 @@ class _TableCache:
             out.append(self._free.pop() if self._free else None)
         return out
 
-    def _pop_oldest(self) -> tuple:
-        k = next(iter(self._d))
-        return k, self._d.pop(k)
-
     def put(self, key: tuple, value: Any, slots: list) -> Any:
         self._d[key] = (value, slots)
+        if self._capturing():
+            self._sticky.add(key)
         return value
 
 
@@ -298,6 +308,10 @@ class MultiLayerApply:
         return True
 
 
+def presplit_enabled() -> bool:
+    return os.environ.get('KFAC_GEMM3_PRESPLIT', '0') == '1'
+
+
 def grouped_gemm_enabled() -> bool:
     """``KFAC_PRECOND_GEMM=torch`` keeps the per-layer hipBLASLt fp32 chain;
     the default is the grouped bf16x3 MFMA kernel (csrc/gemm3.hip)."""
@@ -371,6 +385,21 @@ class GroupedPrecondition:
             return ('inverse', wm, bg, a_inv, g_inv)
         return None
 
+    @staticmethod
+    def _splits(layer: Any) -> tuple | None:
+        """bf16 hi/lo planes of the layer's constant operands (eigenbases),
+        refreshed once per second-order update, or None.
+
+        Opt-in (``KFAC_GEMM3_PRESPLIT=1``): on MI355X the in-kernel split
+        measured the same within run-to-run noise (ResNet-50 plain graph step
+        8.88 / 9.11 ms pre-split vs 9.08 / 9.10 ms in-kernel, same box) --
+        the grouped GEMM is bound by its operand loads and LDS traffic, not
+        by the split -- and the planes cost as much memory as the bases."""
+        if not presplit_enabled():
+            return None
+        fn = getattr(layer, 'q_split', None)
+        return fn() if fn is not None else None
+
     def prepare(self, layers: list, damping: float) -> bool:
         lib = native()
         if lib is None or not layers or not grouped_gemm_enabled():
@@ -386,15 +415,19 @@ class GroupedPrecondition:
         for layer, (kind, wm, bg, fa, fg) in zip(layers, ops):
             g, a = fg.shape[0], fa.shape[0]
             dev = fa.device
+            hl = self._splits(layer) if kind == 'eigen' else None
+            qa_hl, qg_hl = hl if hl is not None else (None, None)
             t1 = layer._buf('_tmp1', (g, a), torch.float32, dev) if kind == 'eigen' \
                 else self._inv_tmp(layer, (g, a), dev)
             out = layer._grad_buffer(dev)
             if tuple(out.shape) != (g, a):
                 return False
             key.append((kind, wm.data_ptr(), None if bg is None else bg.data_ptr(),
-                        fa.data_ptr(), fg.data_ptr(), t1.data_ptr(), out.data_ptr(), g, a))
-            # T1: [Wg | bg] @ QA  (or A^-1)
-            t[0].append((wm, bg, fa, t1, None, None, None, 0.0))
+                        fa.data_ptr(), fg.data_ptr(), t1.data_ptr(), out.data_ptr(), g, a,
+                        None if qa_hl is None else (qa_hl.data_ptr(), qg_hl.data_ptr())))
+            # T1: [Wg | bg] @ QA  (or A^-1); rows: (A, A_extra, B, C, S, dg, da,
+            # damping, A_hl, B_hl)
+            t[0].append((wm, bg, fa, t1, None, None, None, 0.0, None, qa_hl))
             if kind == 'eigen':
                 t2 = layer._buf('_tmp2', (g, a), torch.float32, dev)
                 key.append((t2.data_ptr(), layer.prediv_eigenvalues,
@@ -402,13 +435,14 @@ class GroupedPrecondition:
                             None if layer.dg is None else layer.dg.data_ptr(),
                             None if layer.da is None else layer.da.data_ptr()))
                 if layer.prediv_eigenvalues:
-                    t[1].append((fg, None, t1, t2, layer.dgda, None, None, 0.0))
+                    t[1].append((fg, None, t1, t2, layer.dgda, None, None, 0.0, qg_hl, None))
                 else:
-                    t[1].append((fg, None, t1, t2, None, layer.dg, layer.da, float(damping)))
-                t[2].append((fg, None, t2, t1, None, None, None, 0.0))
-                t[3].append((t1, None, fa, out, None, None, None, 0.0))
+                    t[1].append((fg, None, t1, t2, None, layer.dg, layer.da, float(damping),
+                                 qg_hl, None))
+                t[2].append((fg, None, t2, t1, None, None, None, 0.0, qg_hl, None))
+                t[3].append((t1, None, fa, out, None, None, None, 0.0, None, qa_hl))
             else:
-                t[2].append((fg, None, t1, out, None, None, None, 0.0))
+                t[2].append((fg, None, t1, out, None, None, None, 0.0, None, None))
         key_t = tuple(key)
         if key_t != self._key:
             tables = self._cache.get(key_t)
@@ -424,7 +458,7 @@ class GroupedPrecondition:
                     tab, tiles, host = lib.build_gemm_table(
                         list(cols[0]), list(cols[1]), list(cols[2]), list(cols[3]),
                         list(cols[4]), list(cols[5]), list(cols[6]), list(cols[7]), akc, bkc,
-                        slot,
+                        slot, list(cols[8]), list(cols[9]),
                     )
                     tables.append((tab, len(rows), tiles, akc, bkc, host))
                 self._cache.put(key_t, tables, slots)

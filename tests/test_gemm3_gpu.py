@@ -139,3 +139,37 @@ def test_grouped_precondition_matches_torch_chain(cuda, monkeypatch, method, pre
             scale = b.abs().max().item()
             assert (a - b).abs().max().item() <= 1e-4 * scale + 1e-7, step
     assert pres[0]._grouped is not None and pres[0]._grouped._key is not None
+
+
+@pytest.mark.parametrize('a_kc', [True, False])
+@pytest.mark.parametrize('b_kc', [True, False])
+def test_presplit_operands_bitwise_equal(cuda, a_kc, b_kc):
+    """Pre-split bf16 hi/lo operands (eigenbases split once per update)
+    give exactly the result of the in-kernel split."""
+    lib = _lib()
+    torch.manual_seed(4)
+    shapes = [(64, 64, 64), (148, 2048, 36), (132, 96, 256), (36, 20, 8)]
+    As, Bs, C1, C2, Ahl, Bhl = [], [], [], [], [], []
+    for m, n, k in shapes:
+        A = torch.randn(m, k, device=cuda) if a_kc else torch.randn(k, m, device=cuda)
+        B = torch.randn(n, k, device=cuda) if b_kc else torch.randn(k, n, device=cuda)
+        for X, out in ((A, Ahl), (B, Bhl)):
+            r, c = X.shape
+            hl = torch.empty((r, c // 4, 8), dtype=torch.bfloat16, device=cuda)
+            xv = X.view(r, c // 4, 4)
+            hl[:, :, :4].copy_(xv)
+            hl[:, :, 4:].copy_(xv - hl[:, :, :4].float())
+            out.append(hl)
+        As.append(A)
+        Bs.append(B)
+        C1.append(torch.full((m, n), float('nan'), device=cuda))
+        C2.append(torch.full((m, n), float('nan'), device=cuda))
+    none = [None] * len(shapes)
+    zeros = [0.0] * len(shapes)
+    t1, n1, _ = lib.build_gemm_table(As, none, Bs, C1, none, none, none, zeros, a_kc, b_kc)
+    lib.gemm3_grouped(t1, len(As), n1, a_kc, b_kc)
+    t2, n2, _ = lib.build_gemm_table(As, none, Bs, C2, none, none, none, zeros, a_kc, b_kc,
+                                     None, Ahl, Bhl)
+    lib.gemm3_grouped(t2, len(As), n2, a_kc, b_kc)
+    for c1, c2 in zip(C1, C2):
+        assert torch.equal(c1, c2)
