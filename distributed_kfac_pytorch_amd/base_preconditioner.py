@@ -342,6 +342,14 @@ class BaseKFACPreconditioner:
         self._graphs: Any = None
         if os.environ.get('KFAC_GRAPHS', '1') != '0':
             self._graphs = StepGraphs()
+        # factor SYRKs (+ their all-reduce) run on a side stream forked from
+        # the hook's stream, so they overlap the rest of forward / backward;
+        # joined back before anything reads the factors (KFAC_FACTOR_STREAM=0:
+        # inline)
+        self._factor_streams: dict[Any, torch.cuda.Stream] = {}
+        self._factor_forked: set = set()
+        self._factor_inputs: list[tuple[torch.Tensor, int]] = []
+        self._factor_stream_off = False
         self._hook_handles: list[Any] = []
         for module in self._layers:
             self._hook_handles.append(
@@ -405,6 +413,7 @@ class BaseKFACPreconditioner:
     def state_dict(self, include_factors: bool = True) -> dict[str, Any]:
         """Reference-format state: steps, non-callable hyperparameters and
         (optionally) ``{'layers': {name: {'A': .., 'G': ..}}}``."""
+        self._join_factor_streams()
         sd: dict[str, Any] = {'steps': self.steps}
         for key in (
             'factor_update_steps',
@@ -430,6 +439,7 @@ class BaseKFACPreconditioner:
     ) -> None:
         """Restore ``state_dict``; optionally recompute (and broadcast) all
         second-order state from the loaded factors."""
+        self._join_factor_streams()
         self._steps = state_dict['steps']
         for key in (
             'factor_update_steps',
@@ -542,6 +552,7 @@ class BaseKFACPreconditioner:
     def step(self) -> None:
         """One K-FAC step: call after ``loss.backward()`` (gradients already
         averaged by DDP) and before ``optimizer.step()``."""
+        self._join_factor_streams()
         ordered = list(reversed(list(self._layers.values())))
         if (
             not self._update_factors_in_hook
@@ -685,11 +696,13 @@ class BaseKFACPreconditioner:
 
     def reset_batch(self) -> None:
         """Drop accumulated (not yet folded) factor contributions."""
+        self._join_factor_streams()
         for _, layer in self._layers.values():
             layer.reset_batch()
 
     def memory_usage(self) -> dict[str, int]:
         """Bytes held by K-FAC state on this rank, per category + total."""
+        self._join_factor_streams()
         self._tdc.flush_allreduce_buckets()
         sizes: dict[str, int] = defaultdict(int)
         for _, layer in self._layers.values():
@@ -717,6 +730,55 @@ class BaseKFACPreconditioner:
                 lambda g, m=module: self._save_grad_output(m, None, (g,)),
             )
 
+    def _factor_stream(self, t: torch.Tensor) -> torch.cuda.Stream | None:
+        if (not t.is_cuda or self._factor_stream_off
+                or os.environ.get('KFAC_FACTOR_STREAM', '1') == '0'):
+            return None
+        dev = t.device
+        s = self._factor_streams.get(dev)
+        if s is None:
+            s = torch.cuda.Stream(device=dev)
+            self._factor_streams[dev] = s
+        return s
+
+    def _join_factor_streams(self) -> None:
+        """Make the current stream wait for the factor side streams (every
+        reader of the factors calls this first)."""
+        if not self._factor_forked:
+            return
+        for dev in self._factor_forked:
+            torch.cuda.current_stream(dev).wait_stream(self._factor_streams[dev])
+        self._factor_forked = set()
+        # the side stream read each layer input / output gradient after the
+        # hook returned: if the model modified one in place meanwhile (the
+        # hazard the reference's input clone guards against), that factor
+        # contribution may be stale -- say so and go back to inline updates
+        changed = [t for t, v in self._factor_inputs if t._version != v]
+        self._factor_inputs = []
+        if changed and not self._factor_stream_off:
+            self._factor_stream_off = True
+            warnings.warn(
+                'a K-FAC layer input was modified in place after its forward '
+                'hook; factor updates now run inline on the compute stream '
+                '(KFAC_FACTOR_STREAM=0 avoids the side stream from the start)',
+                stacklevel=2,
+            )
+
+    def _on_factor_stream(self, t: torch.Tensor, fn: Callable[[], None]) -> None:
+        """Run ``fn`` (SYRK + EMA + all-reduce issue of one factor) on the
+        side stream after the work that produced ``t``; ``t`` is kept alive
+        for the side stream by the caching allocator."""
+        s = self._factor_stream(t)
+        if s is None:
+            fn()
+            return
+        s.wait_stream(torch.cuda.current_stream(t.device))
+        with torch.cuda.stream(s):
+            fn()
+        t.record_stream(s)
+        self._factor_inputs.append((t, t._version))
+        self._factor_forked.add(t.device)
+
     @torch.no_grad()
     def _save_input(self, module: torch.nn.Module, input: tuple[torch.Tensor, ...]) -> None:
         """Forward-hook body: A contribution (+ fused EMA and all-reduce)."""
@@ -730,6 +792,17 @@ class BaseKFACPreconditioner:
             self._update_factors_in_hook
             and self._mini_steps[name] % self._accumulation_steps == 0
         )
+        if in_hook and self._accumulation_steps == 1 and isinstance(input[0], torch.Tensor):
+            decay = self.factor_decay
+            group = self._assignment.factor_group(name, 'A')
+
+            def work() -> None:
+                with tracing.phase('factor_a'):
+                    layer.save_and_update_a(list(input), alpha=decay)
+                layer.reduce_a_factor(group)
+            self._on_factor_stream(input[0], work)
+            return
+        self._join_factor_streams()
         with tracing.phase('factor_a'):
             if in_hook and self._accumulation_steps == 1:
                 layer.save_and_update_a(list(input), alpha=self.factor_decay)
@@ -759,6 +832,18 @@ class BaseKFACPreconditioner:
             self._update_factors_in_hook
             and self._mini_steps[name] % self._accumulation_steps == 0
         )
+        if in_hook and self._accumulation_steps == 1 and isinstance(grad_output[0], torch.Tensor):
+            decay = self.factor_decay
+            group = self._assignment.factor_group(name, 'G')
+            go = grad_output
+
+            def work() -> None:
+                with tracing.phase('factor_g'):
+                    layer.save_and_update_g(go, alpha=decay)
+                layer.reduce_g_factor(group)
+            self._on_factor_stream(grad_output[0], work)
+            return
+        self._join_factor_streams()
         with tracing.phase('factor_g'):
             if in_hook and self._accumulation_steps == 1:
                 layer.save_and_update_g(grad_output, alpha=self.factor_decay)

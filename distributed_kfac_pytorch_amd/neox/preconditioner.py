@@ -235,6 +235,7 @@ class GPTNeoXKFACPreconditioner(BaseKFACPreconditioner):
     def state_dict(self, include_factors: bool = True) -> dict[str, Any]:
         """All ranks must enter.  Factors are collected from each layer's
         inverse worker and returned on every rank (CPU tensors)."""
+        self._join_factor_streams()
         sd = super().state_dict(include_factors=False)
         if not include_factors:
             return sd
@@ -263,6 +264,7 @@ class GPTNeoXKFACPreconditioner(BaseKFACPreconditioner):
 
     def load_state_dict(self, state_dict: dict[str, Any], compute_inverses: bool = True) -> None:
         """Restore hyperparameters; load factors on their primary ranks."""
+        self._join_factor_streams()
         state_dict = dict(state_dict)
         layers = state_dict.pop('layers', None)
         super().load_state_dict(state_dict, compute_inverses=False)
@@ -282,6 +284,7 @@ class GPTNeoXKFACPreconditioner(BaseKFACPreconditioner):
 
     def save_factors_to_dir(self) -> None:
         """Each inverse worker writes ``<dir>/<layer name>`` for its layers."""
+        self._join_factor_streams()
         if self.factor_checkpoint_dir is None:
             raise ValueError('factor_checkpoint_dir is None')
         if get_rank() == 0:
@@ -297,6 +300,7 @@ class GPTNeoXKFACPreconditioner(BaseKFACPreconditioner):
     def load_factors_from_dir(self, compute_inverses: bool = True) -> None:
         """Load per-layer factor files on the primary ranks (missing files
         are skipped)."""
+        self._join_factor_streams()
         if self.factor_checkpoint_dir is None:
             raise ValueError('factor_checkpoint_dir is None.')
         if not os.path.isdir(self.factor_checkpoint_dir):
