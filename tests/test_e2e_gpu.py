@@ -133,3 +133,33 @@ def test_graph_replay_matches_eager(cuda, prediv, method):
         for o in opts:
             o.step()
     assert pres[0]._graphs.replays > 0 and pres[0]._graphs.captures >= 1
+
+
+def test_factor_side_stream_matches_inline(cuda, monkeypatch):
+    """Factor SYRK/EMA on the hook side stream == inline on the compute
+    stream; an input mutated after its hook switches to inline updates."""
+    base = _net().to(cuda)
+    models = [copy.deepcopy(base), copy.deepcopy(base)]
+    pres = [
+        kfac.KFACPreconditioner(m, factor_update_steps=1, inv_update_steps=3, lr=0.1)
+        for m in models
+    ]
+    pres[1]._factor_stream_off = True  # inline reference
+    torch.manual_seed(3)
+    for _ in range(4):
+        x = torch.randn(8, 3, 14, 14, device=cuda)
+        y = torch.randint(0, 10, (8,), device=cuda)
+        for m, p in zip(models, pres):
+            m.zero_grad(set_to_none=False)
+            torch.nn.functional.cross_entropy(m(x), y).backward()
+            p.step()
+        assert pres[0]._factor_streams, 'side stream was not used'
+        for (_, la), (_, lb) in zip(pres[0]._layers.values(), pres[1]._layers.values()):
+            assert torch.allclose(la.a_factor, lb.a_factor, rtol=1e-5, atol=1e-6)
+            assert torch.allclose(la.g_factor, lb.g_factor, rtol=1e-5, atol=1e-6)
+    x = torch.randn(8, 3, 14, 14, device=cuda)
+    torch.nn.functional.cross_entropy(models[0](x), y).backward()
+    x.add_(1.0)  # first layer's input changes after its forward hook
+    with pytest.warns(UserWarning, match='modified in place'):
+        pres[0].step()
+    assert pres[0]._factor_stream_off
