@@ -53,10 +53,10 @@ constexpr int GNT = 256;  // threads per block
 constexpr int LDK = 40;   // k-contig LDS row (32 + 8 pad) in shorts
 constexpr int LDM = 160;  // m-contig LDS row (128 + 32 pad) in shorts
 #ifndef GEMM3_CH
-#define GEMM3_CH 16
+#define GEMM3_CH 4
 #endif
 #ifndef GEMM3_GM
-#define GEMM3_GM 4
+#define GEMM3_GM 8
 #endif
 constexpr int CH = GEMM3_CH;  // consecutive tiles per XCD chunk
 constexpr int GM = GEMM3_GM;  // tile rows per column group (L2 reuse)
