@@ -41,6 +41,7 @@ from distributed_kfac_pytorch_amd.ops import linalg
 from distributed_kfac_pytorch_amd.ops import precondition as pops
 from distributed_kfac_pytorch_amd.parallel.assignment import WorkAssignment
 from distributed_kfac_pytorch_amd.parallel.comm import get_rank
+from distributed_kfac_pytorch_amd.parallel.comm import get_world_size
 from distributed_kfac_pytorch_amd.parallel.comm import (
     TorchDistributedCommunicator,
 )
@@ -731,8 +732,14 @@ class BaseKFACPreconditioner:
             )
 
     def _factor_stream(self, t: torch.Tensor) -> torch.cuda.Stream | None:
-        if (not t.is_cuda or self._factor_stream_off
-                or os.environ.get('KFAC_FACTOR_STREAM', '1') == '0'):
+        # KFAC_FACTOR_STREAM: 1 force on, 0 force off, unset = single-process
+        # jobs only.  Multi-rank it stays inline: in the 2-rank rehearsal
+        # (profiles/fstream_w2_ab_mi355x.jsonl) the side stream made the
+        # factor phases 65-236 ms/step against <1 ms inline.
+        mode = os.environ.get('KFAC_FACTOR_STREAM', 'auto')
+        if not t.is_cuda or self._factor_stream_off or mode == '0':
+            return None
+        if mode != '1' and get_world_size() > 1:
             return None
         dev = t.device
         s = self._factor_streams.get(dev)
