@@ -54,6 +54,9 @@ from distributed_kfac_pytorch_amd.models.resnet import get_model  # noqa: E402
 # under the earlier harness settings).  For N GPUs the comparison point is
 # the reference's linear-scaling upper bound N * 753.96.
 REFERENCE_IMG_S_PER_GPU = 753.96
+# the reference's K-FAC-only cost on the same box and harness: 42.44 ms/step
+# with K-FAC minus 10.93 ms/step for its own SGD step
+REFERENCE_KFAC_OVERHEAD_MS = 31.51
 
 
 def parse_args() -> argparse.Namespace:
@@ -92,6 +95,8 @@ def parse_args() -> argparse.Namespace:
     p.add_argument('--profile-mark', action='store_true',
                    help='bracket the timed steps with marker kernels (rocprof windows)')
     p.add_argument('--lr', type=float, default=0.0125)
+    p.add_argument('--data-pool', type=int, default=8,
+                   help='distinct synthetic batches cycled through the input buffer')
     p.add_argument('--impl', default='native', choices=['native', 'reference'],
                    help='reference = time the upstream kfac_pytorch package '
                         'found on $KFAC_REFERENCE_PATH (same config) to '
@@ -177,11 +182,25 @@ def run(args: argparse.Namespace, use_kfac: bool, rank: int, world: int,
             compute_method='inverse' if args.kfac_inv_method else 'eigen',
             grad_worker_fraction=args.kfac_grad_worker_fraction,
         )
-    x = torch.randn(args.batch_size, 3, args.image_size, args.image_size,
-                    device=dev)
-    if cl:
-        x = x.contiguous(memory_format=torch.channels_last)
-    y = torch.randint(0, 1000, (args.batch_size,), device=dev)
+    # a pool of distinct synthetic batches, cycled through one static input
+    # buffer (graph replays read it): the K-FAC factors see batch-to-batch
+    # variation as with real data, so eigenbasis warm starts are not
+    # flattered by a constant batch
+    fmt = torch.channels_last if cl else torch.contiguous_format
+    pool_x = [torch.randn(args.batch_size, 3, args.image_size, args.image_size,
+                          device=dev).contiguous(memory_format=fmt)
+              for _ in range(max(1, args.data_pool))]
+    pool_y = [torch.randint(0, 1000, (args.batch_size,), device=dev)
+              for _ in range(max(1, args.data_pool))]
+    x = torch.empty_like(pool_x[0])
+    y = torch.empty_like(pool_y[0])
+    counter = [0]
+
+    def next_batch() -> None:
+        i = counter[0] % len(pool_x)
+        counter[0] += 1
+        x.copy_(pool_x[i])
+        y.copy_(pool_y[i])
     crit = torch.nn.CrossEntropyLoss(label_smoothing=0.1)
     amp = not args.fp32
 
@@ -200,6 +219,7 @@ def run(args: argparse.Namespace, use_kfac: bool, rank: int, world: int,
         runner = GraphedTrainStep(forward_backward, opt, precond)
 
     def step() -> None:
+        next_batch()
         if runner is not None:
             runner()
             return
@@ -209,27 +229,74 @@ def run(args: argparse.Namespace, use_kfac: bool, rank: int, world: int,
             precond.step()
         opt.step()
 
+    def kind() -> str:
+        if precond is None:
+            return 'plain'
+        st = precond.steps
+        if st % precond.inv_update_steps == 0:
+            return 'inverse'
+        if st % precond.factor_update_steps == 0:
+            return 'factor'
+        return 'plain'
+
     for _ in range(args.warmup):
         step()
+    # Align the timed window to the K-FAC schedule: it starts ON a
+    # second-order update step, so every window (whatever --steps is)
+    # contains at least one eigendecomposition/inversion refresh.  The
+    # alignment steps are untimed warmup.
+    align = 0
+    if precond is not None:
+        while precond.steps % precond.inv_update_steps != 0:
+            step()
+            align += 1
     timer = None
     if args.phase_timing and precond is not None:
         timer = tracing.enable_phase_timing(True)
     marker = _profile_marker(dev) if args.profile_mark else None
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    kinds: list[str] = []
     barrier_sync(world)
     if marker is not None:
         marker()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        kinds.append(kind())
+        ev[i].record()
         step()
+    ev[args.steps].record()
     if marker is not None:
         marker()
     barrier_sync(world)
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+    # per-step GPU-timeline intervals (no per-step host sync)
+    per_step = [ev[i].elapsed_time(ev[i + 1]) for i in range(args.steps)]
+    by_kind = {}
+    for k in ('plain', 'factor', 'inverse'):
+        v = [t for t, kk in zip(per_step, kinds) if kk == k]
+        by_kind[k] = (sum(v) / len(v)) if v else 0.0
+    t = torch.tensor([elapsed, by_kind['plain'], by_kind['factor'], by_kind['inverse']],
+                     device=dev, dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
-    out = {'seconds': elapsed, 'ms_per_step': elapsed / args.steps * 1e3}
+    elapsed = float(t[0].item())
+    by_kind = {'plain': float(t[1]), 'factor': float(t[2]), 'inverse': float(t[3])}
+    out = {'seconds': elapsed, 'ms_per_step': elapsed / args.steps * 1e3,
+           'kind_ms': {k: round(v, 3) for k, v in by_kind.items() if v > 0.0},
+           'kind_counts': {k: kinds.count(k) for k in ('plain', 'factor', 'inverse')},
+           'align_steps': align}
+    if precond is not None:
+        # period-averaged step time at the reference cadence: one refresh,
+        # (inv/factor - 1) factor-update steps and the rest plain steps per
+        # inv_update_steps period, each at its in-window measured time
+        inv_p, f_p = precond.inv_update_steps, precond.factor_update_steps
+        n_factor = len([s for s in range(1, inv_p) if s % f_p == 0])
+        n_plain = inv_p - 1 - n_factor
+        tf = by_kind['factor'] or by_kind['plain']
+        out['period_ms_per_step'] = (
+            by_kind['inverse'] + n_factor * tf + n_plain * by_kind['plain']
+        ) / inv_p
+        out['refresh_ms'] = by_kind['inverse'] - by_kind['plain']
     if timer is not None:
         out['phase_ms_per_step'] = {
             k: v / args.steps for k, v in timer.summary().items()
@@ -264,7 +331,11 @@ def main() -> None:
     if args.baseline and not args.no_kfac:
         base = run(args, False, rank, world, dev)
     gb = args.batch_size * world
-    value = gb * args.steps / res['seconds']
+    window_value = gb * args.steps / res['seconds']
+    # headline: period-averaged throughput (the reference baseline was timed
+    # over whole 100-step periods); without K-FAC the window value
+    ms = res.get('period_ms_per_step', res['ms_per_step'])
+    value = gb * 1e3 / ms
     line = {
         'impl': args.impl,
         'metric': 'images/sec (whole node), ResNet-50 ImageNet K-FAC training',
@@ -273,7 +344,7 @@ def main() -> None:
         'n_gpus': world,
         'steps': args.steps,
         'warmup': args.warmup,
-        'ms_per_step': round(res['ms_per_step'], 3),
+        'ms_per_step': round(ms, 3),
         'higher_is_better': True,
         'scaling': 'weak',
         'vs_baseline': round(value / (REFERENCE_IMG_S_PER_GPU * world), 4),
@@ -297,17 +368,32 @@ def main() -> None:
             },
             'channels_last': not args.no_channels_last,
         },
+        'timing': (
+            'period-averaged: the timed window of exactly `steps` steps starts on '
+            'a second-order update step; ms_per_step = (refresh step + factor '
+            'steps + plain steps of one inv_update_steps period, each at its '
+            'in-window time) / period' if not args.no_kfac else 'window average'
+        ),
+        'window_ms_per_step': round(res['ms_per_step'], 3),
+        'window_images_per_sec': round(window_value, 2),
+        'inverse_steps_timed': res['kind_counts']['inverse'],
+        'kind_ms': res['kind_ms'],
+        'kind_counts': res['kind_counts'],
     }
+    if 'refresh_ms' in res:
+        line['eigen_refresh_ms' if not args.kfac_inv_method else 'inverse_refresh_ms'] = round(
+            res['refresh_ms'], 3)
     if base is not None:
         line['sgd_ms_per_step'] = round(base['ms_per_step'], 3)
         line['sgd_images_per_sec'] = round(gb * args.steps / base['seconds'], 2)
-        line['kfac_overhead_ms'] = round(
-            res['ms_per_step'] - base['ms_per_step'], 3,
-        )
+        line['kfac_overhead_ms'] = round(ms - base['ms_per_step'], 3)
+        # the reference kfac_pytorch on the same MI355X and harness
+        # (profiles/bench_reference_impl_mi355x_1gpu_r1c.json)
+        line['reference_kfac_overhead_ms'] = REFERENCE_KFAC_OVERHEAD_MS
     if base is not None and 'step_graphs' in base:
         line['sgd_step_graphs'] = base['step_graphs']
     for k in ('phase_ms_per_step', 'phase_counts', 'kfac_layers', 'step_graphs',
-              'kfac_memory_mb', 'kfac_steps_end'):
+              'kfac_memory_mb', 'kfac_steps_end', 'align_steps'):
         if k in res:
             line[k] = res[k]
     if rank == 0:

@@ -25,9 +25,11 @@ void scale_copy(int dtype, const void* src, void* dst, int64_t n, float scale,
                 hipStream_t s);
 // syrk.hip
 int64_t syrk_workspace_splits(int64_t N, int64_t D);
+int64_t syrk_workspace_floats(int64_t D, int64_t splits);
 void syrk(int in_dtype, const void* x, int64_t N, int64_t K, int64_t ldx,
           bool bias, float* C, int64_t D, int64_t ldc, float alpha,
-          float beta, int splits, hipStream_t s, const ConvGeom* geom = nullptr);
+          float beta, int splits, hipStream_t s, const ConvGeom* geom,
+          float* ws);
 // im2col.hip
 void im2col_nhwc(int dtype, const void* x, int64_t B, int64_t H, int64_t W,
                  int64_t C, int64_t sB, int64_t sH, int64_t sW, int kh, int kw,
@@ -62,8 +64,8 @@ void jacobi_eigh_batched(const float* A, int64_t n, int64_t batch,
 int64_t multi_blocks_for(int64_t rows, int64_t cols);
 void kl_dot_multi(const LayerDesc* descs, int nlayers, int64_t total_blocks,
                   double* acc, hipStream_t s);
-void kl_finalize_dev(double* acc, const float* params, float* scale,
-                     hipStream_t s);
+void kl_finalize_dev(const double* acc, int64_t nparts, const float* params,
+                     float* scale, hipStream_t s);
 void apply_multi(const LayerDesc* descs, int nlayers, int64_t total_blocks,
                  const float* scale, hipStream_t s);
 // gemm3.hip
@@ -155,6 +157,14 @@ void scale_copy(at::Tensor& dst, const at::Tensor& src, double scale) {
 }
 
 // ---------------------------------------------------------------- syrk
+// Split-K partial-tile workspace (stream-ordered caching-allocator memory;
+// inside a HIP-graph capture it comes from the graph's private pool).
+at::Tensor syrk_ws(const at::Tensor& C, int64_t D, int64_t splits) {
+  const int64_t n = kfac::syrk_workspace_floats(D, splits);
+  if (n == 0) return at::Tensor();
+  return at::empty({n}, C.options());
+}
+
 // C[D,D] = beta*C + alpha * Xt^T Xt, Xt = [X | 1] when bias.
 void syrk(const at::Tensor& x, at::Tensor& C, bool bias, double alpha,
           double beta, int64_t splits) {
@@ -173,9 +183,10 @@ void syrk(const at::Tensor& x, at::Tensor& C, bool bias, double alpha,
   const int64_t ldx = N > 1 ? x.stride(0) : K;
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   int sp = splits > 0 ? (int)splits : (int)kfac::syrk_workspace_splits(N, D);
+  at::Tensor ws = syrk_ws(C, D, sp);
   kfac::syrk(dtype_tag(x), x.data_ptr(), N, K, ldx, bias,
              C.data_ptr<float>(), D, C.stride(0), (float)alpha, (float)beta,
-             sp, cur_stream());
+             sp, cur_stream(), nullptr, ws.defined() ? ws.data_ptr<float>() : nullptr);
 }
 
 // C[D,D] = beta*C + alpha * P^T P with P the (implicit) patch matrix of an
@@ -211,8 +222,10 @@ void syrk_conv(const at::Tensor& x, at::Tensor& C, int64_t kh, int64_t kw,
                    (int32_t)ph, (int32_t)pw, (int32_t)OH, (int32_t)OW};
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   int sp = splits > 0 ? (int)splits : (int)kfac::syrk_workspace_splits(N, D);
+  at::Tensor ws = syrk_ws(C, D, sp);
   kfac::syrk(dtype_tag(x), x.data_ptr(), N, K, /*ldx=*/K, bias, C.data_ptr<float>(), D,
-             C.stride(0), (float)alpha, (float)beta, sp, cur_stream(), &g);
+             C.stride(0), (float)alpha, (float)beta, sp, cur_stream(), &g,
+             ws.defined() ? ws.data_ptr<float>() : nullptr);
 }
 
 // --------------------------------------------------------------- im2col
@@ -445,22 +458,24 @@ std::tuple<at::Tensor, int64_t, at::Tensor> build_layer_table(
   return {dev_t, blocks, cpu};
 }
 
+// acc: >= total_blocks fp64 partial sums (one per block, no atomics)
 void kl_dot_multi(const at::Tensor& table, int64_t nlayers,
                   int64_t total_blocks, at::Tensor& acc) {
-  TORCH_CHECK(acc.scalar_type() == at::kDouble && acc.numel() == 256 && acc.is_contiguous(),
-              "kl_dot_multi: acc must be 256 contiguous fp64 partial sums");
+  TORCH_CHECK(acc.scalar_type() == at::kDouble && acc.numel() >= total_blocks &&
+                  acc.is_contiguous(),
+              "kl_dot_multi: acc must hold one contiguous fp64 partial per block");
   c10::hip::HIPGuardMasqueradingAsCUDA g(acc.device());
   kfac::kl_dot_multi((const kfac::LayerDesc*)table.data_ptr(), (int)nlayers,
                      total_blocks, acc.data_ptr<double>(), cur_stream());
 }
 
-void kl_finalize_dev(at::Tensor& acc, const at::Tensor& params,
+void kl_finalize_dev(const at::Tensor& acc, int64_t nparts, const at::Tensor& params,
                      at::Tensor& scale) {
-  TORCH_CHECK(acc.scalar_type() == at::kDouble && acc.numel() == 256 &&
+  TORCH_CHECK(acc.scalar_type() == at::kDouble && acc.numel() >= nparts &&
               params.scalar_type() == at::kFloat &&
               scale.scalar_type() == at::kFloat);
   c10::hip::HIPGuardMasqueradingAsCUDA g(acc.device());
-  kfac::kl_finalize_dev(acc.data_ptr<double>(), params.data_ptr<float>(),
+  kfac::kl_finalize_dev(acc.data_ptr<double>(), nparts, params.data_ptr<float>(),
                         scale.data_ptr<float>(), cur_stream());
 }
 

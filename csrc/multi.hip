@@ -5,8 +5,11 @@
 // contiguous chain (base_preconditioner.py:409-433, layers/base.py:406-422).
 // ResNet-50 has 54 K-FAC layers: one launch per layer per op is ~110 small
 // launches per step on the critical path.  Here a step issues three:
-//   kl_dot_multi    acc += sum_l <P_l, [Wg_l | bg_l]>      (fp64 atomics)
-//   kl_finalize_dev scale = min(1, sqrt(kl_clip / |acc * lr^2|)), acc = 0
+//   kl_dot_multi    part[b] = block b's share of sum_l <P_l, [Wg_l | bg_l]>
+//   kl_finalize_dev scale = min(1, sqrt(kl_clip / |sum_b part[b] * lr^2|))
+// The per-block fp64 partials are summed in a fixed order (no atomics), so
+// the KL-clip scale -- and every gradient it multiplies -- is bitwise
+// reproducible run to run and between graph replay and eager execution.
 //   apply_multi     [Wg_l | bg_l] = scale * P_l
 // Layers are described by a device-resident descriptor table; each block
 // finds its layer by binary search over the per-layer block prefix sums.
@@ -22,7 +25,7 @@ namespace {
 
 constexpr int MT = 256;
 constexpr int EPT = 8;  // elements per thread per block
-constexpr int KL_SLOTS = 256;  // KL partial-sum accumulators (see kl_dot)
+constexpr int KL_RED = 256;  // threads of the partial-sum reduction
 
 // The table's pointers are generic to the compiler; address-space-1 casts
 // make the accesses global_load/store instead of FLAT (which also count on
@@ -88,26 +91,24 @@ kl_dot_multi_kernel(const LayerDesc* __restrict__ descs, int nlayers,
     double t = 0.0;
 #pragma unroll
     for (int w = 0; w < MT / 64; ++w) t += part[w];
-    // spread over KL_SLOTS accumulators: ~26k blocks adding into ONE
-    // address serialise on the L2 atomic unit (0.17 ms for ResNet-50)
-    if (t != 0.0) atomicAdd(&acc[blockIdx.x % KL_SLOTS], t);
+    acc[blockIdx.x] = t;  // one slot per block: no atomics, fixed order
   }
 }
 
-// params: [0] kl_clip, [1] lr.  acc: KL_SLOTS partial sums (zeroed here).
-__global__ void __launch_bounds__(KL_SLOTS)
-kl_finalize_dev_kernel(double* __restrict__ acc, const float* __restrict__ params,
-                       float* __restrict__ scale) {
-  __shared__ double part[KL_SLOTS / 64];
-  double v = acc[threadIdx.x];
-  acc[threadIdx.x] = 0.0;
+// params: [0] kl_clip, [1] lr.  acc: nparts per-block partial sums.
+__global__ void __launch_bounds__(KL_RED)
+kl_finalize_dev_kernel(const double* __restrict__ acc, int64_t nparts,
+                       const float* __restrict__ params, float* __restrict__ scale) {
+  __shared__ double part[KL_RED / 64];
+  double v = 0.0;
+  for (int64_t i = threadIdx.x; i < nparts; i += KL_RED) v += acc[i];
   v = wave_reduce_sum(v);
   if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
   __syncthreads();
   if (threadIdx.x == 0) {
     double tot = 0.0;
 #pragma unroll
-    for (int w = 0; w < KL_SLOTS / 64; ++w) tot += part[w];
+    for (int w = 0; w < KL_RED / 64; ++w) tot += part[w];
     const double lr = params[1];
     const double vg = tot * lr * lr;
     double sc = 1.0;
@@ -153,9 +154,9 @@ void kl_dot_multi(const LayerDesc* descs, int nlayers, int64_t total_blocks,
       descs, nlayers, acc);
 }
 
-void kl_finalize_dev(double* acc, const float* params, float* scale,
-                     hipStream_t s) {
-  kl_finalize_dev_kernel<<<1, KL_SLOTS, 0, s>>>(acc, params, scale);
+void kl_finalize_dev(const double* acc, int64_t nparts, const float* params,
+                     float* scale, hipStream_t s) {
+  kl_finalize_dev_kernel<<<1, KL_RED, 0, s>>>(acc, nparts, params, scale);
 }
 
 void apply_multi(const LayerDesc* descs, int nlayers, int64_t total_blocks,

@@ -12,8 +12,11 @@
 //     as the mirror, so C is exactly symmetric (the reference's (C+C^T)/2 is
 //     a no-op here),
 //   * tall-skinny shapes (N >> D, e.g. 401408 x 147 for the ResNet-50 stem)
-//     split the row range over blocks and reduce with float atomics into the
-//     upper triangle, followed by a mirror pass.
+//     split the row range over blocks; each block stores its fp32 partial
+//     tile into a workspace slab and a second kernel sums the slabs in a
+//     FIXED split order, applies beta/alpha and writes both triangles.  The
+//     result is bitwise reproducible run to run (no float atomics), which
+//     the HIP-graph-vs-eager parity test relies on.
 //
 // Tiling (gfx950, wave64): 128x128 output tile per 256-thread block, 4 waves
 // in a 2x2 grid, each wave 64x64 = 2x2 MFMA 32x32 accumulators.  BK = 32
@@ -365,7 +368,7 @@ __global__ void __launch_bounds__(NT)
 syrk_kernel(const void* __restrict__ X, int64_t N, int64_t K, int64_t ldx,
             int bias, float* __restrict__ C, int64_t D, int64_t ldc,
             float alpha, float beta, int T, int splits, int64_t rows_per_split,
-            int vec_ok, ConvGeom geom) {
+            int vec_ok, ConvGeom geom, float* __restrict__ ws) {
   using LT = typename std::conditional<std::is_same<TIn, float>::value, float,
                                        short>::type;
   constexpr int LW = std::is_same<TIn, float>::value ? LDS_W32 : LDS_W16;
@@ -455,11 +458,14 @@ syrk_kernel(const void* __restrict__ X, int64_t N, int64_t K, int64_t ldx,
       for (int rb = 0; rb < 4; ++rb) {
         const int64_t gr0 = c0i + wr * 64 + mi * 32 + 8 * rb + 4 * (l >> 5);
         if (splits > 1) {
+          // partial tile -> workspace slab [tile][split][BM][BM] (plain
+          // stores; 32 lanes write 128 contiguous bytes per row)
+          float* slab = ws + ((int64_t)tile * splits + split) * (BM * BM);
+          const int lc = wc * 64 + nj * 32 + (l & 31);
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const int64_t gr = gr0 + e;
-            if (gr < D && gc < D && gr <= gc)
-              atomicAdd(&C[gr * ldc + gc], alpha * acc[mi][nj][rb * 4 + e]);
+            const int lr = wr * 64 + mi * 32 + 8 * rb + 4 * (l >> 5) + e;
+            slab[lr * BM + lc] = acc[mi][nj][rb * 4 + e];
           }
         } else if (!diag) {
           // strictly upper tile: write C[gr][gc] and mirror C[gc][gr..gr+3]
@@ -500,90 +506,123 @@ syrk_kernel(const void* __restrict__ X, int64_t N, int64_t K, int64_t ldx,
   }
 }
 
-// C[i][j] *= beta on the upper triangle (split-K pre-pass)
+// Split-K reduction: one 32x32 sub-block of the upper triangle per block.
+// C[i][j] = beta*C[i][j] + alpha * sum_s slab[s][i][j]  (s ascending), and
+// C[j][i] = C[i][j] through an LDS transpose (both writes coalesced).
 __global__ void __launch_bounds__(256)
-scale_upper_kernel(float* __restrict__ C, int64_t D, int64_t ldc, float beta) {
-  const int64_t i = blockIdx.x;
-  for (int64_t j = i + threadIdx.x; j < D; j += blockDim.x) {
-    C[i * ldc + j] = beta == 0.f ? 0.f : beta * C[i * ldc + j];
-  }
-}
-
-// lower triangle := transpose of upper (32x32 LDS tiles; coalesced both ways)
-__global__ void __launch_bounds__(256)
-mirror_upper_kernel(float* __restrict__ C, int64_t D, int64_t ldc) {
+splitk_reduce_kernel(const float* __restrict__ ws, int splits, int T,
+                     float* __restrict__ C, int64_t D, int64_t ldc,
+                     float alpha, float beta, int T32) {
   __shared__ float tile[32][33];
-  const int64_t ti = blockIdx.y, tj = blockIdx.x;
-  if (tj > ti) return;  // only tiles on/below the diagonal are written
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  for (int r = ty; r < 32; r += 8) {
-    const int64_t i = tj * 32 + r, j = ti * 32 + tx;  // source (upper) tile
-    tile[r][tx] = (i < D && j < D) ? C[i * ldc + j] : 0.f;
+  // blockIdx.x -> (bi, bj), bi <= bj, over the T32 x T32 sub-block grid
+  int bi, bj;
+  tile_of((int)blockIdx.x, T32, bi, bj);
+  const int t = threadIdx.x;
+  const int r = t >> 3, c4 = (t & 7) * 4;
+  const int ti = bi >> 2, tj = bj >> 2;
+  const int64_t tidx = (int64_t)ti * T - (int64_t)ti * (ti - 1) / 2 + (tj - ti);
+  const int lr = (bi & 3) * 32 + r, lc = (bj & 3) * 32 + c4;
+  const float* src = ws + tidx * splits * (BM * BM) + lr * BM + lc;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int s = 0; s < splits; ++s) {
+    const float4 v = *reinterpret_cast<const float4*>(src + (int64_t)s * (BM * BM));
+    acc.x += v.x;
+    acc.y += v.y;
+    acc.z += v.z;
+    acc.w += v.w;
+  }
+  const int64_t gr = (int64_t)bi * 32 + r;
+  const float a4[4] = {acc.x, acc.y, acc.z, acc.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int64_t gc = (int64_t)bj * 32 + c4 + e;
+    float v = 0.f;
+    const bool upper = gr < D && gc < D && (bi < bj || gr <= gc);
+    if (upper) {
+      const float old = beta != 0.f ? C[gr * ldc + gc] : 0.f;
+      v = beta * old + alpha * a4[e];
+      C[gr * ldc + gc] = v;
+    }
+    tile[r][c4 + e] = v;
   }
   __syncthreads();
-  for (int r = ty; r < 32; r += 8) {
-    const int64_t i = ti * 32 + r, j = tj * 32 + tx;  // destination
-    if (i < D && j < D && j < i) C[i * ldc + j] = tile[tx][r];
+  // mirror: C[bj*32 + r][bi*32 + c] = tile[c][r]  (strictly lower elements)
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int c = c4 + e;
+    const int64_t i = (int64_t)bj * 32 + r, j = (int64_t)bi * 32 + c;
+    if (i < D && j < D && j < i) C[i * ldc + j] = tile[c][r];
   }
 }
 
 }  // namespace
 
+// Row splits for one SYRK.  Only shapes whose upper-triangle tile count
+// cannot fill the chip are split (target ~768 blocks = 3 per CU), and the
+// fp32 partial-tile workspace is capped at 32 MB.
 int64_t syrk_workspace_splits(int64_t N, int64_t D) {
   const int64_t T = ceil_div(D, BM);
   const int64_t tiles = T * (T + 1) / 2;
-  const int64_t target_blocks = 768;  // ~3 blocks per CU on 256 CUs
+  const int64_t target_blocks = 768;
   int64_t splits = ceil_div(target_blocks, tiles);
   const int64_t max_by_rows = ceil_div(N, 4 * BK);  // >= 4 k-tiles per split
   if (splits > max_by_rows) splits = max_by_rows;
-  if (splits < 1) splits = 1;
+  const int64_t max_by_ws = (int64_t(32) << 20) / (4 * tiles * BM * BM);
+  if (splits > max_by_ws) splits = max_by_ws;
+  if (splits < 2) splits = 1;
   if (splits > 4096) splits = 4096;
   return splits;
 }
 
+int64_t syrk_workspace_floats(int64_t D, int64_t splits) {
+  if (splits <= 1) return 0;
+  const int64_t T = ceil_div(D, BM);
+  return T * (T + 1) / 2 * splits * BM * BM;
+}
+
 // geom == nullptr: X is a dense [N, K] matrix (row stride ldx); otherwise
-// X is an NHWC conv input and its rows are the conv patches (implicit im2col)
+// X is an NHWC conv input and its rows are the conv patches (implicit im2col).
+// ws: syrk_workspace_floats(D, splits) floats when splits > 1.
 void syrk(int in_dtype, const void* x, int64_t N, int64_t K, int64_t ldx,
           bool bias, float* C, int64_t D, int64_t ldc, float alpha,
-          float beta, int splits, hipStream_t s, const ConvGeom* geom) {
+          float beta, int splits, hipStream_t s, const ConvGeom* geom,
+          float* ws) {
   if (D <= 0) return;
   const int T = (int)ceil_div(D, BM);
   const int64_t tiles = (int64_t)T * (T + 1) / 2;
-  if (splits < 1) splits = 1;
+  if (splits < 1 || ws == nullptr) splits = 1;
   const int64_t rows_per_split =
       splits > 1 ? ceil_div(ceil_div(N, splits), BK) * BK : (N > 0 ? N : 1);
-  if (splits > 1) {
-    scale_upper_kernel<<<dim3((unsigned)D), dim3(256), 0, s>>>(C, D, ldc, beta);
-  }
   const dim3 grid((unsigned)(tiles * splits));
-  const float beta_k = splits > 1 ? 1.f : beta;
   const ConvGeom g = geom != nullptr ? *geom : ConvGeom{};
   if (in_dtype == kF32) {
     const int vec_ok = ((ldx & 3) == 0) &&
                        ((reinterpret_cast<uintptr_t>(x) & 15) == 0);
     if (geom != nullptr)
       syrk_kernel<float, PatchStaging<float>><<<grid, dim3(NT), 0, s>>>(
-          x, N, K, ldx, bias ? 1 : 0, C, D, ldc, alpha, beta_k, T, splits,
-          rows_per_split, vec_ok, g);
+          x, N, K, ldx, bias ? 1 : 0, C, D, ldc, alpha, beta, T, splits,
+          rows_per_split, vec_ok, g, ws);
     else
       syrk_kernel<float, DenseStaging<float>><<<grid, dim3(NT), 0, s>>>(
-          x, N, K, ldx, bias ? 1 : 0, C, D, ldc, alpha, beta_k, T, splits,
-          rows_per_split, vec_ok, g);
+          x, N, K, ldx, bias ? 1 : 0, C, D, ldc, alpha, beta, T, splits,
+          rows_per_split, vec_ok, g, ws);
   } else {
     const int vec_ok = ((ldx & 7) == 0) &&
                        ((reinterpret_cast<uintptr_t>(x) & 15) == 0);
     if (geom != nullptr)
       syrk_kernel<bf16_t, PatchStaging<bf16_t>><<<grid, dim3(NT), 0, s>>>(
-          x, N, K, ldx, bias ? 1 : 0, C, D, ldc, alpha, beta_k, T, splits,
-          rows_per_split, vec_ok, g);
+          x, N, K, ldx, bias ? 1 : 0, C, D, ldc, alpha, beta, T, splits,
+          rows_per_split, vec_ok, g, ws);
     else
       syrk_kernel<bf16_t, DenseStaging<bf16_t>><<<grid, dim3(NT), 0, s>>>(
-          x, N, K, ldx, bias ? 1 : 0, C, D, ldc, alpha, beta_k, T, splits,
-          rows_per_split, vec_ok, g);
+          x, N, K, ldx, bias ? 1 : 0, C, D, ldc, alpha, beta, T, splits,
+          rows_per_split, vec_ok, g, ws);
   }
   if (splits > 1) {
-    const unsigned t = (unsigned)ceil_div(D, 32);
-    mirror_upper_kernel<<<dim3(t, t), dim3(256), 0, s>>>(C, D, ldc);
+    const int T32 = (int)ceil_div(D, 32);
+    const unsigned blocks = (unsigned)((int64_t)T32 * (T32 + 1) / 2);
+    splitk_reduce_kernel<<<dim3(blocks), dim3(256), 0, s>>>(
+        ws, splits, T, C, D, ldc, alpha, beta, T32);
   }
 }
 

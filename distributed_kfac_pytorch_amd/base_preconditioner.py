@@ -80,6 +80,13 @@ class StepGraphs:
         self.replays = 0
         self.captures = 0
         self._lane_streams: list = []
+        # descriptor tables the current graph reads (pinned in their caches)
+        self._held: list[tuple[Any, Any]] = []
+
+    def _release(self) -> None:
+        for owner, key in self._held:
+            owner.release(key)
+        self._held = []
 
     def _streams(self, n: int) -> list:
         while len(self._lane_streams) < n:
@@ -194,6 +201,14 @@ class StepGraphs:
             # grouped MFMA GEMMs (4 launches for all layers); tables are built
             # here, outside the capture
             grouped = pre._grouped.prepare(workers, damping)
+            # the graph keeps reading these device tables: pin them so the
+            # table caches never evict (free) them while the graph lives
+            self.graph = None
+            self._release()
+            if grouped:
+                self._held.append((pre._grouped, pre._grouped.hold()))
+            if not bcast:
+                self._held.append((pre._multi_apply, pre._multi_apply.hold()))
             g = torch.cuda.CUDAGraph()
             side = torch.cuda.Stream()
             side.wait_stream(torch.cuda.current_stream())
@@ -538,9 +553,9 @@ class BaseKFACPreconditioner:
             mats.append(l.g_factor)
         invs = linalg.inverse_many(mats, damping) if mats else []
         for (_, l), x in zip(inv_a, invs[: len(inv_a)]):
-            l.a_inv = x.to(l.inv_dtype)
+            l.set_a_inv(x)
         for (_, l), x in zip(inv_g, invs[len(inv_a):]):
-            l.g_inv = x.to(l.inv_dtype)
+            l.set_g_inv(x)
         batched |= {id(l) for _, l in inv_a} | {id(l) for _, l in inv_g}
         for _, l in mine_a:
             if id(l) not in batched:

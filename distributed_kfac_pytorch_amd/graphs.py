@@ -146,7 +146,10 @@ class GraphedTrainStep:
             self.preconditioner.step()
         self.optimizer.step()
         self.eager_steps += 1
-        return loss
+        # detached: a caller holding the loss must not keep this step's
+        # autograd graph (and its AccumulateGrad nodes, bound to the eager
+        # stream) alive across the next capture
+        return loss.detach()
 
     def _advance(self) -> None:
         """Host-side K-FAC state change of one replayed step."""

@@ -96,15 +96,39 @@ class KFACInverseLayer(KFACBaseLayer):
         d = torch.eye(f.shape[0], dtype=f.dtype, device=f.device) * damping
         return torch.linalg.inv((f + d).to(torch.float32)).to(self.inv_dtype)
 
+    @staticmethod
+    def _install(old: Any, new: torch.Tensor) -> torch.Tensor:
+        """Copy ``new`` into the existing inverse buffer when possible, so
+        A^-1 / G^-1 keep one device address across inverse updates: the
+        grouped-GEMM descriptor tables and captured HIP graphs
+        (``StepGraphs``, ``graphs.GraphedTrainStep``) hold that address."""
+        if (
+            isinstance(old, torch.Tensor)
+            and old.shape == new.shape
+            and old.dtype == new.dtype
+            and old.device == new.device
+            and old.is_contiguous()
+        ):
+            if old.data_ptr() != new.data_ptr():
+                old.copy_(new)
+            return old
+        return new.contiguous()
+
+    def set_a_inv(self, inv: torch.Tensor) -> None:
+        self.a_inv = self._install(self.a_inv, inv.to(self.inv_dtype))
+
+    def set_g_inv(self, inv: torch.Tensor) -> None:
+        self.g_inv = self._install(self.g_inv, inv.to(self.inv_dtype))
+
     def compute_a_inv(self, damping: float = 0.001) -> None:
         if self.a_factor is None:
             raise RuntimeError('Cannot invert A before A has been computed')
-        self.a_inv = self._inverse(self.a_factor, damping)
+        self.set_a_inv(self._inverse(self.a_factor, damping))
 
     def compute_g_inv(self, damping: float = 0.001) -> None:
         if self.g_factor is None:
             raise RuntimeError('Cannot invert G before G has been computed')
-        self.g_inv = self._inverse(self.g_factor, damping)
+        self.set_g_inv(self._inverse(self.g_factor, damping))
 
     def preconditioned_grad(self, damping: float = 0.001) -> None:
         """P = G_inv [Wg | bg] A_inv into the persistent grad buffer."""

@@ -143,9 +143,16 @@ class _TableCache:
     so each entry owns its staging buffers until evicted.  Pinned memory
     cannot be allocated while a capture is running, so the buffers are
     allocated the first time they are needed outside a capture and recycled
-    after that.  Each captured step kind keeps its own entry; the size bound
-    only stops eager training with fresh gradient tensors every step from
-    growing the cache.
+    after that.
+
+    Staging reuse is fenced: an eager upload records a HIP event on the
+    stream that runs its H2D copy, and a buffer whose entry is evicted is
+    parked until that event has completed -- the host never rewrites a
+    staging buffer a queued copy has yet to read (the host runs ahead of the
+    GPU by whole steps).  Entries referenced by a captured graph are never
+    evicted: those built or looked up during a capture (sticky), and those a
+    caller pins explicitly (``pin`` / ``unpin``, used by ``StepGraphs``
+    whose tables are built just before its capture).
     """
 
     SLOT_BYTES = 1 << 16  # >= 500 layers of descriptors per table
@@ -153,15 +160,34 @@ class _TableCache:
     def __init__(self, size: int = 8, slots_per_entry: int = 1) -> None:
         self.size = size
         self.per = slots_per_entry
+        # key -> (value, slots, event | None)
         self._d: dict = {}
+        # clean staging buffers (no pending H2D copy reads them)
         self._free: list[torch.Tensor] = []
-        # entries a captured graph refers to (its kernels read the device
-        # table, its H2D copy re-reads the staging buffer): never evicted
+        # evicted buffers whose last copy may still be queued: (buf, event)
+        self._parked: list[tuple[torch.Tensor, Any]] = []
         self._sticky: set = set()
+        self._pins: dict = {}
 
     @staticmethod
     def _capturing() -> bool:
         return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+
+    def _held(self, key: tuple) -> bool:
+        return key in self._sticky or self._pins.get(key, 0) > 0
+
+    def pin(self, key: tuple | None) -> None:
+        if key is not None and key in self._d:
+            self._pins[key] = self._pins.get(key, 0) + 1
+
+    def unpin(self, key: tuple | None) -> None:
+        if key is None:
+            return
+        n = self._pins.get(key, 0) - 1
+        if n > 0:
+            self._pins[key] = n
+        else:
+            self._pins.pop(key, None)
 
     def get(self, key: tuple) -> Any:
         v = self._d.pop(key, None)
@@ -172,17 +198,31 @@ class _TableCache:
             return v[0]
         return None
 
+    def _unpark(self, wait: bool) -> None:
+        keep = []
+        for buf, ev in self._parked:
+            if ev is None or ev.query():
+                self._free.append(buf)
+            elif wait:
+                ev.synchronize()
+                self._free.append(buf)
+            else:
+                keep.append((buf, ev))
+        self._parked = keep
+
     def reserve(self) -> list[torch.Tensor | None]:
         """Staging buffers for one new entry (None: let the builder
         allocate, which is only possible outside a capture)."""
-        while len(self._d) - len(self._sticky) >= self.size:
-            victim = next((k for k in self._d if k not in self._sticky), None)
+        while len(self._d) - sum(1 for k in self._d if self._held(k)) >= self.size:
+            victim = next((k for k in self._d if not self._held(k)), None)
             if victim is None:
                 break
-            _, slots = self._d.pop(victim)
-            self._free += [t for t in slots if t is not None]
+            _, slots, ev = self._d.pop(victim)
+            self._parked += [(t, ev) for t in slots if t is not None]
         capturing = self._capturing()
         if not capturing and torch.cuda.is_available():
+            # a parked buffer is reused only once its last copy has run
+            self._unpark(wait=len(self._free) < self.per)
             # top up so that a later capture never has to allocate
             while len(self._free) < self.per * self.size:
                 self._free.append(torch.empty(self.SLOT_BYTES, dtype=torch.uint8, pin_memory=True))
@@ -192,9 +232,14 @@ class _TableCache:
         return out
 
     def put(self, key: tuple, value: Any, slots: list) -> Any:
-        self._d[key] = (value, slots)
+        ev = None
         if self._capturing():
             self._sticky.add(key)
+        elif torch.cuda.is_available() and any(t is not None for t in slots):
+            # the uploads were enqueued on the current stream
+            ev = torch.cuda.Event()
+            ev.record()
+        self._d[key] = (value, slots, ev)
         return value
 
 
@@ -215,17 +260,24 @@ class MultiLayerApply:
         self._blocks = 0
         self._tables = _TableCache(slots_per_entry=1)
         self._acc: torch.Tensor | None = None
+        self._retired: list[torch.Tensor] = []
         self._scale: torch.Tensor | None = None
         self._params: torch.Tensor | None = None
         self._param_vals: tuple[float, float] | None = None
         self._n = 0
 
-    def _buffers(self, device: torch.device) -> None:
+    def _buffers(self, device: torch.device, nparts: int) -> None:
         if self._acc is None or self._acc.device != device:
-            self._acc = torch.zeros(256, dtype=torch.float64, device=device)  # KL partial sums
+            self._acc = None
             self._scale = torch.ones(1, dtype=torch.float32, device=device)
             self._params = torch.zeros(2, dtype=torch.float32, device=device)
             self._param_vals = None
+        if self._acc is None or self._acc.numel() < nparts:
+            # one fp64 KL partial per block (summed in a fixed order).  A
+            # replaced buffer is kept alive: a captured graph may still read it
+            if self._acc is not None:
+                self._retired.append(self._acc)
+            self._acc = torch.zeros(max(nparts, 256), dtype=torch.float64, device=device)
 
     def prepare(
         self,
@@ -279,7 +331,7 @@ class MultiLayerApply:
             self._table, self._blocks, _ = entry
             self._key = key_t
         self._n = len(ps)
-        self._buffers(ps[0].device)
+        self._buffers(ps[0].device, self._blocks)
         if kl_clip is not None:
             vals = (float(kl_clip), float(lr))
             if vals != self._param_vals:
@@ -288,6 +340,15 @@ class MultiLayerApply:
                 self._param_vals = vals
         return True
 
+    def hold(self) -> tuple | None:
+        """Pin the current table (a graph about to be captured uses it);
+        returns the handle for ``release``."""
+        self._tables.pin(self._key)
+        return self._key
+
+    def release(self, key: tuple | None) -> None:
+        self._tables.unpin(key)
+
     def launch(self, with_kl: bool) -> None:
         """The three (or one, without KL clip) multi-tensor launches."""
         lib = native()
@@ -295,7 +356,7 @@ class MultiLayerApply:
             lib.apply_multi(self._table, self._n, self._blocks, None)
             return
         lib.kl_dot_multi(self._table, self._n, self._blocks, self._acc)
-        lib.kl_finalize_dev(self._acc, self._params, self._scale)
+        lib.kl_finalize_dev(self._acc, self._blocks, self._params, self._scale)
         lib.apply_multi(self._table, self._n, self._blocks, self._scale)
 
     def run(self, layers: list, kl_clip: float | None, lr: float) -> bool:
@@ -474,6 +535,15 @@ class GroupedPrecondition:
             t = torch.empty(shape, dtype=torch.float32, device=dev)
             layer._gtmp = t
         return t
+
+    def hold(self) -> tuple | None:
+        """Pin the current tables (a graph about to be captured uses
+        them); returns the handle for ``release``."""
+        self._cache.pin(self._key)
+        return self._key
+
+    def release(self, key: tuple | None) -> None:
+        self._cache.unpin(key)
 
     def launch(self) -> None:
         lib = native()

@@ -62,11 +62,34 @@ def test_syrk_split_k_forced(cuda):
     lib = _native.native()
     x = torch.randn(5000, 96, device=cuda)
     out = torch.zeros(96, 96, device=cuda)
-    for splits in (1, 3, 17):
+    for splits in (1, 3, 17, 64):
         lib.syrk(x, out, False, 1.0, 0.0, splits)
         ref = _ref_cov(x, False)
         assert (out.double() - ref).abs().max().item() < 1e-4 * ref.abs().max().item()
         assert torch.equal(out, out.t())
+
+
+@pytest.mark.parametrize('d,bias', [(96, False), (147, True), (300, True)])
+def test_syrk_split_k_deterministic_ema(cuda, d, bias):
+    """The split-K workspace reduction sums partial tiles in a fixed order:
+    repeated launches are bitwise identical, the EMA (beta) is applied once,
+    and the result is exactly symmetric."""
+    lib = _native.native()
+    torch.manual_seed(1)
+    k = d - int(bias)
+    x = torch.randn(20000, k, device=cuda).to(torch.bfloat16)
+    c0 = torch.randn(d, d, device=cuda)
+    c0 = c0 + c0.t()
+    outs = []
+    for _ in range(3):
+        out = c0.clone()
+        lib.syrk(x, out, bias, 0.05 / x.shape[0], 0.95, 13)
+        outs.append(out)
+    assert all(torch.equal(outs[0], o) for o in outs[1:])
+    assert torch.equal(outs[0], outs[0].t())
+    ref = 0.95 * c0.double() + (0.05 / x.shape[0]) * _ref_cov(x, bias)
+    assert (outs[0].double() - ref).abs().max().item() < 2e-5 * ref.abs().max().item()
+    assert lib.syrk_default_splits(20000, d) > 1
 
 
 @pytest.mark.parametrize('natural', [True, False])
