@@ -77,29 +77,69 @@ def diffs(ma, oa, pa, mb, ob, pb) -> dict:  # type: ignore[no-untyped-def]
     return out
 
 
+def precond_error(pre) -> float:  # type: ignore[no-untyped-def]
+    """Largest relative error, over layers, of the installed eigen
+    preconditioner Qg((Qg^T V Qa) * dGdA)Qa^T against float64 math on the
+    layer's own factors (random V)."""
+    worst = 0.0
+    for _, l in pre._layers.values():
+        if getattr(l, 'dgda', None) is None:
+            continue
+        a = l.a_factor.double().cpu()
+        g = l.g_factor.double().cpu()
+        da, qa = torch.linalg.eigh(a)
+        dg, qg = torch.linalg.eigh(g)
+        damp = pre.damping
+        v = torch.randn(g.shape[0], a.shape[0], dtype=torch.float64)
+        ex = qg @ ((qg.t() @ v @ qa) / (torch.outer(dg.clamp(min=0), da.clamp(min=0)) + damp)) @ qa.t()
+        Qa, Qg, S = l.qa.double().cpu(), l.qg.double().cpu(), l.dgda.double().cpu()
+        got = Qg @ ((Qg.t() @ v @ Qa) * S) @ Qa.t()
+        worst = max(worst, float((got - ex).abs().max() / ex.abs().max()))
+    return worst
+
+
+def make(dev: torch.device, method: str, mode: str):  # type: ignore[no-untyped-def]
+    """mode: graph (GraphedTrainStep) | step (StepGraphs eager) | eager."""
+    m, o, p, f = setup(dev, method)
+    if mode == 'eager':
+        p._graphs = None
+    if mode == 'graph':
+        r = GraphedTrainStep(f, o, p)
+        return m, o, p, lambda: float(r()), r
+
+    def run() -> float:
+        o.zero_grad(set_to_none=False)
+        v = float(f())
+        p.step()
+        o.step()
+        return v
+    return m, o, p, run, None
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument('--method', default='eigen')
     ap.add_argument('--steps', type=int, default=14)
+    ap.add_argument('--a', default='graph', help='graph | step | eager')
+    ap.add_argument('--b', default='step', help='graph | step | eager')
     ap.add_argument('--deterministic', action='store_true',
                     help='torch.backends.cudnn.deterministic (MIOpen)')
     args = ap.parse_args()
     torch.backends.cudnn.deterministic = args.deterministic
     dev = torch.device('cuda')
-    ma, oa, pa, fa = setup(dev, args.method)
-    mb, ob, pb, fbk = setup(dev, args.method)
-    runner = GraphedTrainStep(fa, oa, pa)
+    ma, oa, pa, sa, runner = make(dev, args.method, args.a)
+    mb, ob, pb, sb, _ = make(dev, args.method, args.b)
     for i in range(args.steps):
-        kind = runner.kind()
-        la = float(runner())
-        ob.zero_grad(set_to_none=False)
-        lb = float(fbk())
-        pb.step()
-        ob.step()
+        kind = runner.kind() if runner is not None else ('inverse' if pa.steps % 6 == 0 else '')
+        la = sa()
+        lb = sb()
         torch.cuda.synchronize()
         rec = {'step': i, 'kind': kind, 'loss': abs(la - lb)}
         rec.update(diffs(ma, oa, pa, mb, ob, pb))
-        rec['replays'] = runner.replays
+        if args.method == 'eigen' and pa.steps % 6 == 1:
+            rec['err_a'] = precond_error(pa)
+            rec['err_b'] = precond_error(pb)
+        rec['replays'] = runner.replays if runner is not None else 0
         print(json.dumps(rec), flush=True)
 
 
