@@ -90,6 +90,10 @@ std::vector<at::Tensor> rocsolver_eigh(at::Tensor A, int64_t algo,
                                        int64_t max_sweeps, double tol);
 int64_t sytrd_max_n();
 int64_t spd_lds_max_n();
+// eigh_block_host.cpp
+std::vector<at::Tensor> block_jacobi_eigh(at::Tensor A, c10::optional<at::Tensor> Q0,
+                                          int64_t max_sweeps, double tol,
+                                          int64_t inner_sweeps, double noise, bool refine);
 at::Tensor spd_inverse(at::Tensor F, double damping);
 std::vector<at::Tensor> sytrd_reduce(std::vector<at::Tensor> stacks);
 std::vector<at::Tensor> tridiag_eigvecs(at::Tensor A, at::Tensor d, at::Tensor e,
@@ -803,5 +807,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("A_hls") = std::vector<c10::optional<at::Tensor>>(),
         py::arg("B_hls") = std::vector<c10::optional<at::Tensor>>());
   m.def("gemm3_grouped", &gemm3_grouped);
+  // GIL released: one host thread per eigensolver lane (the sweep loop reads
+  // its convergence flags back once per sweep)
+  m.def("block_jacobi_eigh", &block_jacobi_eigh, py::call_guard<py::gil_scoped_release>(),
+        py::arg("A"), py::arg("Q0") = py::none(), py::arg("max_sweeps") = 12,
+        py::arg("tol") = 1e-6, py::arg("inner_sweeps") = 2, py::arg("noise") = 4e-6,
+        py::arg("refine") = true);
   m.attr("arch") = "gfx950";
 }

@@ -12,9 +12,10 @@ every rank).  MI355X-first differences:
   output in an extra autograd node).  With one micro-batch per update the
   accumulate + EMA is a single fused SYRK.
 * Second order.  All factors this rank owns are decomposed together
-  (``ops.linalg.eigh_many``: batched Jacobi for small factors, batched
-  rocSOLVER per size bucket for large ones), then broadcasts are issued in
-  the reference's (reversed layer, A then G) order.
+  (``ops.linalg.eigh_many``: one-workgroup LDS Jacobi for n <= 128, the
+  native block-Jacobi solver warm-started from each factor's previous
+  eigenbasis above that), then broadcasts are issued in the reference's
+  (reversed layer, A then G) order.
 * No host syncs in ``step()``.  The KL-clip scale is reduced on the device
   (fp64 accumulator) and applied by the gradient-write kernel; the
   reference performs two ``.item()`` syncs per layer per step.
@@ -532,7 +533,11 @@ class BaseKFACPreconditioner:
             if l.g_factor is None:
                 raise RuntimeError('Cannot eigendecompose G before G has been computed')
             mats.append(l.g_factor)
-        results = linalg.eigh_many(mats) if mats else []
+        # warm starts: each factor's previous eigenbasis (factors drift
+        # slowly between second-order updates; ops.linalg block Jacobi)
+        warm = [self._warm_basis(l.qa, m) for (_, l), m in zip(eig_a, mats[: len(eig_a)])]
+        warm += [self._warm_basis(l.qg, m) for (_, l), m in zip(eig_g, mats[len(eig_a):])]
+        results = linalg.eigh_many(mats, warm) if mats else []
         for (_, l), (d, q) in zip(eig_a, results[: len(eig_a)]):
             assert isinstance(l, KFACEigenLayer)
             l.set_a_eig(d, q)
@@ -563,6 +568,19 @@ class BaseKFACPreconditioner:
         for _, l in mine_g:
             if id(l) not in batched:
                 l.compute_g_inv(damping=damping)
+
+    @staticmethod
+    def _warm_basis(q: Any, factor: torch.Tensor) -> torch.Tensor | None:
+        if (
+            os.environ.get('KFAC_EIGH_WARM', '1') == '0'
+            or not isinstance(q, torch.Tensor)
+            or q.shape != factor.shape
+            or q.dtype != torch.float32
+            or q.device != factor.device
+            or not q.is_cuda
+        ):
+            return None
+        return q
 
     @torch.no_grad()
     def step(self) -> None:

@@ -49,7 +49,7 @@ JACOBI_TOL = float(os.environ.get('KFAC_JACOBI_TOL', '1e-7'))
 _ALGOS = {'syevd': 0, 'syevj': 1, 'syevdj': 2}
 # n above which auto picks syevd over syevj (Jacobi sweeps are O(n^3) each)
 # largest n sent to the LDS Jacobi kernel (its hard limit is jacobi_max_n())
-JACOBI_MAX_N = int(os.environ.get('KFAC_JACOBI_MAX_N', '64'))
+JACOBI_MAX_N = int(os.environ.get('KFAC_JACOBI_MAX_N', '128'))
 
 
 def sytrd_min_n() -> int:
@@ -84,18 +84,136 @@ def _algo_for(n: int) -> str:
     return 'syevd'
 
 
-def _gpu_bucket(stack: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+def block_jacobi_enabled() -> bool:
+    """Native warm-started block Jacobi (csrc/eigh_block.hip) for every
+    factor above the LDS Jacobi tier (``KFAC_EIGH_BLOCK=0``: rocSOLVER)."""
+    return os.environ.get('KFAC_EIGH_BLOCK', '1') != '0' and os.environ.get(
+        'KFAC_EIGH', 'auto') == 'auto'
+
+
+def cold_algo() -> str:
+    """Solver for a factor with no previous eigenbasis (first refresh,
+    checkpoint load): ``KFAC_EIGH_COLD`` = block | syevd."""
+    return os.environ.get('KFAC_EIGH_COLD', 'block')
+
+
+BJ_MAX_SWEEPS_WARM = int(os.environ.get('KFAC_BJ_SWEEPS', '10'))
+BJ_MAX_SWEEPS_COLD = int(os.environ.get('KFAC_BJ_SWEEPS_COLD', '20'))
+BJ_TOL = float(os.environ.get('KFAC_BJ_TOL', '1e-6'))
+BJ_INNER = int(os.environ.get('KFAC_BJ_INNER', '2'))
+BJ_NOISE = float(os.environ.get('KFAC_BJ_NOISE', '4e-6'))
+BJ_REFINE = os.environ.get('KFAC_BJ_REFINE', '1') != '0'
+# per-call statistics of the block-Jacobi tier (bench / tests read them)
+last_stats: dict[str, Any] = {}
+
+
+def _block_jacobi(stack: torch.Tensor, warm: torch.Tensor | None) -> tuple[torch.Tensor, torch.Tensor]:
+    lib = native()
+    sweeps_max = BJ_MAX_SWEEPS_WARM if warm is not None else BJ_MAX_SWEEPS_COLD
+    evals, evecs, sweeps, _ = lib.block_jacobi_eigh(
+        stack.contiguous(), warm, sweeps_max, BJ_TOL, BJ_INNER, BJ_NOISE, BJ_REFINE)
+    sw = sweeps.tolist()  # host tensor: the solver already synchronised
+    n = stack.shape[-1]
+    last_stats.setdefault('sweeps', []).extend((n, s) for s in sw)
+    bad = [i for i, s in enumerate(sw) if s < 0]
+    if bad:
+        # not converged within the sweep budget: rocSOLVER for those
+        logger.warning('block Jacobi did not converge for %d factor(s) of n=%d; '
+                       'using syevd', len(bad), n)
+        idx = torch.tensor(bad, device=stack.device)
+        e2, v2 = lib.rocsolver_eigh(stack.index_select(0, idx).contiguous(), 0, 100, 1e-7)
+        evals = evals.clone()
+        evecs = evecs.clone()
+        evals.index_copy_(0, idx, e2)
+        evecs.index_copy_(0, idx, v2.contiguous())
+    return evals, evecs
+
+
+WARM_ACCEPT_TOL = float(os.environ.get('KFAC_EIGH_ACCEPT_TOL', '1e-6'))
+# the acceptance GEMM sits on the critical path of a lane: the largest
+# (A) factors essentially never pass, so they go straight to the solver
+WARM_ACCEPT_MAX_N = int(os.environ.get('KFAC_EIGH_ACCEPT_MAX_N', '2048'))
+
+
+def _accept_warm(stack: torch.Tensor, warm: torch.Tensor
+                 ) -> tuple[list[int], torch.Tensor, torch.Tensor]:
+    """Factors the previous eigenbasis still diagonalises.
+
+    With Q0 the previous basis, the Rayleigh quotients r = diag(Q0^T A Q0)
+    and the residual ||A Q0 - Q0 diag(r)||_F = off(Q0^T A Q0)_F cost ONE
+    batched GEMM; a factor whose residual is below KFAC_EIGH_ACCEPT_TOL *
+    ||A||_F (the block-Jacobi convergence test: no rotation would be
+    applied) keeps Q0 with the fresh eigenvalues r.  On real ResNet-50
+    factors about a third of the factors (most G factors) pass at the
+    step-100 refresh (profiles/refresh_probe_r2_resnet50_step100.jsonl).
+    Returns (accepted indices, their sorted evals, their evecs)."""
+    aq = torch.bmm(stack, warm)
+    r = (warm * aq).sum(1)
+    res = (aq - warm * r.unsqueeze(1)).flatten(1).norm(dim=1)
+    fro = stack.flatten(1).norm(dim=1)
+    ok = (res <= WARM_ACCEPT_TOL * fro).tolist()
+    idx = [i for i, v in enumerate(ok) if v]
+    if not idx:
+        return [], r[:0], warm[:0]
+    sel = torch.tensor(idx, device=stack.device)
+    rs, order = r.index_select(0, sel).sort(dim=1)
+    q = warm.index_select(0, sel)
+    q = q.gather(2, order.unsqueeze(1).expand(-1, q.shape[1], -1))
+    return idx, rs, q
+
+
+def large_algo() -> str:
+    """Solver for factors above the LDS Jacobi tier that the warm-start
+    acceptance test did not settle: ``KFAC_EIGH_LARGE`` = syevd | block.
+
+    Default syevd: on the real ResNet-50 step-100 refresh the native block
+    Jacobi (warm) needs 6-12 sweeps on the large A factors (the step-0
+    basis of a rank-deficient early factor is a poor start) and the mix
+    takes 1002 ms against 395 ms for syevd at equal accuracy
+    (profiles/refresh_probe_r2_resnet50_step100.jsonl)."""
+    return os.environ.get('KFAC_EIGH_LARGE', 'syevd')
+
+
+def _large_bucket(stack: torch.Tensor, warm: torch.Tensor | None
+                  ) -> tuple[torch.Tensor, torch.Tensor]:
+    n = stack.shape[-1]
+    if block_jacobi_enabled() and (
+        large_algo() == 'block' and (warm is not None or cold_algo() == 'block')
+    ):
+        return _block_jacobi(stack, warm)
+    algo = _algo_for(n)
+    if algo in ('sytrd', 'auto'):
+        algo = 'syevd'
+    if algo == 'torch':
+        return torch.linalg.eigh(stack)
+    evals, evecs = native().rocsolver_eigh(stack.contiguous(), _ALGOS[algo], 100, 1e-7)
+    return evals, evecs
+
+
+def _gpu_bucket(stack: torch.Tensor, warm: torch.Tensor | None = None
+                ) -> tuple[torch.Tensor, torch.Tensor]:
     n = stack.shape[-1]
     lib = native()
     if n <= JACOBI_MAX_N:
         return lib.jacobi_eigh(stack.contiguous(), JACOBI_SWEEPS, JACOBI_TOL)
-    algo = _algo_for(n)
-    if algo == 'sytrd':  # below KFAC_SYTRD_MIN_N
-        algo = 'syevd'
-    if algo == 'torch':
-        return torch.linalg.eigh(stack)
-    evals, evecs = lib.rocsolver_eigh(stack.contiguous(), _ALGOS[algo], 100, 1e-7)
-    return evals, evecs
+    if warm is not None and block_jacobi_enabled() and n <= WARM_ACCEPT_MAX_N:
+        idx, r, q = _accept_warm(stack, warm)
+        last_stats.setdefault('accepted', []).extend([n] * len(idx))
+        if len(idx) == stack.shape[0]:
+            return r, q
+        if idx:
+            rest = [i for i in range(stack.shape[0]) if i not in set(idx)]
+            sel = torch.tensor(rest, device=stack.device)
+            e2, v2 = _large_bucket(stack.index_select(0, sel).contiguous(),
+                                   warm.index_select(0, sel).contiguous())
+            evals = torch.empty(stack.shape[:2], dtype=e2.dtype, device=stack.device)
+            evecs = torch.empty_like(stack)
+            evals.index_copy_(0, torch.tensor(idx, device=stack.device), r)
+            evecs.index_copy_(0, torch.tensor(idx, device=stack.device), q)
+            evals.index_copy_(0, sel, e2)
+            evecs.index_copy_(0, sel, v2.contiguous())
+            return evals, evecs
+    return _large_bucket(stack, warm)
 
 
 def _bucket_cost(n: int, count: int) -> float:
@@ -104,15 +222,27 @@ def _bucket_cost(n: int, count: int) -> float:
 
 def eigh_many(
     mats: list[torch.Tensor],
+    warm: list[torch.Tensor | None] | None = None,
 ) -> list[tuple[torch.Tensor, torch.Tensor]]:
-    """Eigendecompose each symmetric matrix; returns ``[(evals, evecs)]``."""
+    """Eigendecompose each symmetric matrix; returns ``[(evals, evecs)]``.
+
+    ``warm[i]``, when given, is a previous eigenbasis of ``mats[i]``'s factor
+    (eigenvectors in columns); the block-Jacobi tier starts from it.  Size
+    buckets are split into warm and cold sub-buckets."""
     out: list[tuple[torch.Tensor, torch.Tensor] | None] = [None] * len(mats)
-    buckets: dict[tuple[int, torch.device], list[int]] = defaultdict(list)
+    buckets: dict[tuple, list[int]] = defaultdict(list)
     for i, m in enumerate(mats):
-        buckets[(m.shape[0], m.device)].append(i)
+        w = warm[i] if warm is not None else None
+        ok = (
+            w is not None and isinstance(w, torch.Tensor) and w.shape == m.shape
+            and w.dtype == torch.float32 and w.device == m.device
+        )
+        if warm is not None and not ok and w is not None:
+            warm[i] = None
+        buckets[(m.shape[0], m.device, bool(ok))].append(i)
     gpu = [(k, v) for k, v in buckets.items() if k[1].type == 'cuda']
     cpu = [(k, v) for k, v in buckets.items() if k[1].type != 'cuda']
-    for (n, _), idxs in cpu:
+    for (n, _, _), idxs in cpu:
         stack = torch.stack([mats[i].to(torch.float32) for i in idxs])
         evals, evecs = torch.linalg.eigh(stack)
         for k, i in enumerate(idxs):
@@ -130,7 +260,11 @@ def eigh_many(
                 key: torch.stack([mats[i].to(torch.float32) for i in idxs])
                 for key, idxs in gpu
             }
-            for i, r in _launch_jobs(gpu, stacks, dev).items():
+            warms = {
+                key: torch.stack([warm[i] for i in idxs])  # type: ignore[index]
+                for key, idxs in gpu if key[2]
+            }
+            for i, r in _launch_jobs(gpu, stacks, dev, warms).items():
                 out[i] = r
     return [o for o in out if o is not None]
 
@@ -159,15 +293,21 @@ def _jobs(gpu: list) -> list[tuple[tuple, list[int], int, int]]:
     return jobs
 
 
-def _run_lane(stream: torch.cuda.Stream, jobs: list, stacks: dict) -> list:
+def _run_lane(stream: torch.cuda.Stream, jobs: list, stacks: dict,
+              warms: dict | None = None) -> list:
     with torch.cuda.stream(stream):
-        return [_gpu_bucket(stacks[key][lo:hi]) for key, _, lo, hi in jobs]
+        res = []
+        for key, _, lo, hi in jobs:
+            w = warms.get(key) if warms else None
+            res.append(_gpu_bucket(stacks[key][lo:hi], None if w is None else w[lo:hi]))
+        return res
 
 
 def _launch_jobs(
     gpu: list,
     stacks: dict,
     dev: torch.device,
+    warms: dict | None = None,
 ) -> dict[int, tuple[torch.Tensor, torch.Tensor]]:
     """Run the solver jobs on ``KFAC_EIGH_STREAMS`` lanes (LPT on n^3), one
     host thread per lane, and join the lanes back into the current stream.
@@ -214,10 +354,10 @@ def _launch_jobs(
         s.wait_event(ready)
     if len(active) > 1 and _threads_enabled():
         pool = _executor(len(active))
-        futs = [pool.submit(_run_lane, s, ln, stacks) for s, ln in active]
+        futs = [pool.submit(_run_lane, s, ln, stacks, warms) for s, ln in active]
         results = [f.result() for f in futs]
     else:
-        results = [_run_lane(s, ln, stacks) for s, ln in active]
+        results = [_run_lane(s, ln, stacks, warms) for s, ln in active]
     for (s, ln), res in zip(active, results):
         main.wait_stream(s)
         for (key, idxs, lo, hi), (evals, evecs) in zip(ln, res):

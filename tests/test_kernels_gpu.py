@@ -339,3 +339,88 @@ def test_identity(cuda):
     c = torch.randn(70, 70, device=cuda)
     factors.identity_(c)
     assert torch.equal(c, torch.eye(70, device=cuda))
+
+
+def _kfac_like(n: int, seed: int, cuda, drift: float = 0.02):
+    """(old, new) K-FAC-like factors: EMA of batch covariances whose
+    underlying basis drifts by a small rotation between the two."""
+    g = torch.Generator().manual_seed(seed)
+    lam = torch.exp(-torch.arange(n, dtype=torch.float64) / max(n / 8, 1.0))
+    u, _ = torch.linalg.qr(torch.randn(n, n, generator=g, dtype=torch.float64))
+    k = torch.randn(n, n, generator=g, dtype=torch.float64) * drift / n ** 0.5
+    u2 = torch.linalg.matrix_exp(k - k.t()) @ u
+    m = max(32, n // 2)
+
+    def cov(b):
+        x = (torch.randn(m, n, generator=g, dtype=torch.float64) * lam.sqrt()) @ b.t()
+        return x.t() @ x / m
+
+    a = torch.eye(n, dtype=torch.float64)
+    for _ in range(12):
+        a = 0.95 * a + 0.05 * cov(u)
+    old = a.clone()
+    for _ in range(10):
+        a = 0.95 * a + 0.05 * cov(u2)
+    return old.float().to(cuda), a.float().to(cuda)
+
+
+@pytest.mark.parametrize('n', [129, 300, 640, 1025])
+def test_block_jacobi_cold_and_warm(cuda, n):
+    """K-HIP-3 large tier: cold start and warm start from the previous
+    eigenbasis both match a float64 reference to 1e-5 relative (eigenvalues
+    and reconstruction) with orthonormal vectors; the warm start needs
+    fewer sweeps."""
+    lib = _native.native()
+    old, new = _kfac_like(n, n, cuda)
+    _, q0 = torch.linalg.eigh(old.double())
+    q0 = q0.float().unsqueeze(0).contiguous()
+    sweeps = {}
+    for mode, warm in (('cold', None), ('warm', q0)):
+        d, q, sw, _ = lib.block_jacobi_eigh(new.unsqueeze(0).contiguous(), warm, 20, 1e-6, 1,
+                                             4e-6, True)
+        assert int(sw[0]) > 0, (mode, 'not converged')
+        sweeps[mode] = int(sw[0])
+        _check_eigpairs(new, d[0], q[0], tol=1e-5)
+        eye = torch.eye(n, device=cuda, dtype=torch.float64)
+        assert (q[0].double().t() @ q[0].double() - eye).abs().max().item() < 1e-5
+        assert bool((d[0][1:] >= d[0][:-1]).all())
+    assert sweeps['warm'] < sweeps['cold'], sweeps
+
+
+def test_eigh_many_warm_accept(cuda):
+    """A factor its previous basis still diagonalises keeps that basis (one
+    GEMM, no solve); the others of the bucket are solved; all exact."""
+    mats, warms = [], []
+    for j, n in enumerate((200, 200, 200, 333)):
+        old, new = _kfac_like(n, 200 + j, cuda)
+        if j == 0:
+            new = old.clone()  # unchanged factor
+        mats.append(new)
+        warms.append(torch.linalg.eigh(old.double())[1].float().contiguous())
+    linalg.last_stats.clear()
+    res = linalg.eigh_many(mats, warms)
+    for m, (d, q) in zip(mats, res):
+        _check_eigpairs(m, d, q)
+    assert linalg.last_stats.get('accepted') == [200], linalg.last_stats
+
+
+def test_eigh_many_block_jacobi_and_fallback(cuda, monkeypatch):
+    """KFAC_EIGH_LARGE=block routes the large factors through the native
+    block Jacobi (warm where a previous basis is given); a factor that does
+    not converge within the sweep budget falls back to syevd, still exact."""
+    monkeypatch.setenv('KFAC_EIGH_LARGE', 'block')
+    mats, warms = [], []
+    for j, n in enumerate((200, 200, 333, 96)):
+        old, new = _kfac_like(n, 100 + j, cuda)
+        mats.append(new)
+        warms.append(torch.linalg.eigh(old.double())[1].float() if j != 1 else None)
+    linalg.last_stats.clear()
+    res = linalg.eigh_many(mats, warms)
+    for m, (d, q) in zip(mats, res):
+        _check_eigpairs(m, d, q)
+    assert linalg.last_stats['sweeps'], linalg.last_stats
+    monkeypatch.setattr(linalg, 'BJ_MAX_SWEEPS_WARM', 1)
+    monkeypatch.setattr(linalg, 'BJ_MAX_SWEEPS_COLD', 1)
+    res = linalg.eigh_many(mats, warms)
+    for m, (d, q) in zip(mats, res):
+        _check_eigpairs(m, d, q)
