@@ -95,6 +95,7 @@ std::vector<at::Tensor> block_jacobi_eigh(at::Tensor A, c10::optional<at::Tensor
                                           int64_t max_sweeps, double tol,
                                           int64_t inner_sweeps, double noise, bool refine);
 at::Tensor spd_inverse(at::Tensor F, double damping);
+std::vector<at::Tensor> spd_inverse_blocked(at::Tensor F, double damping);
 std::vector<at::Tensor> sytrd_reduce(std::vector<at::Tensor> stacks);
 std::vector<at::Tensor> tridiag_eigvecs(at::Tensor A, at::Tensor d, at::Tensor e,
                                         at::Tensor tau);
@@ -795,6 +796,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_act", &bn_act);
   m.def("spd_lds_max_n", &spd_lds_max_n);
   m.def("spd_inverse", &spd_inverse, py::call_guard<py::gil_scoped_release>());
+  m.def("spd_inverse_blocked", &spd_inverse_blocked, py::call_guard<py::gil_scoped_release>());
   m.def("sytrd_reduce", &sytrd_reduce, py::call_guard<py::gil_scoped_release>());
   m.def("tridiag_eigvecs", &tridiag_eigvecs, py::call_guard<py::gil_scoped_release>());
   m.def("rocsolver_eigh", &rocsolver_eigh, py::call_guard<py::gil_scoped_release>(),

@@ -26,6 +26,7 @@
 // The skipped-pair count per sweep is the convergence signal (read by the
 // host once per sweep).
 #include "common.h"
+#include "mfma_tile.h"
 
 namespace kfac {
 
@@ -36,9 +37,9 @@ constexpr int PB = 2 * BB;      // pair block edge (64)
 constexpr int PLD = PB + 1;     // padded LDS row for the pair solve
 constexpr int PT = 256;         // threads of the pair solve
 constexpr int AT = 256;         // threads of the apply kernel (4 waves)
-constexpr int ALD = PB + 4;     // LDS row of the apply tiles (68 floats)
+constexpr int ALD = tile::TILE_LD;  // LDS row of the apply tiles (68 floats)
 
-typedef float v16f __attribute__((ext_vector_type(16)));
+using tile::v16f;
 
 // circle method over m players (m even): pair k of round r
 __device__ __forceinline__ void rr_pair(int m, int r, int k, int& p, int& q) {
@@ -211,38 +212,9 @@ bj_pair_solve(BJArgs a) {
 }
 
 // ---------------------------------------------------------------- apply
-// 64x64x64 fp32 MFMA product on LDS tiles: each of the 4 waves computes one
-// 32x32 quadrant (wi, wj) of  C = A^T * Bt  with A stored [k][i] and Bt
-// stored [k][j] (row stride ALD): both operand reads are 32 consecutive
-// floats per half-wave (conflict-free).
-__device__ __forceinline__ v16f mm64(const float* A, const float* Bt, int wi, int wj) {
-  const int l = threadIdx.x & 63;
-  const int r = l & 31, h = l >> 5;
-  v16f acc;
-#pragma unroll
-  for (int e = 0; e < 16; ++e) acc[e] = 0.f;
-#pragma unroll 8
-  for (int k = 0; k < PB; k += 2) {
-    const float av = A[(k + h) * ALD + wi * 32 + r];   // A^T[i][k]
-    const float bv = Bt[(k + h) * ALD + wj * 32 + r];  // Bt[k][j]
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
-  }
-  return acc;
-}
-
-// a wave's 32x32 accumulator quadrant -> LDS tile T[i][j] (TRANS: T[j][i])
-// C/D layout of 32x32 MFMA: col = lane & 31, row = (e & 3) + 8 (e >> 2) + 4 (lane >> 5)
-template <bool TRANS>
-__device__ __forceinline__ void store_quad(float* T, const v16f& acc, int wi, int wj) {
-  const int l = threadIdx.x & 63;
-#pragma unroll
-  for (int e = 0; e < 16; ++e) {
-    const int row = wi * 32 + (e & 3) + 8 * (e >> 2) + 4 * (l >> 5);
-    const int col = wj * 32 + (l & 31);
-    if (TRANS) T[col * ALD + row] = acc[e];
-    else T[row * ALD + col] = acc[e];
-  }
-}
+// 64x64 tile products: mfma_tile.h (fp32 MFMA, k-major LDS operands)
+using tile::mm64;
+using tile::store_quad;
 
 __global__ void __launch_bounds__(AT)
 bj_apply(BJArgs a, int nb_groups) {

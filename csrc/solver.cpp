@@ -265,3 +265,34 @@ at::Tensor spd_inverse(at::Tensor F, double damping) {
                         n * n, n * n, (float)damping, s);
   return X;
 }
+
+// ---------------------------------------------------------------------------
+// K-HIP-5 blocked tier (csrc/spdinv_chol.hip): blocked Cholesky + triangular
+// inverse + W^T W on fp32 MFMA tiles, any n.  Returns (X [cnt, n, n] exactly
+// symmetric, failed [cnt] int32: 1 where a Cholesky pivot was non-positive /
+// non-finite -- the caller re-solves those with a pivoted LU so no NaN is
+// ever installed).
+namespace kfac {
+int64_t spd_chol_pad(int64_t n);
+void spd_inverse_chol(const float* F, float* X, float* M, float* W, float* Linv, int* fail,
+                      int64_t n, int batch, float damping, hipStream_t s);
+}  // namespace kfac
+
+std::vector<at::Tensor> spd_inverse_blocked(at::Tensor F, double damping) {
+  TORCH_CHECK(F.is_cuda() && F.scalar_type() == at::kFloat && F.dim() == 3 &&
+              F.size(1) == F.size(2) && F.is_contiguous());
+  const int64_t cnt = F.size(0), n = F.size(1);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(F.device());
+  hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+  auto X = at::empty_like(F);
+  auto fail = at::zeros({cnt}, F.options().dtype(at::kInt));
+  if (cnt == 0 || n == 0) return {X, fail};
+  const int64_t N = kfac::spd_chol_pad(n);
+  auto M = at::empty({cnt, N, N}, F.options());
+  auto W = at::empty({cnt, N, N}, F.options());
+  auto L = at::empty({cnt, N / 64, 64, 64}, F.options());
+  kfac::spd_inverse_chol(F.data_ptr<float>(), X.data_ptr<float>(), M.data_ptr<float>(),
+                         W.data_ptr<float>(), L.data_ptr<float>(), fail.data_ptr<int>(), n,
+                         (int)cnt, (float)damping, s);
+  return {X, fail};
+}

@@ -475,16 +475,21 @@ def eigh(mat: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
 
 def inverse_many(mats: list[torch.Tensor], damping: float) -> list[torch.Tensor]:
     """``(F + damping I)^-1`` for every symmetric factor, fp32, batched by
-    size: n <= ``spd_lds_max_n()`` in ONE launch per size (K-HIP-5,
-    csrc/spdinv.hip: Gauss-Jordan in LDS, one workgroup per matrix), larger
-    n one Cholesky + ``cholesky_inverse`` per matrix.  No host
-    synchronisation; the results are exactly symmetric.  CPU tensors use
-    the PyTorch math.
+    size (K-HIP-5, csrc/spdinv_chol.hip): blocked Cholesky, triangular
+    inverse and W^T W on fp32 MFMA tiles, every factor of a size in one
+    launch per block step; exactly symmetric results.
 
-    Batched Cholesky is avoided for n > 176: on MI355X (ROCm 7.2 rocSOLVER)
-    the strided-batched potrf + potri path returned sporadic NaN rows
-    (csrc/solver.cpp ``spd_inverse``) and torch's batched ``cholesky_ex``
-    returned wrong inverses and then faulted (tools/spd_dbg.py)."""
+    Gauss-Jordan without exchanges (the one-workgroup LDS kernel,
+    csrc/spdinv.hip, still available with ``KFAC_SPD_SMALL=gj``) was 50x
+    less accurate than fp32 LU on rank-deficient factors at the reference
+    damping -- the cause of the INVERSE-method divergence on ResNet-32 --
+    while Cholesky has LU's backward stability at half the flops.
+
+    Robustness: a factor whose Cholesky pivots fail (non-positive or
+    non-finite), or whose result is not finite, is re-solved with a pivoted
+    LU (``torch.linalg.inv``, the reference's routine) -- never installed as
+    NaN.  That check costs one host read-back per size bucket per
+    second-order update.  CPU tensors use the PyTorch math."""
     out: list[torch.Tensor | None] = [None] * len(mats)
     buckets: dict[tuple[int, torch.device], list[int]] = defaultdict(list)
     for i, m in enumerate(mats):
@@ -492,12 +497,22 @@ def inverse_many(mats: list[torch.Tensor], damping: float) -> list[torch.Tensor]
     for (_, dev), idxs in buckets.items():
         n = mats[idxs[0]].shape[0]
         if dev.type == 'cuda' and use_native(mats[idxs[0]]):
-            stack = torch.stack([mats[i].to(torch.float32) for i in idxs])
-            if n <= int(native().spd_lds_max_n()):
+            stack = torch.stack([mats[i].to(torch.float32) for i in idxs]).contiguous()
+            if os.environ.get('KFAC_SPD_SMALL', 'chol') == 'gj' and n <= int(
+                    native().spd_lds_max_n()):
                 inv = native().spd_inverse(stack, float(damping))
+                bad = ~torch.isfinite(inv).flatten(1).all(dim=1)
             else:
-                inv = torch.stack([_damped_inverse_torch(m, damping) for m in stack])
-                inv = 0.5 * (inv + inv.transpose(-1, -2))
+                inv, fail = native().spd_inverse_blocked(stack, float(damping))
+                bad = (fail != 0) | ~torch.isfinite(inv).flatten(1).all(dim=1)
+            failed = bad.nonzero().flatten().tolist()
+            if failed:
+                logger.warning('damped inverse: %d factor(s) of n=%d failed the '
+                               'no-pivoting elimination; using LU', len(failed), n)
+                for k in failed:
+                    a = stack[k] + damping * torch.eye(n, device=dev, dtype=torch.float32)
+                    x = torch.linalg.inv(a.double()).float()
+                    inv[k] = 0.5 * (x + x.t())
             for k, i in enumerate(idxs):
                 out[i] = inv[k]
         else:
@@ -513,17 +528,13 @@ def damped_inverse(mat: torch.Tensor, damping: float) -> torch.Tensor:
 
 
 def _damped_inverse_torch(mat: torch.Tensor, damping: float) -> torch.Tensor:
-    """PyTorch math: the damped factor is SPD, so a Cholesky factorisation
-    plus ``cholesky_inverse`` replaces the general LU inverse (half the
-    flops, no pivoting); if the factorisation fails (indefinite input) it
-    falls back to ``torch.linalg.inv``."""
+    """PyTorch math (CPU): the damped factor is SPD, so a Cholesky
+    factorisation plus ``cholesky_inverse`` replaces the general LU inverse
+    (half the flops, no pivoting); if the factorisation fails (indefinite
+    input) it falls back to ``torch.linalg.inv``."""
     a = mat.to(torch.float32)
     a = a + damping * torch.eye(a.shape[-1], dtype=a.dtype, device=a.device)
     chol, info = torch.linalg.cholesky_ex(a)
-    if a.is_cuda:
-        # no host sync on the GPU: a damped K-FAC factor is SPD by
-        # construction (PSD running average + damping * I)
-        return torch.cholesky_inverse(chol)
     if bool((info != 0).any()):
         return torch.linalg.inv(a)
     return torch.cholesky_inverse(chol)

@@ -278,12 +278,12 @@ def test_eigh_many_sytrd_tier(cuda, monkeypatch, sizes):
         _check_eigpairs(m, d, q)
 
 
-@pytest.mark.parametrize('n', [1, 7, 64, 129, 176, 177, 300, 640])
+@pytest.mark.parametrize('n', [1, 7, 64, 129, 176, 177, 300, 577, 640, 2049])
 def test_spd_inverse(cuda, n):
-    """K-HIP-5: LDS Gauss-Jordan (n <= 176) and batched Cholesky (larger n)
-    damped inverses vs a float64 reference; exactly symmetric."""
+    """K-HIP-5: LDS Gauss-Jordan (n <= 176) and blocked MFMA Gauss-Jordan
+    (larger n) damped inverses vs a float64 reference; exactly symmetric."""
     torch.manual_seed(n)
-    b, damping = 3, 1e-2
+    b, damping = (3 if n < 1000 else 2), 1e-2
     x = torch.randn(b, n, 2 * n, device=cuda)
     f = x @ x.transpose(1, 2) / (2 * n)
     got = torch.stack(linalg.inverse_many(list(f), damping))
@@ -424,3 +424,37 @@ def test_eigh_many_block_jacobi_and_fallback(cuda, monkeypatch):
     res = linalg.eigh_many(mats, warms)
     for m, (d, q) in zip(mats, res):
         _check_eigpairs(m, d, q)
+
+
+@pytest.mark.parametrize('n', [177, 577, 2049])
+def test_spd_inverse_rank_deficient_kfac(cuda, n):
+    """Rank-deficient PSD factors (fewer rows than columns, as for the
+    ResNet-50 layer4 A factors at batch 32) at the reference damping
+    (condition number ~1e3-1e4): the blocked kernel is as accurate as the
+    reference's fp32 routine (torch.linalg.inv, pivoted LU) against float64."""
+    torch.manual_seed(n + 1)
+    x = torch.randn(n // 3, n, device=cuda)
+    f = (x.t() @ x / (n // 3)).contiguous()
+    damping = 1e-3
+    inv, fail = _native.native().spd_inverse_blocked(f.unsqueeze(0).contiguous(), damping)
+    assert int(fail[0]) == 0
+    eye = torch.eye(n, device=cuda)
+    ref = torch.linalg.inv(f.double() + damping * eye.double())
+    err = (inv[0].double() - ref).abs().max().item()
+    lu32 = torch.linalg.inv(f + damping * eye)
+    err_lu = (lu32.double() - ref).abs().max().item()
+    assert err <= 4 * err_lu + 1e-6 * ref.abs().max().item(), (err, err_lu)
+
+
+def test_inverse_many_indefinite_falls_back(cuda):
+    """An indefinite 'damped factor' (e.g. a corrupted running average) makes
+    the no-exchange elimination fail; inverse_many detects it on the device
+    and re-solves with a pivoted LU: no NaN is installed."""
+    for n in (40, 300):
+        f = torch.eye(n, device=cuda)
+        f[0, 0] = -1.0  # F + damping I is indefinite
+        f[1, 1] = -0.5
+        got = linalg.inverse_many([f], 0.01)[0]
+        assert bool(torch.isfinite(got).all())
+        ref = torch.linalg.inv(f.double() + 0.01 * torch.eye(n, device=cuda, dtype=torch.float64))
+        assert (got.double() - ref).abs().max().item() < 1e-4 * ref.abs().max().item()
