@@ -570,6 +570,10 @@ class BaseKFACPreconditioner:
                 l.compute_g_inv(damping=damping)
 
     @staticmethod
+    def _bcast_inv(fn: Callable[..., None], src: int, group: Any) -> None:
+        fn(src=src, group=group, bucketed=True)
+
+    @staticmethod
     def _warm_basis(q: Any, factor: torch.Tensor) -> torch.Tensor | None:
         if (
             os.environ.get('KFAC_EIGH_WARM', '1') == '0'
@@ -607,16 +611,17 @@ class BaseKFACPreconditioner:
                 self._compute_second_order(ordered)
             if self._assignment.broadcast_inverses():
                 with tracing.phase('inverse_broadcast'):
+                    # fused per (column group, source) buckets: a handful of
+                    # RCCL broadcasts instead of ~4 per layer
                     for name, layer in ordered:
                         if self._assignment.is_grad_worker(name):
-                            layer.broadcast_a_inv(
-                                src=self._assignment.inv_worker(name, 'A'),
-                                group=self._assignment.grad_worker_group(name),
-                            )
-                            layer.broadcast_g_inv(
-                                src=self._assignment.inv_worker(name, 'G'),
-                                group=self._assignment.grad_worker_group(name),
-                            )
+                            self._bcast_inv(layer.broadcast_a_inv,
+                                            self._assignment.inv_worker(name, 'A'),
+                                            self._assignment.grad_worker_group(name))
+                            self._bcast_inv(layer.broadcast_g_inv,
+                                            self._assignment.inv_worker(name, 'G'),
+                                            self._assignment.grad_worker_group(name))
+                    self._tdc.flush_broadcast_buckets()
             self._tdc.flush_allreduce_buckets()
             # eigenbases changed: refresh their bf16 hi/lo planes for the
             # grouped GEMMs now, eagerly (never inside a later graph capture)
@@ -764,15 +769,31 @@ class BaseKFACPreconditioner:
                 lambda g, m=module: self._save_grad_output(m, None, (g,)),
             )
 
+    @staticmethod
+    def _stream_friendly_backend() -> bool:
+        """Collectives that stay device-side: RCCL ('nccl') orders its
+        all-reduce after the issuing (side) stream with a HIP event, so the
+        factor SYRK + all-reduce chain overlaps forward / backward.  gloo
+        stages GPU tensors through the host: there the side stream only adds
+        host round trips (2-rank gloo rehearsal on one GPU: factor phases
+        65-236 ms/step against <1 ms inline,
+        profiles/fstream_w2_ab_mi355x.jsonl), so it stays inline."""
+        if get_world_size() <= 1:
+            return True
+        try:
+            import torch.distributed as dist
+
+            return dist.get_backend() == 'nccl'
+        except (RuntimeError, ValueError):
+            return False
+
     def _factor_stream(self, t: torch.Tensor) -> torch.cuda.Stream | None:
-        # KFAC_FACTOR_STREAM: 1 force on, 0 force off, unset = single-process
-        # jobs only.  Multi-rank it stays inline: in the 2-rank rehearsal
-        # (profiles/fstream_w2_ab_mi355x.jsonl) the side stream made the
-        # factor phases 65-236 ms/step against <1 ms inline.
+        # KFAC_FACTOR_STREAM: 1 force on, 0 force off, unset = on for
+        # single-process jobs and RCCL process groups
         mode = os.environ.get('KFAC_FACTOR_STREAM', 'auto')
         if not t.is_cuda or self._factor_stream_off or mode == '0':
             return None
-        if mode != '1' and get_world_size() > 1:
+        if mode != '1' and not self._stream_friendly_backend():
             return None
         dev = t.device
         s = self._factor_streams.get(dev)

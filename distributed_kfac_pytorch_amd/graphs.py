@@ -33,16 +33,25 @@ K-FAC state (``steps``) exactly as an eager step would.  Values baked into a
 graph -- K-FAC hyperparameters, the optimizer's learning rates -- form a
 signature; when it changes the affected graphs are dropped and re-captured.
 
-Graphs are used only without a multi-rank process group: factor all-reduces
-and gradient broadcasts are torch.distributed async work with host-side
-completion callbacks, which a graph cannot replay.  With a world size > 1 the
-runner executes every step eagerly.
+Multi-rank jobs run every step eagerly by default (the K-FAC precondition
+phase is still replayed from ``StepGraphs``).  The K-FAC collectives
+themselves no longer block capture (``AsyncTensor`` has no host callbacks:
+``Work.wait()`` only orders the current stream after RCCL's), but the DDP
+gradient all-reduce does: DDP's C++ reducer launches its bucket all-reduces
+from autograd hooks, rebuilds its buckets during the first iterations, and
+ProcessGroupNCCL's watchdog polls each collective's HIP event from its own
+thread.  Capturing that needs DDP built under a side stream, the bucket
+rebuild finished before capture, and asynchronous error handling off --
+none of which can be validated here (no multi-GPU RCCL box is available to
+this build).  ``KFAC_STEP_GRAPHS_MULTI=1`` opts a multi-rank job in; a
+capture that raises falls back to eager steps.
 """
 from __future__ import annotations
 
 import contextlib
 import gc
 import logging
+import os
 from collections import defaultdict
 from typing import Any
 from typing import Callable
@@ -99,8 +108,9 @@ class GraphedTrainStep:
         self.preconditioner = preconditioner
         self.warmup = warmup
         if enabled is None:
-            enabled = torch.cuda.is_available() and not (
-                dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+            multi = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+            enabled = torch.cuda.is_available() and (
+                not multi or os.environ.get('KFAC_STEP_GRAPHS_MULTI', '0') == '1'
             )
         self.enabled = enabled
         self.graphs: dict[str, torch.cuda.CUDAGraph] = {}

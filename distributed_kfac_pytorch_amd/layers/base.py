@@ -174,10 +174,12 @@ class KFACBaseLayer:
         }
 
     # ---------------------------------------------------------- second order
-    def broadcast_a_inv(self, src: int, group: dist.ProcessGroup | None = None) -> None:
+    def broadcast_a_inv(self, src: int, group: dist.ProcessGroup | None = None,
+                        bucketed: bool = False) -> None:
         raise NotImplementedError
 
-    def broadcast_g_inv(self, src: int, group: dist.ProcessGroup | None = None) -> None:
+    def broadcast_g_inv(self, src: int, group: dist.ProcessGroup | None = None,
+                        bucketed: bool = False) -> None:
         raise NotImplementedError
 
     def compute_a_inv(self, damping: float = 0.001) -> None:

@@ -159,8 +159,18 @@ class KFACEigenLayer(KFACBaseLayer):
         return self._qa_hl, self._qg_hl
 
     # ------------------------------------------------------------ broadcasts
-    def broadcast_a_inv(self, src: int, group: dist.ProcessGroup | None = None) -> None:
-        """Broadcast QA (and dA unless prediv) from the A inverse worker."""
+    def _bcast(self, t: torch.Tensor, src: int, group: dist.ProcessGroup | None,
+               bucketed: bool) -> Any:
+        if bucketed and self.tdc.bucket_cap_bytes > 0 and t.is_contiguous():
+            # fused per-(group, src) broadcast; flushed by the preconditioner
+            return self.tdc.broadcast_bucketed(t, src=src, group=group)
+        return self.tdc.broadcast(t, src=src, group=group)
+
+    def broadcast_a_inv(self, src: int, group: dist.ProcessGroup | None = None,
+                        bucketed: bool = False) -> None:
+        """Broadcast QA (and dA unless prediv) from the A inverse worker.
+        ``bucketed`` fuses the tensors per (group, src) bucket; the caller
+        must then call ``tdc.flush_broadcast_buckets()`` on every rank."""
         if self.qa is None or (not self.prediv_eigenvalues and self.da is None):
             if get_rank() == src:
                 raise RuntimeError(
@@ -171,12 +181,13 @@ class KFACEigenLayer(KFACBaseLayer):
             dev = self.module.device
             self.qa = torch.empty(d, d, device=dev, dtype=self.inv_dtype)
             self.da = torch.empty(d, device=dev, dtype=self.inv_dtype)
-        self.qa = self.tdc.broadcast(self.qa, src=src, group=group)
+        self.qa = self._bcast(self.qa, src, group, bucketed)
         if not self.prediv_eigenvalues:
             assert self.da is not None
-            self.da = self.tdc.broadcast(self.da, src=src, group=group)
+            self.da = self._bcast(self.da, src, group, bucketed)
 
-    def broadcast_g_inv(self, src: int, group: dist.ProcessGroup | None = None) -> None:
+    def broadcast_g_inv(self, src: int, group: dist.ProcessGroup | None = None,
+                        bucketed: bool = False) -> None:
         """Broadcast QG and dG (or dGdA with prediv) from the G worker."""
         if (
             self.qg is None
@@ -196,13 +207,13 @@ class KFACEigenLayer(KFACBaseLayer):
                 self.dg = torch.empty(g, device=dev, dtype=self.inv_dtype)
             else:
                 self.dgda = torch.empty(g, a, device=dev, dtype=self.inv_dtype)
-        self.qg = self.tdc.broadcast(self.qg, src=src, group=group)
+        self.qg = self._bcast(self.qg, src, group, bucketed)
         if not self.prediv_eigenvalues:
             assert self.dg is not None
-            self.dg = self.tdc.broadcast(self.dg, src=src, group=group)
+            self.dg = self._bcast(self.dg, src, group, bucketed)
         else:
             assert self.dgda is not None
-            self.dgda = self.tdc.broadcast(self.dgda, src=src, group=group)
+            self.dgda = self._bcast(self.dgda, src, group, bucketed)
 
     # ---------------------------------------------------------- decomposition
     def _eig(self, factor: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:

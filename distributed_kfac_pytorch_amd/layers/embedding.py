@@ -139,7 +139,7 @@ class KFACEmbeddingEigenLayer(_DiagonalAMixin, KFACEigenLayer):
         self._da_store = torch.clamp(self.a_factor.to(self.inv_dtype), min=0.0)
         self.da = self._da_store
 
-    def broadcast_a_inv(self, src: int, group: Any = None) -> None:
+    def broadcast_a_inv(self, src: int, group: Any = None, bucketed: bool = False) -> None:
         if self.da is None:
             v = self.module.a_factor_shape[0]
             self.da = torch.empty(v, device=self.module.device, dtype=self.inv_dtype)
@@ -176,7 +176,7 @@ class KFACEmbeddingInverseLayer(_DiagonalAMixin, KFACInverseLayer):
             raise RuntimeError('Cannot invert A before A has been computed')
         self.a_inv = (1.0 / (self.a_factor.to(torch.float32) + damping)).to(self.inv_dtype)
 
-    def broadcast_a_inv(self, src: int, group: Any = None) -> None:
+    def broadcast_a_inv(self, src: int, group: Any = None, bucketed: bool = False) -> None:
         if self.a_inv is None:
             v = self.module.a_factor_shape[0]
             self.a_inv = torch.empty(v, device=self.module.device, dtype=self.inv_dtype)

@@ -60,7 +60,17 @@ class KFACInverseLayer(KFACBaseLayer):
     def _sym(self) -> bool:
         return self.symmetric_factors and self.symmetry_aware
 
-    def broadcast_a_inv(self, src: int, group: dist.ProcessGroup | None = None) -> None:
+    def _bcast(self, t: torch.Tensor, src: int, group: dist.ProcessGroup | None,
+               bucketed: bool) -> Any:
+        if self._sym():
+            # triangle-packed broadcasts stay per tensor
+            return self.tdc.broadcast(t, src=src, group=group, symmetric=True)
+        if bucketed and self.tdc.bucket_cap_bytes > 0 and t.is_contiguous():
+            return self.tdc.broadcast_bucketed(t, src=src, group=group)
+        return self.tdc.broadcast(t, src=src, group=group)
+
+    def broadcast_a_inv(self, src: int, group: dist.ProcessGroup | None = None,
+                        bucketed: bool = False) -> None:
         if self.a_inv is None:
             if get_rank() == src:
                 raise RuntimeError(
@@ -71,11 +81,10 @@ class KFACInverseLayer(KFACBaseLayer):
             self.a_inv = torch.empty(
                 d, d, device=self.module.device, dtype=self.inv_dtype,
             )
-        self.a_inv = self.tdc.broadcast(
-            self.a_inv, src=src, group=group, symmetric=self._sym(),
-        )
+        self.a_inv = self._bcast(self.a_inv, src, group, bucketed)
 
-    def broadcast_g_inv(self, src: int, group: dist.ProcessGroup | None = None) -> None:
+    def broadcast_g_inv(self, src: int, group: dist.ProcessGroup | None = None,
+                        bucketed: bool = False) -> None:
         if self.g_inv is None:
             if get_rank() == src:
                 raise RuntimeError(
@@ -86,9 +95,7 @@ class KFACInverseLayer(KFACBaseLayer):
             self.g_inv = torch.empty(
                 d, d, device=self.module.device, dtype=self.inv_dtype,
             )
-        self.g_inv = self.tdc.broadcast(
-            self.g_inv, src=src, group=group, symmetric=self._sym(),
-        )
+        self.g_inv = self._bcast(self.g_inv, src, group, bucketed)
 
     def _inverse(self, f: torch.Tensor, damping: float) -> torch.Tensor:
         if self.symmetric_factors:

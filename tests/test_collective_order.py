@@ -1,0 +1,115 @@
+"""Deadlock guard: every rank of a communicator must issue the same
+collective sequence.
+
+Records ``(op, group ranks, numel, dtype, src)`` for every
+``torch.distributed`` collective the K-FAC runtime issues on each of 4 gloo
+ranks across factor-update, second-order-update and plain steps (DDP's own
+gradient all-reduces run inside its C++ reducer and are not recorded), then
+asserts that for every process group all of its members recorded the
+identical sequence.  Covers HYBRID-OPT (gwf 0.5: column and row subgroups
+plus the world group), MEM-OPT and COMM-OPT, both compute methods, small
+and default bucket caps.  Reference semantics: ``kfac/base_preconditioner.py:
+308-380`` issues collectives in reversed registration order on all ranks.
+"""
+from __future__ import annotations
+
+import pytest
+import torch
+import torch.distributed as dist
+
+import distributed_kfac_pytorch_amd as kfac
+from tests.harness import run_distributed
+
+
+class _Net(torch.nn.Module):
+    def __init__(self) -> None:
+        super().__init__()
+        self.conv1 = torch.nn.Conv2d(3, 8, 3, padding=1)
+        self.conv2 = torch.nn.Conv2d(8, 8, 3, stride=2, padding=1, bias=False)
+        self.fc1 = torch.nn.Linear(8 * 4 * 4, 32)
+        self.fc2 = torch.nn.Linear(32, 10)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        x = torch.relu(self.conv1(x))
+        x = torch.relu(self.conv2(x))
+        x = torch.relu(self.fc1(x.flatten(1)))
+        return self.fc2(x)
+
+
+def _record(frac: float, method: str, bucket_mb: float, steps: int) -> None:
+    world = dist.get_world_size()
+    rank = dist.get_rank()
+    calls: list[tuple] = []
+    originals = {}
+
+    def group_ranks(group) -> tuple:  # type: ignore[no-untyped-def]
+        if group is None:
+            return tuple(range(world))
+        return tuple(dist.get_process_group_ranks(group))
+
+    def wrap(name: str):  # type: ignore[no-untyped-def]
+        fn = getattr(dist, name)
+        originals[name] = fn
+
+        def inner(tensor, *args, **kwargs):  # type: ignore[no-untyped-def]
+            if name == 'broadcast':
+                src = kwargs.get('src', args[0] if args else None)
+                group = kwargs.get('group', args[1] if len(args) > 1 else None)
+            else:
+                src = None
+                group = kwargs.get('group', args[1] if len(args) > 1 else None)
+            calls.append((name, group_ranks(group), tensor.numel(), str(tensor.dtype), src))
+            return fn(tensor, *args, **kwargs)
+        setattr(dist, name, inner)
+
+    torch.manual_seed(0)
+    model = torch.nn.parallel.DistributedDataParallel(_Net())
+    opt = torch.optim.SGD(model.parameters(), lr=0.05)
+    pre = kfac.KFACPreconditioner(
+        model, factor_update_steps=2, inv_update_steps=4,
+        grad_worker_fraction=frac, compute_method=method,
+        allreduce_bucket_cap_mb=bucket_mb,
+    )
+    g = torch.Generator().manual_seed(rank)
+    x = torch.randn(8, 3, 8, 8, generator=g)
+    y = torch.randint(0, 10, (8,), generator=g)
+    for name in ('all_reduce', 'broadcast', 'all_gather', 'reduce_scatter'):
+        wrap(name)
+    try:
+        for _ in range(steps):
+            opt.zero_grad()
+            torch.nn.functional.cross_entropy(model(x), y).backward()
+            pre.step()
+            opt.step()
+        pre.state_dict()
+    finally:
+        for name, fn in originals.items():
+            setattr(dist, name, fn)
+    assert calls, 'no collective recorded'
+    everyone: list = [None] * world
+    dist.all_gather_object(everyone, calls)
+    groups = {c[1] for per_rank in everyone for c in per_rank}
+    for grp in groups:
+        seqs = {r: [c for c in everyone[r] if c[1] == grp] for r in grp}
+        ref = seqs[grp[0]]
+        for r, seq in seqs.items():
+            assert seq == ref, (
+                f'group {grp}: rank {r} issued {len(seq)} collectives, rank {grp[0]} '
+                f'{len(ref)}; first difference at '
+                f'{next((i for i, (a, b) in enumerate(zip(seq, ref)) if a != b), min(len(seq), len(ref)))}'
+            )
+    for r, per_rank in enumerate(everyone):
+        assert all(r in c[1] for c in per_rank), f'rank {r} used a group it is not in'
+
+
+@pytest.mark.parametrize(
+    'frac,method,bucket_mb',
+    [
+        (0.5, 'eigen', 25.0),     # HYBRID-OPT: inverse + gradient broadcasts
+        (0.5, 'eigen', 0.001),    # one bucket per tensor
+        (0.25, 'inverse', 25.0),  # MEM-OPT
+        (1.0, 'inverse', 0.0),    # COMM-OPT, unbucketed all-reduce
+    ],
+)
+def test_collective_sequences_match(frac, method, bucket_mb):
+    run_distributed(_record, 4, frac, method, bucket_mb, 9)
