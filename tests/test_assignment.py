@@ -152,3 +152,26 @@ def test_repr_lists_layers():
                         grad_worker_fraction=1.0, group_func=identity)
     s = repr(a)
     assert 'layer="x"' in s and 'inv_workers' in s
+
+
+def _expectation_cases() -> list:
+    import json
+    import os
+
+    path = os.path.join(os.path.dirname(__file__), 'data', 'assignment_expectations.json')
+    with open(path) as f:
+        return [pytest.param(*c[1:], id=c[0]) for c in json.load(f)['cases']]
+
+
+@pytest.mark.parametrize(
+    'work,worker_groups,world_size,colocate,expected', _expectation_cases(),
+)
+def test_greedy_assignment_reference_table(work, worker_groups, world_size, colocate,
+                                           expected):
+    """The reference's exact greedy placements, including its tie-break
+    order (descending cost, then descending key), pinned as data."""
+    from distributed_kfac_pytorch_amd.parallel.assignment import KAISAAssignment
+
+    assert KAISAAssignment.greedy_assignment(
+        work, worker_groups, world_size, colocate,
+    ) == expected
