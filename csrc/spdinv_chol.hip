@@ -65,50 +65,51 @@ __global__ void __launch_bounds__(CT) chol_diag(CholArgs a) {
   __shared__ float L[T64 * DLD];
   __shared__ float Vi[T64 * DLD];
   const int mat = blockIdx.x, tid = threadIdx.x;
+  const int j = tid & 63, i0 = tid >> 6;  // thread owns column j, rows i0 + 4 r
   const int64_t N = a.N;
   float* Mk = tile_at(a.M, mat, N, a.k, a.k);
   for (int e = tid; e < T64 * T64; e += CT) {
-    const int i = e >> 6, j = e & 63;
-    L[i * DLD + j] = Mk[(int64_t)i * N + j];
+    const int i = e >> 6, c = e & 63;
+    L[i * DLD + c] = Mk[(int64_t)i * N + c];
+    Vi[i * DLD + c] = i == c ? 1.f : 0.f;
   }
   __syncthreads();
   bool bad = false;
+  // right-looking Cholesky of the 64x64 block (lower triangle)
   for (int p = 0; p < T64; ++p) {
     const float d = L[p * DLD + p];
     bad |= !(d > 0.f) || !isfinite(d);
-    const float s = sqrtf(fmaxf(d, 1e-30f));
-    const float rs = 1.f / s;
+    const float sd = sqrtf(fmaxf(d, 1e-30f));
     __syncthreads();
-    // column p below the diagonal, then the trailing lower update
-    if (tid < T64 && tid > p) L[tid * DLD + p] *= rs;
-    if (tid == p) L[p * DLD + p] = s;
+    if (tid < T64) {
+      if (tid > p) L[tid * DLD + p] *= 1.f / sd;
+      else if (tid == p) L[p * DLD + p] = sd;
+    }
     __syncthreads();
-    const int m = T64 - p - 1;
-    for (int e = tid; e < m * m; e += CT) {
-      const int i = p + 1 + e / m, j = p + 1 + e % m;
-      if (j <= i) L[i * DLD + j] -= L[i * DLD + p] * L[j * DLD + p];
+    if (j > p) {
+      const float ljp = L[j * DLD + p];
+#pragma unroll 4
+      for (int i = i0; i < T64; i += CT / T64)
+        if (i >= j) L[i * DLD + j] -= L[i * DLD + p] * ljp;
     }
     __syncthreads();
   }
-  // Vi = L^-1 (lower): thread c < 64 solves L x = e_c by forward substitution
-  if (tid < T64) {
-    const int c = tid;
-    for (int i = 0; i < T64; ++i) {
-      float v = 0.f;
-      if (i >= c) {
-        float acc = (i == c) ? 1.f : 0.f;
-        for (int q = c; q < i; ++q) acc -= L[i * DLD + q] * Vi[q * DLD + c];
-        v = acc / L[i * DLD + i];
-      }
-      Vi[i * DLD + c] = v;
-    }
+  // Vi = L^-1 by right-looking forward elimination on the identity
+  for (int p = 0; p < T64; ++p) {
+    const float rd = 1.f / L[p * DLD + p];
+    if (tid < T64) Vi[p * DLD + tid] *= rd;
+    __syncthreads();
+    const float xp = Vi[p * DLD + j];
+#pragma unroll 4
+    for (int i = i0; i < T64; i += CT / T64)
+      if (i > p) Vi[i * DLD + j] -= L[i * DLD + p] * xp;
+    __syncthreads();
   }
-  __syncthreads();
   float* Lo = a.Linv + ((int64_t)mat * (N / T64) + a.k) * T64 * T64;
   for (int e = tid; e < T64 * T64; e += CT) {
-    const int i = e >> 6, j = e & 63;
-    Mk[(int64_t)i * N + j] = j <= i ? L[i * DLD + j] : 0.f;
-    Lo[e] = Vi[i * DLD + j];
+    const int i = e >> 6, c = e & 63;
+    Mk[(int64_t)i * N + c] = c <= i ? L[i * DLD + c] : 0.f;
+    Lo[e] = c <= i ? Vi[i * DLD + c] : 0.f;
   }
   if (tid == 0 && bad) a.fail[mat] = 1;
 }

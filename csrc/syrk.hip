@@ -524,7 +524,22 @@ splitk_reduce_kernel(const float* __restrict__ ws, int splits, int T,
   const int lr = (bi & 3) * 32 + r, lc = (bj & 3) * 32 + c4;
   const float* src = ws + tidx * splits * (BM * BM) + lr * BM + lc;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int s = 0; s < splits; ++s) {
+  // 8 independent loads in flight per thread (fixed summation order)
+  int s = 0;
+  for (; s + 8 <= splits; s += 8) {
+    float4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      v[u] = *reinterpret_cast<const float4*>(src + (int64_t)(s + u) * (BM * BM));
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      acc.x += v[u].x;
+      acc.y += v[u].y;
+      acc.z += v[u].z;
+      acc.w += v[u].w;
+    }
+  }
+  for (; s < splits; ++s) {
     const float4 v = *reinterpret_cast<const float4*>(src + (int64_t)s * (BM * BM));
     acc.x += v.x;
     acc.y += v.y;
@@ -569,8 +584,10 @@ int64_t syrk_workspace_splits(int64_t N, int64_t D) {
   if (splits > max_by_rows) splits = max_by_rows;
   const int64_t max_by_ws = (int64_t(32) << 20) / (4 * tiles * BM * BM);
   if (splits > max_by_ws) splits = max_by_ws;
+  // the reduction re-reads every slab once: beyond ~64 slabs per tile it
+  // costs more than the extra parallelism gains (PMC: profiles/pmc)
+  if (splits > 64) splits = 64;
   if (splits < 2) splits = 1;
-  if (splits > 4096) splits = 4096;
   return splits;
 }
 
