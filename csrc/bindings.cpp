@@ -66,6 +66,7 @@ void kl_dot_multi(const LayerDesc* descs, int nlayers, int64_t total_blocks,
                   double* acc, hipStream_t s);
 void kl_finalize_dev(const double* acc, int64_t nparts, const float* params,
                      float* scale, hipStream_t s);
+void kl_reduce_partials(const double* acc, int64_t nparts, double* out, hipStream_t s);
 void apply_multi(const LayerDesc* descs, int nlayers, int64_t total_blocks,
                  const float* scale, hipStream_t s);
 // gemm3.hip
@@ -420,8 +421,10 @@ std::tuple<at::Tensor, at::Tensor> upload_table(
 std::tuple<at::Tensor, int64_t, at::Tensor> build_layer_table(
     const std::vector<at::Tensor>& ps, const std::vector<at::Tensor>& ws,
     const std::vector<c10::optional<at::Tensor>>& bs,
-    const c10::optional<at::Tensor>& host_buf) {
+    const c10::optional<at::Tensor>& host_buf,
+    const std::vector<double>& bscales) {
   TORCH_CHECK(ps.size() == ws.size() && ps.size() == bs.size());
+  TORCH_CHECK(bscales.empty() || bscales.size() == ps.size(), "build_layer_table: bscales size");
   std::vector<kfac::LayerDesc> host(ps.size());
   int64_t blocks = 0;
   for (size_t i = 0; i < ps.size(); ++i) {
@@ -447,6 +450,7 @@ std::tuple<at::Tensor, int64_t, at::Tensor> build_layer_table(
       d.b = bs[i]->data_ptr();
       d.bdt = dtype_tag(*bs[i]);
     }
+    d.bscale = bscales.empty() ? 1.f : (float)bscales[i];
     d.rows = rows;
     d.cols = cols;
     d.ldp = p.stride(0);
@@ -482,6 +486,15 @@ void kl_finalize_dev(const at::Tensor& acc, int64_t nparts, const at::Tensor& pa
   c10::hip::HIPGuardMasqueradingAsCUDA g(acc.device());
   kfac::kl_finalize_dev(acc.data_ptr<double>(), nparts, params.data_ptr<float>(),
                         scale.data_ptr<float>(), cur_stream());
+}
+
+// out[0] = fixed-order sum of acc[0:nparts] (one fp64 per-rank KL sum)
+void kl_reduce_partials(const at::Tensor& acc, int64_t nparts, at::Tensor& out) {
+  TORCH_CHECK(acc.scalar_type() == at::kDouble && acc.numel() >= nparts &&
+              out.scalar_type() == at::kDouble && out.numel() >= 1);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(acc.device());
+  kfac::kl_reduce_partials(acc.data_ptr<double>(), nparts, out.data_ptr<double>(),
+                           cur_stream());
 }
 
 void apply_multi(const at::Tensor& table, int64_t nlayers,
@@ -783,9 +796,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("jacobi_eigh", &jacobi_eigh);
   m.def("jacobi_max_n", &kfac::jacobi_max_n);
   m.def("build_layer_table", &build_layer_table, py::arg("ps"), py::arg("ws"),
-        py::arg("bs"), py::arg("host") = py::none());
+        py::arg("bs"), py::arg("host") = py::none(),
+        py::arg("bscales") = std::vector<double>());
   m.def("kl_dot_multi", &kl_dot_multi);
   m.def("kl_finalize_dev", &kl_finalize_dev);
+  m.def("kl_reduce_partials", &kl_reduce_partials);
   m.def("apply_multi", &apply_multi);
   // GIL released: several host threads can each drive rocSOLVER on their
   // own stream (rocSOLVER's syevd blocks its calling thread internally)

@@ -13,6 +13,11 @@ struct LayerDesc {
   int64_t rows, cols, ldp, wcols;
   int64_t block_start;  // first block of this layer
   int32_t wdt, bdt;     // dtype tags
+  // weight of the bias term in the KL sum: 1, or 1/mp for a bias replicated
+  // over the mp ranks of a row-parallel (tensor-parallel) layer, so an
+  // all-reduce of the per-rank sums counts it once
+  float bscale;
+  int32_t pad;
 };
 
 // gemm3.hip: one GEMM of a grouped launch

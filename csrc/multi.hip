@@ -11,6 +11,9 @@
 // the KL-clip scale -- and every gradient it multiplies -- is bitwise
 // reproducible run to run and between graph replay and eager execution.
 //   apply_multi     [Wg_l | bg_l] = scale * P_l
+// Under tensor parallelism kl_reduce_partials folds the partials into one
+// per-rank sum that a single all-reduce over the model-parallel group
+// combines before kl_finalize_dev (nparts = 1).
 // Layers are described by a device-resident descriptor table; each block
 // finds its layer by binary search over the per-layer block prefix sums.
 // kl_clip and lr are read from a small device array so the launches can be
@@ -80,7 +83,7 @@ kl_dot_multi_kernel(const LayerDesc* __restrict__ descs, int nlayers,
       const uint32_t i = ue / uc, j = ue - i * uc;
       const float pv = load_p(d.p, (int64_t)i * d.ldp + j);
       const float g = j < d.wcols ? load_any(d.w, (int64_t)i * d.wcols + j, d.wdt)
-                                  : load_any(d.b, i, d.bdt);
+                                  : load_any(d.b, i, d.bdt) * d.bscale;
       s += (double)pv * (double)g;
     }
   }
@@ -117,6 +120,25 @@ kl_finalize_dev_kernel(const double* __restrict__ acc, int64_t nparts,
       if (sc > 1.0) sc = 1.0;
     }
     scale[0] = (float)sc;
+  }
+}
+
+// out[0] = sum of the nparts partials in a fixed order (the per-rank KL sum
+// that a model-parallel all-reduce combines before kl_finalize_dev)
+__global__ void __launch_bounds__(KL_RED)
+kl_reduce_partials_kernel(const double* __restrict__ acc, int64_t nparts,
+                          double* __restrict__ out) {
+  __shared__ double part[KL_RED / 64];
+  double v = 0.0;
+  for (int64_t i = threadIdx.x; i < nparts; i += KL_RED) v += acc[i];
+  v = wave_reduce_sum(v);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double tot = 0.0;
+#pragma unroll
+    for (int w = 0; w < KL_RED / 64; ++w) tot += part[w];
+    out[0] = tot;
   }
 }
 
@@ -157,6 +179,10 @@ void kl_dot_multi(const LayerDesc* descs, int nlayers, int64_t total_blocks,
 void kl_finalize_dev(const double* acc, int64_t nparts, const float* params,
                      float* scale, hipStream_t s) {
   kl_finalize_dev_kernel<<<1, KL_RED, 0, s>>>(acc, nparts, params, scale);
+}
+
+void kl_reduce_partials(const double* acc, int64_t nparts, double* out, hipStream_t s) {
+  kl_reduce_partials_kernel<<<1, KL_RED, 0, s>>>(acc, nparts, out);
 }
 
 void apply_multi(const LayerDesc* descs, int nlayers, int64_t total_blocks,

@@ -206,6 +206,23 @@ class KFACBaseLayer:
             self._grad_buf = torch.empty(shape, dtype=torch.float32, device=device)
         return self._grad_buf
 
+    def precond_operands(self) -> tuple[torch.Tensor, torch.Tensor | None, bool]:
+        """``(Wg matrix, bias grad or None, stable)`` that preconditioning
+        reads.  ``stable``: the matrix is the parameter gradient itself (not
+        a reshaped copy), so its address is fixed between steps and the
+        grouped GEMM tables keyed on it stay valid.  Tensor-parallel layers
+        return their gathered full-gradient buffers instead."""
+        helper = self.module
+        wg = helper.get_weight_grad()
+        wm = helper.weight_grad_matrix()
+        bg = helper.get_bias_grad() if helper.has_bias() else None
+        stable = wg is not None and wm.is_contiguous() and wm.data_ptr() == wg.data_ptr()
+        return wm, bg, stable
+
+    def precond_out(self, device: torch.device) -> torch.Tensor:
+        """fp32 buffer receiving the preconditioned gradient P."""
+        return self._grad_buffer(device)
+
     def broadcast_grad(
         self,
         src: int,

@@ -296,18 +296,16 @@ class KFACEigenLayer(KFACBaseLayer):
             raise RuntimeError(
                 'Eigendecompositions for both A and G have not been computed',
             )
-        wg = self.module.weight_grad_matrix()
-        bias = self.module.has_bias()
+        wg, bg, _ = self.precond_operands()
         dt = qa.dtype
         g_rows, a_cols = qg.shape[0], qa.shape[0]
         dev = qa.device
         t1 = self._buf('_tmp1', (g_rows, a_cols), dt, dev)
         t2 = self._buf('_tmp2', (g_rows, a_cols), dt, dev)
         # t1 = [Wg | bg] QA  (no concatenation)
-        if bias:
+        if bg is not None:
             torch.mm(wg.to(dt), qa[:-1], out=t1)
-            bg = self.module.get_bias_grad().reshape(-1).to(dt)
-            t1.addr_(bg, qa[-1])
+            t1.addr_(bg.reshape(-1).to(dt), qa[-1])
         else:
             torch.mm(wg.to(dt), qa, out=t1)
         torch.mm(qg.t(), t1, out=t2)  # V1
@@ -317,7 +315,7 @@ class KFACEigenLayer(KFACBaseLayer):
             pops.eigen_scale_(t2, dg=self.dg, da=self.da, damping=damping)
         torch.mm(qg, t2, out=t1)
         if dt == torch.float32:
-            out = self._grad_buffer(dev)
+            out = self.precond_out(dev)
             torch.mm(t1, qa.t(), out=out)
         else:
             out = (t1 @ qa.t()).to(torch.float32)

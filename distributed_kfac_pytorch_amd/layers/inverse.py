@@ -146,21 +146,21 @@ class KFACInverseLayer(KFACBaseLayer):
                 'inverted',
             )
         dt = a_inv.dtype
-        wg = self.module.weight_grad_matrix().to(dt)
+        wg, bg, _ = self.precond_operands()
+        wg = wg.to(dt)
         dev = a_inv.device
         shape = (g_inv.shape[0], a_inv.shape[0])
         if self._tmp1 is None or tuple(self._tmp1.shape) != shape or self._tmp1.dtype != dt:
             self._tmp1 = torch.empty(shape, dtype=dt, device=dev)
         t1 = self._tmp1
         # t1 = [Wg | bg] A_inv  without concatenation
-        if self.module.has_bias():
+        if bg is not None:
             torch.mm(wg, a_inv[:-1], out=t1)
-            bg = self.module.get_bias_grad().reshape(-1).to(dt)
-            t1.addr_(bg, a_inv[-1])
+            t1.addr_(bg.reshape(-1).to(dt), a_inv[-1])
         else:
             torch.mm(wg, a_inv, out=t1)
         if dt == torch.float32:
-            out = self._grad_buffer(dev)
+            out = self.precond_out(dev)
             torch.mm(g_inv, t1, out=out)
         else:
             out = (g_inv @ t1).to(torch.float32)

@@ -4,11 +4,14 @@ Row-parallel ("input") layers gather their sharded input to the primary
 rank of the model-parallel (MP) group, which owns the full A factor and
 all-reduces it over its data-parallel (DP) group; G is replicated across MP
 ranks and all-reduced over the pipeline-stage peers.  Column-parallel
-("output") layers mirror this for G.  Preconditioning gathers the weight
-(and sharded bias) gradient to the primary, preconditions the full matrix
-and scatters the shards back -- with a true ``dist.gather`` /
-``dist.scatter`` (see ``neox/mpu.py``) rather than the reference's
-all-gather / zero-padded reduce-scatter emulation.
+("output") layers mirror this for G.  Preconditioning (reference
+``kfac/gpt_neox/layer.py:203-310``) gathers the weight (and sharded bias)
+gradient to the primary, preconditions the full matrix and scatters the
+shards back -- with a true ``dist.gather`` into persistent buffers and ONE
+``dist.scatter`` of [weight shard | bias] per layer (see ``neox/mpu.py``)
+rather than the reference's all-gather / zero-padded reduce-scatter
+emulation.  The preconditioner runs the three phases over all layers, so
+the primary's GEMMs are one grouped MFMA launch (``ops/precondition.py``).
 """
 from __future__ import annotations
 
@@ -21,7 +24,6 @@ import torch.distributed as dist
 from distributed_kfac_pytorch_amd.layers.eigen import KFACEigenLayer
 from distributed_kfac_pytorch_amd.neox.mpu import gather_from_model_parallel_region
 from distributed_kfac_pytorch_amd.neox.mpu import scatter_to_model_parallel_region
-from distributed_kfac_pytorch_amd.neox.mpu import split_tensor_along_dim
 from distributed_kfac_pytorch_amd.parallel.comm import get_rank
 from distributed_kfac_pytorch_amd.parallel.comm import get_world_size
 
@@ -48,6 +50,13 @@ class GPTNeoXKFACEigenLayer(KFACEigenLayer):
         self.model_parallel_group = model_parallel_group
         self.pipe_parallel_peer_group = pipe_parallel_peer_group
         super().__init__(module, **kwargs)
+        # persistent MP buffers (primary only): gathered full Wg / bias grad,
+        # full P, row-parallel gather staging and scatter packing
+        self._full_w: torch.Tensor | None = None
+        self._full_b: torch.Tensor | None = None
+        self._full_p: torch.Tensor | None = None
+        self._gather_w: torch.Tensor | None = None
+        self._scatter_p: torch.Tensor | None = None
 
     # --------------------------------------------------------------- checks
     def _check(self) -> None:
@@ -123,12 +132,114 @@ class GPTNeoXKFACEigenLayer(KFACEigenLayer):
             self._save_and_update_g(g, alpha)
 
     # ------------------------------------------------------------- gradients
+    # The stock eigen math (``KFACEigenLayer.preconditioned_grad``, or the
+    # grouped MFMA GEMM of ``ops.precondition.GroupedPrecondition``) runs on
+    # the primary over the gathered FULL gradient: ``precond_operands`` /
+    # ``precond_out`` point it at persistent full-size buffers.
+    stock_precondition_math = True
+
+    def _mp_world(self) -> int:
+        return get_world_size(self.model_parallel_group)
+
+    @property
+    def kl_bias_scale(self) -> float:
+        """A row-parallel bias gradient is replicated on every MP rank: each
+        counts 1/mp of it so the MP all-reduce of the KL sum counts it once."""
+        if self.parallelism == 'input' and self.module.has_bias():
+            return 1.0 / max(1, self._mp_world())
+        return 1.0
+
     def grad_shape(self) -> tuple[int, int]:
         w = self.module.module.weight
         return (w.shape[0], w.shape[1] + int(self.module.has_bias()))
 
+    def _full_shape(self) -> tuple[int, int]:
+        return (self.module.g_factor_shape[0], self.module.a_factor_shape[0])
+
+    def precond_operands(self) -> tuple[torch.Tensor, torch.Tensor | None, bool]:
+        if self._mp_world() == 1:
+            return super().precond_operands()
+        if self._full_w is None:
+            raise RuntimeError('gather_full_grad() must run before preconditioning')
+        return self._full_w, self._full_b, True
+
+    def precond_out(self, device: torch.device) -> torch.Tensor:
+        if self._mp_world() == 1:
+            return self._grad_buffer(device)
+        return self._buf('_full_p', self._full_shape(), torch.float32, device)
+
+    def gather_full_grad(self) -> None:
+        """Collective over the MP group: assemble the full weight (and bias)
+        gradient in persistent buffers on the primary.  Column-parallel
+        shards are row blocks, gathered straight into the full matrix;
+        row-parallel shards are column blocks, gathered into a staging
+        buffer and interleaved with one copy (the replicated bias is local)."""
+        self._check()
+        world = self._mp_world()
+        if world == 1:
+            return
+        mp = self.model_parallel_group
+        primary = self._is_primary()
+        w_part = self.module.get_weight_grad().contiguous()
+        has_bias = self.module.has_bias()
+        b_part = self.module.get_bias_grad().contiguous() if has_bias else None
+        dev, dt = w_part.device, w_part.dtype
+        rows, cols = w_part.shape
+        if self.parallelism == 'output':
+            full_w = self._buf('_full_w', (rows * world, cols), dt, dev) if primary else None
+            dist.gather(w_part, gather_list=list(full_w.view(world, rows, cols).unbind(0))
+                        if primary else None, dst=self.primary_rank, group=mp)
+            full_b = None
+            if has_bias:
+                assert b_part is not None
+                full_b = self._buf('_full_b', (rows * world,), b_part.dtype, dev) if primary else None
+                dist.gather(b_part, gather_list=list(full_b.view(world, rows).unbind(0))
+                            if primary else None, dst=self.primary_rank, group=mp)
+        else:
+            stage = self._buf('_gather_w', (world, rows, cols), dt, dev) if primary else None
+            dist.gather(w_part, gather_list=list(stage.unbind(0)) if primary else None,
+                        dst=self.primary_rank, group=mp)
+            full_w = full_b = None
+            if primary:
+                full_w = self._buf('_full_w', (rows, cols * world), dt, dev)
+                full_w.view(rows, world, cols).copy_(stage.permute(1, 0, 2))
+                full_b = b_part
+        if primary:
+            self._full_w, self._full_b = full_w, full_b
+
+    def scatter_grad(self) -> None:
+        """Collective over the MP group: every rank receives its shard of the
+        primary's full P -- weight columns and bias together -- in ONE
+        scatter, straight into its persistent local grad buffer (the layout
+        ``update_grad`` / the multi-tensor apply read)."""
+        world = self._mp_world()
+        if world == 1:
+            return
+        mp = self.model_parallel_group
+        primary = self._is_primary()
+        local = self._grad_buffer(self.module.device)
+        chunks = None
+        if primary:
+            p = self.grad
+            assert p is not None
+            if self.parallelism == 'output':
+                # row blocks of P are contiguous: scatter views, no copies
+                chunks = list(p.view(world, local.shape[0], local.shape[1]).unbind(0))
+            else:
+                rows, lcols = local.shape
+                c = lcols - int(self.module.has_bias())
+                pack = self._buf('_scatter_p', (world, rows, lcols), torch.float32, p.device)
+                pack[:, :, :c].copy_(p[:, :c * world].view(rows, world, c).permute(1, 0, 2))
+                if self.module.has_bias():
+                    pack[:, :, c].copy_(p[:, c * world].expand(world, rows))
+                chunks = list(pack.unbind(0))
+        scatter_to_model_parallel_region(chunks, local, self.primary_rank, mp)
+        self.grad = local
+
     def preconditioned_grad(self, damping: float = 0.001) -> None:
-        """Every MP rank enters: gather -> precondition on primary -> scatter."""
+        """Every MP rank enters: gather -> precondition on the primary ->
+        scatter (the preconditioner batches these phases over all layers so
+        the primary's GEMMs run as one grouped launch)."""
         self._check()
         primary = self._is_primary()
         if primary and (
@@ -140,53 +251,7 @@ class GPTNeoXKFACEigenLayer(KFACEigenLayer):
             raise RuntimeError(
                 'Eigendecompositions for both A and G have not been computed',
             )
-        mp = self.model_parallel_group
-        world = get_world_size(mp)
-        wdim = -1 if self.parallelism == 'input' else 0
-        w_part = self.module.get_weight_grad()
-        full_w = gather_from_model_parallel_region(w_part, self.primary_rank, mp, dim=wdim)
-        has_bias = self.module.has_bias()
-        b_part = self.module.get_bias_grad() if has_bias else None
-        full_b = None
-        if has_bias:
-            assert b_part is not None
-            if self.parallelism == 'output':
-                full_b = gather_from_model_parallel_region(b_part, self.primary_rank, mp, dim=0)
-            else:
-                full_b = b_part
-        w_chunks = b_chunks = None
-        b_new = None
+        self.gather_full_grad()
         if primary:
-            assert full_w is not None and self.qa is not None and self.qg is not None
-            g = full_w.to(self.qa.dtype)
-            if has_bias:
-                assert full_b is not None
-                g = torch.cat([g, full_b.reshape(-1, 1).to(g.dtype)], dim=1)
-            v = self.qg.t() @ g @ self.qa
-            if self.prediv_eigenvalues:
-                v = v * self.dgda
-            else:
-                v = v / (torch.outer(self.dg, self.da) + damping)
-            p = (self.qg @ v @ self.qa.t()).to(torch.float32)
-            w_new = p[:, :-1] if has_bias else p
-            w_chunks = list(split_tensor_along_dim(w_new, world, dim=wdim, contiguous_split_chunks=True))
-            if has_bias:
-                b_new = p[:, -1].contiguous()
-                if self.parallelism == 'output':
-                    b_chunks = list(split_tensor_along_dim(b_new, world, dim=0, contiguous_split_chunks=True))
-        w_out = torch.empty(w_part.shape, dtype=torch.float32, device=w_part.device)
-        scatter_to_model_parallel_region(w_chunks, w_out, self.primary_rank, mp)
-        if has_bias:
-            assert b_part is not None
-            b_out = torch.empty(b_part.shape, dtype=torch.float32, device=b_part.device)
-            if self.parallelism == 'output':
-                scatter_to_model_parallel_region(b_chunks, b_out, self.primary_rank, mp)
-            else:
-                if primary:
-                    assert b_new is not None
-                    b_out.copy_(b_new)
-                if world > 1:
-                    dist.broadcast(b_out, src=self.primary_rank, group=mp)
-            self.grad = torch.cat([w_out, b_out.reshape(-1, 1)], dim=1)
-        else:
-            self.grad = w_out
+            KFACEigenLayer.preconditioned_grad(self, damping)
+        self.scatter_grad()

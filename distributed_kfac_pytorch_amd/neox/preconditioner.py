@@ -30,6 +30,7 @@ from distributed_kfac_pytorch_amd.enums import AllreduceMethod
 from distributed_kfac_pytorch_amd.enums import AssignmentStrategy
 from distributed_kfac_pytorch_amd.enums import ComputeMethod
 from distributed_kfac_pytorch_amd.layers.base import KFACBaseLayer
+from distributed_kfac_pytorch_amd.layers.eigen import KFACEigenLayer
 from distributed_kfac_pytorch_amd.layers.register import any_match
 from distributed_kfac_pytorch_amd.layers.register import get_flattened_modules
 from distributed_kfac_pytorch_amd.layers.register import requires_grad
@@ -37,6 +38,7 @@ from distributed_kfac_pytorch_amd.neox.assignment import GPTNeoXAssignment
 from distributed_kfac_pytorch_amd.neox.layer import GPTNeoXKFACEigenLayer
 from distributed_kfac_pytorch_amd.neox.modules import GPTNeoXLinearModuleHelper
 from distributed_kfac_pytorch_amd.neox.topology import ProcessTopology
+from distributed_kfac_pytorch_amd.ops import precondition as pops
 from distributed_kfac_pytorch_amd.parallel.comm import get_rank
 from distributed_kfac_pytorch_amd.parallel.comm import TorchDistributedCommunicator
 from distributed_kfac_pytorch_amd.warnings import ExperimentalFeatureWarning
@@ -183,21 +185,95 @@ class GPTNeoXKFACPreconditioner(BaseKFACPreconditioner):
             loglevel=loglevel,
         )
 
+    # ------------------------------------------------------- precondition
+    def _precondition_all(self, ordered: list) -> None:
+        """Three phases over ALL layers instead of gather / GEMMs / scatter
+        per layer: (1) every layer's gradient is gathered to its primary,
+        (2) each rank preconditions the layers it is primary for -- one
+        grouped MFMA launch set on the GPU (``GroupedPrecondition``), the
+        stock per-layer math otherwise, (3) one scatter per layer returns the
+        shards.  Collectives are issued in the same layer order on every MP
+        rank.  Data-parallel replicas then receive from their grad worker
+        (bucketed broadcasts, as the base preconditioner)."""
+        damping = self.damping
+        workers = [layer for name, layer in ordered if self._assignment.is_grad_worker(name)]
+        for layer in workers:
+            layer.gather_full_grad()
+        mine = [layer for layer in workers if layer._is_primary()]
+        for layer in mine:
+            if layer.qa is None or layer.qg is None:
+                raise RuntimeError('Eigendecompositions for both A and G have not been computed')
+        grouped = False
+        if mine and mine[0].module.device.type == 'cuda':
+            if self._grouped is None:
+                self._grouped = pops.GroupedPrecondition()
+            grouped = self._grouped.run(mine, damping)
+        if not grouped:
+            for layer in mine:
+                KFACEigenLayer.preconditioned_grad(layer, damping)
+        for layer in workers:
+            layer.scatter_grad()
+        for name, layer in ordered:
+            layer.broadcast_grad(
+                src=self._assignment.src_grad_worker(name),
+                group=self._assignment.grad_receiver_group(name),
+                bucketed=True,
+            )
+        self._tdc.flush_broadcast_buckets()
+        self._tdc.flush_allreduce_buckets()
+
     # ------------------------------------------------------------ KL clip
+    def _kl_reduce(self, vg: torch.Tensor) -> None:
+        """Sum the per-rank KL partial over the model-parallel (and, if
+        given, pipeline) group, in place."""
+        from distributed_kfac_pytorch_amd.parallel.comm import get_world_size
+
+        if not dist.is_initialized():
+            return
+        if get_world_size(self.model_parallel_group) > 1:
+            dist.all_reduce(vg, group=self.model_parallel_group)
+        if self.pipeline_parallel_group is not None and get_world_size(
+            self.pipeline_parallel_group,
+        ) > 1:
+            dist.all_reduce(vg, group=self.pipeline_parallel_group)
+
+    def _kl_needs_reduce(self) -> bool:
+        from distributed_kfac_pytorch_amd.parallel.comm import get_world_size
+
+        return dist.is_initialized() and (
+            get_world_size(self.model_parallel_group) > 1
+            or (self.pipeline_parallel_group is not None
+                and get_world_size(self.pipeline_parallel_group) > 1)
+        )
+
     def _apply_gradients(self, ordered: list, kl: float | None) -> None:
         """KL clip over the WHOLE model: each rank sums <P, grad> over its
-        shards (a replicated row-parallel bias counted once per MP group),
-        the partial sums are all-reduced over the model-parallel group (and
-        the pipeline group, if given), and every shard is scaled by the same
-        factor.  The reference sums only rank-local shards, so its MP ranks
-        clip with different scales."""
-        if kl is None or not ordered:
-            for _, layer in ordered:
+        shards (a replicated row-parallel bias weighted 1/mp), the partial
+        sums are all-reduced over the model-parallel group (and the pipeline
+        group, if given), and every shard is scaled by the same factor.  The
+        reference (``kfac/gpt_neox/preconditioner.py``) sums only rank-local
+        shards, so its MP ranks clip with different scales.
+
+        GPU: the native multi-tensor path (``MultiLayerApply``): one
+        KL-partials launch, a fixed-order fold to one fp64 scalar, ONE
+        all-reduce of that scalar, the finalise and one apply launch for the
+        whole model.  CPU / fallback: per-layer fp64 torch reductions."""
+        if not ordered:
+            return
+        layers = [layer for _, layer in ordered]
+        if self._multi_apply is None:
+            self._multi_apply = pops.MultiLayerApply()
+        reduce_fn = self._kl_reduce if kl is not None and self._kl_needs_reduce() else None
+        if self._multi_apply.run(layers, kl, float(self.lr) if kl is not None else 0.0,
+                                 reduce_fn=reduce_fn):
+            return
+        if kl is None:
+            for layer in layers:
                 layer.update_grad(scale=None)
             return
-        dev = ordered[0][1].module.device
+        dev = layers[0].module.device
         vg = torch.zeros(1, dtype=torch.float64, device=dev)
-        for _, layer in ordered:
+        for layer in layers:
             p = layer.grad
             if p is None:
                 raise AssertionError('layer gradient has not been preconditioned')
@@ -206,21 +282,9 @@ class GPTNeoXKFACPreconditioner(BaseKFACPreconditioner):
             ncol = wm.shape[1]
             vg += (p[:, :ncol].double() * wm.double()).sum()
             if m.has_bias():
-                share = 1.0
-                if layer.parallelism == 'input':
-                    share = 1.0 / max(1, m.model_parallel_world_size)
-                vg += (p[:, ncol].double() * m.get_bias_grad().double()).sum() * share
-        if dist.is_initialized():
-            if self.model_parallel_group is not None or dist.get_world_size() > 1:
-                from distributed_kfac_pytorch_amd.parallel.comm import get_world_size
-
-                if get_world_size(self.model_parallel_group) > 1:
-                    dist.all_reduce(vg, group=self.model_parallel_group)
-                if (
-                    self.pipeline_parallel_group is not None
-                    and get_world_size(self.pipeline_parallel_group) > 1
-                ):
-                    dist.all_reduce(vg, group=self.pipeline_parallel_group)
+                vg += (p[:, ncol].double() * m.get_bias_grad().double()).sum() * layer.kl_bias_scale
+        if self._kl_needs_reduce():
+            self._kl_reduce(vg)
         lr = float(self.lr)
         vg = (vg * lr * lr).abs()
         scale = torch.where(
@@ -228,7 +292,7 @@ class GPTNeoXKFACPreconditioner(BaseKFACPreconditioner):
             torch.ones_like(vg),
             torch.clamp(torch.sqrt(float(kl) / vg), max=1.0),
         ).float()
-        for _, layer in ordered:
+        for layer in layers:
             layer.update_grad(scale=scale)
 
     # ------------------------------------------------------------ checkpoint
@@ -240,7 +304,10 @@ class GPTNeoXKFACPreconditioner(BaseKFACPreconditioner):
         if not include_factors:
             return sd
         if self.factor_checkpoint_dir is not None:
+            # factors live in the per-layer files: the dict stays small
+            # (reference ``kfac/gpt_neox/preconditioner.py:350-363``)
             self.save_factors_to_dir()
+            return sd
         me = get_rank()
         layers: dict[str, dict[str, torch.Tensor]] = {}
         for name, layer in self._layers.values():
@@ -269,7 +336,10 @@ class GPTNeoXKFACPreconditioner(BaseKFACPreconditioner):
         layers = state_dict.pop('layers', None)
         super().load_state_dict(state_dict, compute_inverses=False)
         if self.factor_checkpoint_dir is not None:
+            # the per-layer files are the source of truth (reference
+            # ``kfac/gpt_neox/preconditioner.py:314-328``)
             self.load_factors_from_dir(compute_inverses)
+            return
         if layers is None:
             return
         me = get_rank()
@@ -296,6 +366,8 @@ class GPTNeoXKFACPreconditioner(BaseKFACPreconditioner):
                 path = os.path.join(self.factor_checkpoint_dir, name)
                 logger.info(f'saving KFAC factors for {name} to {path}')
                 torch.save(layer.state_dict(), path)
+        if dist.is_initialized():
+            dist.barrier()  # every file is complete when any rank returns
 
     def load_factors_from_dir(self, compute_inverses: bool = True) -> None:
         """Load per-layer factor files on the primary ranks (missing files

@@ -21,6 +21,7 @@ from __future__ import annotations
 import math
 import os
 from typing import Any
+from typing import Callable
 
 import torch
 
@@ -264,6 +265,7 @@ class MultiLayerApply:
         self._scale: torch.Tensor | None = None
         self._params: torch.Tensor | None = None
         self._param_vals: tuple[float, float] | None = None
+        self._sum: torch.Tensor | None = None
         self._n = 0
 
     def _buffers(self, device: torch.device, nparts: int) -> None:
@@ -293,7 +295,7 @@ class MultiLayerApply:
         lib = native()
         if lib is None or not layers:
             return False
-        ps, ws, bs = [], [], []
+        ps, ws, bs, bsc = [], [], [], []
         key = []
         for layer in layers:
             p = layer._grad_buf if use_buffers else layer.grad
@@ -316,10 +318,13 @@ class MultiLayerApply:
             ps.append(p)
             ws.append(wm)
             bs.append(bg)
+            # weight of the bias in the KL sum (1/mp for a bias replicated
+            # over a tensor-parallel group, see neox/layer.py)
+            bsc.append(float(getattr(layer, 'kl_bias_scale', 1.0)))
             key.append((
                 p.data_ptr(), tuple(p.shape), p.stride(0), wm.data_ptr(),
                 tuple(wm.shape), wm.dtype, None if bg is None else bg.data_ptr(),
-                None if bg is None else bg.dtype,
+                None if bg is None else bg.dtype, bsc[-1],
             ))
         key_t = tuple(key)
         if key_t != self._key:
@@ -327,7 +332,7 @@ class MultiLayerApply:
             if entry is None:
                 slots = self._tables.reserve()
                 entry = self._tables.put(
-                    key_t, lib.build_layer_table(ps, ws, bs, slots[0]), slots)
+                    key_t, lib.build_layer_table(ps, ws, bs, slots[0], bsc), slots)
             self._table, self._blocks, _ = entry
             self._key = key_t
         self._n = len(ps)
@@ -349,21 +354,40 @@ class MultiLayerApply:
     def release(self, key: tuple | None) -> None:
         self._tables.unpin(key)
 
-    def launch(self, with_kl: bool) -> None:
-        """The three (or one, without KL clip) multi-tensor launches."""
+    def launch(self, with_kl: bool, reduce_fn: Callable[[torch.Tensor], None] | None = None) -> None:
+        """The three (or one, without KL clip) multi-tensor launches.
+
+        ``reduce_fn`` (tensor parallelism): the per-block partials are first
+        folded into one fp64 per-rank sum, ``reduce_fn`` all-reduces that
+        1-element tensor in place over the model-parallel group, and the
+        scale is finalised from the global sum -- one scalar collective for
+        the whole model."""
         lib = native()
         if not with_kl:
             lib.apply_multi(self._table, self._n, self._blocks, None)
             return
         lib.kl_dot_multi(self._table, self._n, self._blocks, self._acc)
-        lib.kl_finalize_dev(self._acc, self._blocks, self._params, self._scale)
+        if reduce_fn is None:
+            lib.kl_finalize_dev(self._acc, self._blocks, self._params, self._scale)
+        else:
+            if self._sum is None or self._sum.device != self._acc.device:
+                self._sum = torch.zeros(1, dtype=torch.float64, device=self._acc.device)
+            lib.kl_reduce_partials(self._acc, self._blocks, self._sum)
+            reduce_fn(self._sum)
+            lib.kl_finalize_dev(self._sum, 1, self._params, self._scale)
         lib.apply_multi(self._table, self._n, self._blocks, self._scale)
 
-    def run(self, layers: list, kl_clip: float | None, lr: float) -> bool:
+    def run(
+        self,
+        layers: list,
+        kl_clip: float | None,
+        lr: float,
+        reduce_fn: Callable[[torch.Tensor], None] | None = None,
+    ) -> bool:
         """prepare + launch for an eagerly preconditioned step."""
         if not self.prepare(layers, kl_clip, lr):
             return False
-        self.launch(kl_clip is not None)
+        self.launch(kl_clip is not None, reduce_fn)
         for layer in layers:
             layer.grad = None
         return True
@@ -407,19 +431,16 @@ class GroupedPrecondition:
         from distributed_kfac_pytorch_amd.layers.inverse import KFACInverseLayer
 
         # only the stock layer math: subclasses that override the
-        # preconditioning (embedding, tensor-parallel NeoX) keep their path
+        # preconditioning (embedding) keep their path; tensor-parallel NeoX
+        # layers run the stock math on their gathered operands
+        # (``stock_precondition_math``)
         if type(layer).preconditioned_grad not in (
             KFACEigenLayer.preconditioned_grad, KFACInverseLayer.preconditioned_grad,
-        ):
+        ) and not getattr(layer, 'stock_precondition_math', False):
             return None
-        helper = layer.module
-        wg = helper.get_weight_grad()
-        if wg is None or not wg.is_cuda or wg.dtype != torch.float32:
+        wm, bg, stable = layer.precond_operands()
+        if wm is None or not stable or not wm.is_cuda or wm.dtype != torch.float32:
             return None
-        wm = helper.weight_grad_matrix()
-        if not (wm.is_contiguous() and wm.data_ptr() == wg.data_ptr()):
-            return None
-        bg = helper.get_bias_grad() if helper.has_bias() else None
         if bg is not None and (bg.dtype != torch.float32 or not bg.is_contiguous()):
             return None
         if isinstance(layer, KFACEigenLayer):
@@ -473,6 +494,7 @@ class GroupedPrecondition:
             ops.append(o)
         t = [[] for _ in range(4)]  # per table: list of operand tuples
         key = [damping]
+        outs: list[torch.Tensor] = []
         for layer, (kind, wm, bg, fa, fg) in zip(layers, ops):
             g, a = fg.shape[0], fa.shape[0]
             dev = fa.device
@@ -480,9 +502,10 @@ class GroupedPrecondition:
             qa_hl, qg_hl = hl if hl is not None else (None, None)
             t1 = layer._buf('_tmp1', (g, a), torch.float32, dev) if kind == 'eigen' \
                 else self._inv_tmp(layer, (g, a), dev)
-            out = layer._grad_buffer(dev)
+            out = layer.precond_out(dev)
             if tuple(out.shape) != (g, a):
                 return False
+            outs.append(out)
             key.append((kind, wm.data_ptr(), None if bg is None else bg.data_ptr(),
                         fa.data_ptr(), fg.data_ptr(), t1.data_ptr(), out.data_ptr(), g, a,
                         None if qa_hl is None else (qa_hl.data_ptr(), qg_hl.data_ptr())))
@@ -526,6 +549,7 @@ class GroupedPrecondition:
             self._tables = tables
             self._key = key_t
         self._layers = layers
+        self._outs = outs
         return True
 
     @staticmethod
@@ -557,6 +581,6 @@ class GroupedPrecondition:
         if not self.prepare(layers, damping):
             return False
         self.launch()
-        for layer in layers:
-            layer.grad = layer._grad_buf
+        for layer, out in zip(layers, self._outs):
+            layer.grad = out
         return True

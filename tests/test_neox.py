@@ -231,24 +231,44 @@ def _tp2_matches_single(tokens, ref, tmpdir):
         with torch.no_grad():
             for p in model.parameters():
                 p -= 0.1 * p.grad
-    # checkpoint: gathered factors on every rank + per-layer files
+    # checkpoint with factor_checkpoint_dir: per-layer files, no 'layers'
+    # entry (reference kfac/gpt_neox/preconditioner.py:350-363)
     sd = pre.state_dict()
-    assert len(sd['layers']) == 8
-    for v in sd['layers'].values():
-        assert v['A'].device.type == 'cpu' and v['A'].shape[0] == v['A'].shape[1]
+    assert 'layers' not in sd
     files = sorted(os.listdir(tmpdir))
     assert len(files) == 8
-    model2, _, _, _ = model, topo, mp_group, dp_group
+    # without it: factors gathered to every rank as CPU tensors
+    pre.factor_checkpoint_dir = None
+    sd_mem = pre.state_dict()
+    pre.factor_checkpoint_dir = tmpdir
+    assert len(sd_mem['layers']) == 8
+    for v in sd_mem['layers'].values():
+        assert v['A'].device.type == 'cpu' and v['A'].shape[0] == v['A'].shape[1]
     pre2 = GPTNeoXKFACPreconditioner(
-        model2, model_parallel_group=mp_group, data_parallel_group=dp_group,
+        model, model_parallel_group=mp_group, data_parallel_group=dp_group,
         factor_checkpoint_dir=tmpdir,
     )
     dist.barrier()
     if rank == 0:
         os.remove(os.path.join(tmpdir, files[0]))
     dist.barrier()
-    pre2.load_state_dict(sd, compute_inverses=True)
+    # the files are the source of truth: an in-memory 'layers' entry is
+    # ignored (a missing file is skipped)
+    pre2.load_state_dict(sd_mem, compute_inverses=True)
     assert pre2.steps == len(ref)
+    for name, layer in pre2._layers.values():
+        if pre2._assignment.factor_worker(name, 'A') == rank:
+            if name == files[0]:
+                assert layer.a_factor is None
+            else:
+                assert torch.allclose(layer.a_factor.cpu(), sd_mem['layers'][name]['A'])
+    pre3 = GPTNeoXKFACPreconditioner(
+        model, model_parallel_group=mp_group, data_parallel_group=dp_group,
+    )
+    pre3.load_state_dict(sd_mem, compute_inverses=True)
+    for name, layer in pre3._layers.values():
+        if pre3._assignment.factor_worker(name, 'A') == rank:
+            assert torch.allclose(layer.g_factor.cpu(), sd_mem['layers'][name]['G'])
 
 
 def test_tp2_preconditioned_grads_match_single_rank(tmp_path):
