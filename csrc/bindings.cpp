@@ -172,6 +172,21 @@ at::Tensor syrk_ws(const at::Tensor& C, int64_t D, int64_t splits) {
 }
 
 // C[D,D] = beta*C + alpha * Xt^T Xt, Xt = [X | 1] when bias.
+// C: dense [D, D] (unit column stride), or the packed upper triangle
+// [D (D + 1) / 2] (the factor all-reduce wire): returns the ldc to pass to
+// kfac::syrk (0 = packed)
+int64_t syrk_out_ld(const at::Tensor& C, int64_t D) {
+  TORCH_CHECK(C.scalar_type() == at::kFloat, "syrk output must be fp32");
+  if (C.dim() == 1) {
+    TORCH_CHECK(C.numel() == D * (D + 1) / 2 && C.is_contiguous(),
+                "packed syrk output must hold D(D+1)/2 contiguous floats");
+    return 0;
+  }
+  TORCH_CHECK(C.dim() == 2 && C.size(0) == D && C.size(1) == D && C.stride(1) == 1,
+              "syrk output must be [D, D] with unit column stride");
+  return C.stride(0);
+}
+
 void syrk(const at::Tensor& x, at::Tensor& C, bool bias, double alpha,
           double beta, int64_t splits) {
   check_cuda(x, "x");
@@ -181,17 +196,15 @@ void syrk(const at::Tensor& x, at::Tensor& C, bool bias, double alpha,
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 ||
                   x.scalar_type() == at::kFloat,
               "syrk input must be bf16 or fp32");
-  TORCH_CHECK(C.scalar_type() == at::kFloat, "syrk output must be fp32");
-  TORCH_CHECK(C.dim() == 2 && C.size(0) == C.size(1) && C.stride(1) == 1);
   const int64_t N = x.size(0), K = x.size(1);
   const int64_t D = K + (bias ? 1 : 0);
-  TORCH_CHECK(C.size(0) == D, "C must be [K+bias, K+bias]");
+  const int64_t ldc = syrk_out_ld(C, D);
   const int64_t ldx = N > 1 ? x.stride(0) : K;
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   int sp = splits > 0 ? (int)splits : (int)kfac::syrk_workspace_splits(N, D);
   at::Tensor ws = syrk_ws(C, D, sp);
   kfac::syrk(dtype_tag(x), x.data_ptr(), N, K, ldx, bias,
-             C.data_ptr<float>(), D, C.stride(0), (float)alpha, (float)beta,
+             C.data_ptr<float>(), D, ldc, (float)alpha, (float)beta,
              sp, cur_stream(), nullptr, ws.defined() ? ws.data_ptr<float>() : nullptr);
 }
 
@@ -214,13 +227,11 @@ void syrk_conv(const at::Tensor& x, at::Tensor& C, int64_t kh, int64_t kw,
                   x.stride(3) % vec == 0 &&
                   (reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0,
               "syrk_conv: channel count and strides must allow 16-byte loads");
-  TORCH_CHECK(C.scalar_type() == at::kFloat && C.dim() == 2 && C.size(0) == C.size(1) &&
-              C.stride(1) == 1, "syrk_conv output must be fp32 square, unit column stride");
   const int64_t OH = (H + 2 * ph - kh) / sh + 1, OW = (W + 2 * pw - kw) / sw + 1;
   TORCH_CHECK(OH > 0 && OW > 0, "syrk_conv: empty output");
   const int64_t K = Cin * kh * kw;
   const int64_t D = K + (bias ? 1 : 0);
-  TORCH_CHECK(C.size(0) == D, "C must be [C*kh*kw + bias]^2");
+  const int64_t ldc = syrk_out_ld(C, D);
   const int64_t N = B * OH * OW;
   TORCH_CHECK(H < (1 << 30) && W < (1 << 30) && OH * OW < (1LL << 31));
   kfac::ConvGeom g{x.stride(0), x.stride(2), x.stride(3), (int32_t)H, (int32_t)W,
@@ -230,7 +241,7 @@ void syrk_conv(const at::Tensor& x, at::Tensor& C, int64_t kh, int64_t kw,
   int sp = splits > 0 ? (int)splits : (int)kfac::syrk_workspace_splits(N, D);
   at::Tensor ws = syrk_ws(C, D, sp);
   kfac::syrk(dtype_tag(x), x.data_ptr(), N, K, /*ldx=*/K, bias, C.data_ptr<float>(), D,
-             C.stride(0), (float)alpha, (float)beta, sp, cur_stream(), &g,
+             ldc, (float)alpha, (float)beta, sp, cur_stream(), &g,
              ws.defined() ? ws.data_ptr<float>() : nullptr);
 }
 

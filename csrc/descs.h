@@ -42,6 +42,39 @@ struct GemmDesc {
   const uint16_t* Bh;
 };
 
+// gemm3s.hip: one GEMM of a grouped launch on split images.  A split image
+// holds a logical matrix as two bf16 planes (hi at the base, lo `plane`
+// elements later), each [R][ld] with R and ld multiples of 256 and the
+// padding zero, so no load of a 128 x 32 tile ever needs a bounds check.
+//   C[M][N] = A[M][K] B[K][N] (K a multiple of 32 or zero-padded to it);
+//   A image [M][K] (k-contig) or [K][M] (m-contig); B [N][K] or [K][N].
+struct Gemm3sDesc {
+  const uint16_t* A;
+  const uint16_t* B;
+  void* C;              // fp32 [M][ldc], or a split image (hi, lo at +c_plane)
+  const float* S;       // optional scale matrix [M][lds]
+  const float* dg;      // optional: C = acc / (dg[m] * da[n] + damping)
+  const float* da;
+  int64_t a_plane, b_plane, c_plane;
+  int64_t lda, ldb, ldc, lds;
+  int32_t M, N, K;
+  int32_t tiles_n, tile_start;
+  float damping;
+};
+
+// gemm3s.hip: fp32 [rows][cols] (+ one extra column read from a vector)
+// -> split image planes at dst (row stride ldd, lo plane at +plane)
+struct SplitDesc {
+  const float* src;
+  const float* extra;
+  uint16_t* dst;
+  int64_t lds, ldd, plane;
+  int64_t block_start;
+  int32_t rows, cols;
+  int32_t vec;  // src rows 16-B aligned (float4 loads)
+  int32_t pad;
+};
+
 // syrk.hip implicit-im2col mode: the SYRK input rows are the patches of an
 // NHWC conv input, columns in natural (kh, kw, c) order, read straight from
 // the activation (the patch matrix is never materialised)

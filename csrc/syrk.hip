@@ -43,6 +43,12 @@ typedef __bf16 v8bf16 __attribute__((ext_vector_type(8)));
 typedef float v16f __attribute__((ext_vector_type(16)));
 typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
 
+// position of (i, j), i <= j, in the row-major packed upper triangle of a
+// D x D matrix (the layout of comm_pack's triangle wire)
+__device__ __forceinline__ int64_t triu_index(int64_t i, int64_t j, int64_t D) {
+  return i * D - i * (i - 1) / 2 + (j - i);
+}
+
 // upper-triangle tile enumeration: t -> (bi, bj), bi <= bj, row-major
 __device__ __forceinline__ void tile_of(int t, int T, int& bi, int& bj) {
   int i = 0, rem = t;
@@ -366,7 +372,7 @@ __device__ __forceinline__ v8bf16 frag_bf16(const short* L, int cb, int kk) {
 template <typename TIn, typename Stage>
 __global__ void __launch_bounds__(NT)
 syrk_kernel(const void* __restrict__ X, int64_t N, int64_t K, int64_t ldx,
-            int bias, float* __restrict__ C, int64_t D, int64_t ldc,
+            int bias, float* __restrict__ C, int64_t D, int64_t ldc, int packed,
             float alpha, float beta, int T, int splits, int64_t rows_per_split,
             int vec_ok, ConvGeom geom, float* __restrict__ ws) {
   using LT = typename std::conditional<std::is_same<TIn, float>::value, float,
@@ -467,6 +473,18 @@ syrk_kernel(const void* __restrict__ X, int64_t N, int64_t K, int64_t ldx,
             const int lr = wr * 64 + mi * 32 + 8 * rb + 4 * (l >> 5) + e;
             slab[lr * BM + lc] = acc[mi][nj][rb * 4 + e];
           }
+        } else if (packed) {
+          // packed upper triangle (the all-reduce wire layout): owned
+          // elements only, read-modify-write in place, no mirror
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int64_t gr = gr0 + e;
+            if (gr < D && gc < D && gr <= gc) {
+              const int64_t pi = triu_index(gr, gc, D);
+              const float old = beta != 0.f ? C[pi] : 0.f;
+              C[pi] = beta * old + alpha * acc[mi][nj][rb * 4 + e];
+            }
+          }
         } else if (!diag) {
           // strictly upper tile: write C[gr][gc] and mirror C[gc][gr..gr+3]
           float v[4];
@@ -511,7 +529,7 @@ syrk_kernel(const void* __restrict__ X, int64_t N, int64_t K, int64_t ldx,
 // C[j][i] = C[i][j] through an LDS transpose (both writes coalesced).
 __global__ void __launch_bounds__(256)
 splitk_reduce_kernel(const float* __restrict__ ws, int splits, int T,
-                     float* __restrict__ C, int64_t D, int64_t ldc,
+                     float* __restrict__ C, int64_t D, int64_t ldc, int packed,
                      float alpha, float beta, int T32) {
   __shared__ float tile[32][33];
   // blockIdx.x -> (bi, bj), bi <= bj, over the T32 x T32 sub-block grid
@@ -554,12 +572,14 @@ splitk_reduce_kernel(const float* __restrict__ ws, int splits, int T,
     float v = 0.f;
     const bool upper = gr < D && gc < D && (bi < bj || gr <= gc);
     if (upper) {
-      const float old = beta != 0.f ? C[gr * ldc + gc] : 0.f;
+      const int64_t idx = packed ? triu_index(gr, gc, D) : gr * ldc + gc;
+      const float old = beta != 0.f ? C[idx] : 0.f;
       v = beta * old + alpha * a4[e];
-      C[gr * ldc + gc] = v;
+      C[idx] = v;
     }
     tile[r][c4 + e] = v;
   }
+  if (packed) return;  // uniform: the packed triangle has no mirror
   __syncthreads();
   // mirror: C[bj*32 + r][bi*32 + c] = tile[c][r]  (strictly lower elements)
 #pragma unroll
@@ -600,10 +620,13 @@ int64_t syrk_workspace_floats(int64_t D, int64_t splits) {
 // geom == nullptr: X is a dense [N, K] matrix (row stride ldx); otherwise
 // X is an NHWC conv input and its rows are the conv patches (implicit im2col).
 // ws: syrk_workspace_floats(D, splits) floats when splits > 1.
+// ldc == 0: C is the packed upper triangle (D (D + 1) / 2 floats, row-major,
+// the all-reduce wire layout) and only it is written.
 void syrk(int in_dtype, const void* x, int64_t N, int64_t K, int64_t ldx,
           bool bias, float* C, int64_t D, int64_t ldc, float alpha,
           float beta, int splits, hipStream_t s, const ConvGeom* geom,
           float* ws) {
+  const int packed = ldc == 0 ? 1 : 0;
   if (D <= 0) return;
   const int T = (int)ceil_div(D, BM);
   const int64_t tiles = (int64_t)T * (T + 1) / 2;
@@ -617,29 +640,29 @@ void syrk(int in_dtype, const void* x, int64_t N, int64_t K, int64_t ldx,
                        ((reinterpret_cast<uintptr_t>(x) & 15) == 0);
     if (geom != nullptr)
       syrk_kernel<float, PatchStaging<float>><<<grid, dim3(NT), 0, s>>>(
-          x, N, K, ldx, bias ? 1 : 0, C, D, ldc, alpha, beta, T, splits,
+          x, N, K, ldx, bias ? 1 : 0, C, D, ldc, packed, alpha, beta, T, splits,
           rows_per_split, vec_ok, g, ws);
     else
       syrk_kernel<float, DenseStaging<float>><<<grid, dim3(NT), 0, s>>>(
-          x, N, K, ldx, bias ? 1 : 0, C, D, ldc, alpha, beta, T, splits,
+          x, N, K, ldx, bias ? 1 : 0, C, D, ldc, packed, alpha, beta, T, splits,
           rows_per_split, vec_ok, g, ws);
   } else {
     const int vec_ok = ((ldx & 7) == 0) &&
                        ((reinterpret_cast<uintptr_t>(x) & 15) == 0);
     if (geom != nullptr)
       syrk_kernel<bf16_t, PatchStaging<bf16_t>><<<grid, dim3(NT), 0, s>>>(
-          x, N, K, ldx, bias ? 1 : 0, C, D, ldc, alpha, beta, T, splits,
+          x, N, K, ldx, bias ? 1 : 0, C, D, ldc, packed, alpha, beta, T, splits,
           rows_per_split, vec_ok, g, ws);
     else
       syrk_kernel<bf16_t, DenseStaging<bf16_t>><<<grid, dim3(NT), 0, s>>>(
-          x, N, K, ldx, bias ? 1 : 0, C, D, ldc, alpha, beta, T, splits,
+          x, N, K, ldx, bias ? 1 : 0, C, D, ldc, packed, alpha, beta, T, splits,
           rows_per_split, vec_ok, g, ws);
   }
   if (splits > 1) {
     const int T32 = (int)ceil_div(D, 32);
     const unsigned blocks = (unsigned)((int64_t)T32 * (T32 + 1) / 2);
     splitk_reduce_kernel<<<dim3(blocks), dim3(256), 0, s>>>(
-        ws, splits, T, C, D, ldc, alpha, beta, T32);
+        ws, splits, T, C, D, ldc, packed, alpha, beta, T32);
   }
 }
 

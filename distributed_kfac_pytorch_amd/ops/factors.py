@@ -4,7 +4,11 @@
 
     out = beta * out + alpha * Xt^T Xt,   Xt = [x, 1] if bias else x
 
-for a 2D ``x`` of shape [N, K].  On MI355X this is one MFMA SYRK launch
+for a 2D ``x`` of shape [N, K].  ``out`` is either the dense [D, D] factor
+or its packed upper triangle (1-D, D (D + 1) / 2, row-major -- the layout of
+the factor all-reduce wire, see ``parallel/comm.py``
+``PackedFactorBuffer``): the SYRK epilogue then updates the triangle in
+place and writes nothing else.  On MI355X this is one MFMA SYRK launch
 (csrc/syrk.hip) that reads ``x`` once in its native dtype (bf16 under
 autocast, fp32 otherwise), synthesises the bias column, and writes an exactly
 symmetric fp32 result with the EMA / averaging weights folded into
@@ -12,6 +16,8 @@ symmetric fp32 result with the EMA / averaging weights folded into
 (``kfac/layers/utils.py:17-58``).
 """
 from __future__ import annotations
+
+import math
 
 import torch
 
@@ -37,6 +43,26 @@ def _torch_cov_accumulate_(
         out.mul_(beta).add_(cov, alpha=alpha)
 
 
+def packed_dim(out: torch.Tensor) -> int:
+    """D of a packed D x D upper triangle held in the 1-D ``out``."""
+    n = out.numel()
+    d = int((math.isqrt(8 * n + 1) - 1) // 2)
+    if d * (d + 1) // 2 != n:
+        raise ValueError(f'{n} elements is not a packed triangle')
+    return d
+
+
+def _packed_emulate_(out: torch.Tensor, fn) -> None:  # type: ignore[no-untyped-def]
+    """Apply a dense in-place update to a packed triangle (CPU / fallback)."""
+    from distributed_kfac_pytorch_amd.ops import comm_pack
+
+    d = packed_dim(out)
+    dense = out.new_empty((d, d))
+    comm_pack.triu_unpack_(dense, out, 1.0)
+    fn(dense)
+    out.copy_(comm_pack.triu_pack(dense))
+
+
 def cov_accumulate_(
     out: torch.Tensor,
     x: torch.Tensor,
@@ -49,7 +75,10 @@ def cov_accumulate_(
     if x.dim() != 2:
         raise ValueError(f'expected a 2D input, got shape {tuple(x.shape)}')
     d = x.shape[1] + int(bias)
-    if out.shape != (d, d):
+    if out.dim() == 1:
+        if out.numel() != d * (d + 1) // 2:
+            raise ValueError(f'packed output must hold {d * (d + 1) // 2} elements')
+    elif out.shape != (d, d):
         raise ValueError(
             f'output must be [{d}, {d}], got {tuple(out.shape)}',
         )
@@ -60,6 +89,9 @@ def cov_accumulate_(
         if xin.stride(1) != 1 or (xin.shape[0] > 1 and xin.stride(0) < xin.shape[1]):
             xin = xin.contiguous()
         native().syrk(xin, out, bias, float(alpha), float(beta))
+        return out
+    if out.dim() == 1:
+        _packed_emulate_(out, lambda dense: _torch_cov_accumulate_(dense, x, bias, alpha, beta))
         return out
     _torch_cov_accumulate_(out, x, bias, alpha, beta)
     return out
@@ -92,7 +124,7 @@ def conv_cov_accumulate_(
         x.shape[1] % vec
         or any(v % vec for v in (st[0], st[2], st[3]))
         or x.data_ptr() % 16
-        or out.stride(1) != 1
+        or (out.dim() == 2 and out.stride(1) != 1)
     ):
         return False
     native().syrk_conv(x, out, kernel[0], kernel[1], stride[0], stride[1],

@@ -19,6 +19,17 @@ MI355X-first design differences (behaviour visible to callers is the same):
 * Buckets are keyed by the process group object (the reference keys them by
   group *size*, ``distributed.py:370-372``, which lets two different
   same-size groups share a bucket; that quirk is deliberately fixed).
+* Factor all-reduce without pack / unpack passes (``PackedFactorBuffer``):
+  on GPU, a symmetric factor reduced over a group of more than one rank
+  lives, between second-order updates, as its packed upper triangle inside
+  ONE persistent per-group buffer.  The factor-update SYRK reads the
+  averaged triangle from its slot and writes the new local value there
+  pre-scaled by 1/world (csrc/syrk.hip packed epilogue), so the all-reduce
+  (sum) of the buffer IS the averaged factor: no pack kernel before the
+  collective, no unpack after it, no per-step bucket allocation.  The dense
+  matrix is materialised (one unpack) only when something reads the factor
+  -- the eigendecomposition / inversion every ``inv_update_steps`` steps,
+  checkpointing.
 """
 from __future__ import annotations
 
@@ -227,6 +238,120 @@ class AllreduceTensorBucket:
         return self.work
 
 
+class PackedFactorBuffer:
+    """Persistent all-reduce buffer of the packed factor triangles of one
+    process group (see the module docstring).
+
+    Slots are assigned in first-use order -- identical on every rank, since
+    every rank registers the same factors in the same order -- and never
+    move once the buffer has been launched (a later registration re-allocates
+    the buffer and copies it, after waiting for every collective in flight).
+    ``launch()`` all-reduces, in cap-sized contiguous chunks, every chunk
+    holding a slot marked since the previous launch.
+    """
+
+    def __init__(self, group: dist.ProcessGroup | None, cap_bytes: int) -> None:
+        self.group = group
+        self._cap = cap_bytes
+        self._slots: dict[Any, tuple[int, int]] = {}
+        self._size = 0
+        self.flat: torch.Tensor | None = None
+        self._chunks: list[tuple[int, int, list[Any]]] = []
+        self._chunk_of: dict[Any, int] = {}
+        self._dirty: list[Any] = []
+        self._works: dict[Any, Any] = {}
+        self.launches = 0
+
+    def _rechunk(self) -> None:
+        self._chunks = []
+        self._chunk_of = {}
+        start = end = 0
+        keys: list[Any] = []
+        item = self.flat.element_size() if self.flat is not None else 4
+        for key, (off, n) in sorted(self._slots.items(), key=lambda kv: kv[1][0]):
+            if keys and self._cap > 0 and (end + n - start) * item > self._cap:
+                self._chunks.append((start, end, keys))
+                start, keys = end, []
+            keys.append(key)
+            end = off + n
+            if self._cap <= 0:  # unbucketed: one collective per factor
+                self._chunks.append((start, end, keys))
+                start, keys = end, []
+        if keys:
+            self._chunks.append((start, end, keys))
+        for i, (_, _, ks) in enumerate(self._chunks):
+            for k in ks:
+                self._chunk_of[k] = i
+
+    def has(self, key: Any) -> bool:
+        return key in self._slots
+
+    def view(self, key: Any, numel: int | None = None, like: torch.Tensor | None = None) -> torch.Tensor:
+        """The slot of ``key`` (registered on first use with ``numel``
+        elements of ``like``'s dtype / device)."""
+        if key not in self._slots:
+            assert numel is not None and like is not None
+            for w in self._works.values():
+                if w is not None:
+                    w.wait()
+            self._works = {}
+            old = self.flat
+            self._slots[key] = (self._size, numel)
+            self._size += numel
+            self.flat = torch.zeros(self._size, dtype=like.dtype, device=like.device)
+            if old is not None:
+                self.flat[: old.numel()].copy_(old)
+            self._rechunk()
+        off, n = self._slots[key]
+        assert self.flat is not None
+        return self.flat[off: off + n]
+
+    def mark(self, key: Any) -> None:
+        """The slot holds a new pre-scaled local value to be summed."""
+        if key not in self._dirty:
+            self._dirty.append(key)
+
+    def pending(self, key: Any) -> bool:
+        return key in self._dirty
+
+    def launch(self) -> None:
+        """All-reduce every chunk holding a marked slot (collective)."""
+        if not self._dirty:
+            return
+        assert self.flat is not None
+        todo = sorted({self._chunk_of[k] for k in self._dirty})
+        self._dirty = []
+        for i in todo:
+            start, end, keys = self._chunks[i]
+            work = dist.all_reduce(self.flat[start:end], group=self.group, async_op=True)
+            for k in keys:
+                self._works[k] = work
+        self.launches += 1
+
+    def wait(self, key: Any) -> None:
+        """Order the current stream after the slot's last all-reduce."""
+        w = self._works.pop(key, None)
+        if w is not None:
+            w.wait()
+
+
+class _SlotHandle:
+    """Bucket-like handle an ``AsyncTensor`` waits on for one packed slot."""
+
+    __slots__ = ('_buf', '_key')
+
+    def __init__(self, buf: PackedFactorBuffer, key: Any) -> None:
+        self._buf = buf
+        self._key = key
+
+    def communicated(self) -> bool:
+        return not self._buf.pending(self._key)
+
+    @property
+    def work(self) -> Any:
+        return self._buf._works.pop(self._key, None)
+
+
 class TorchDistributedCommunicator:
     """All-reduce / broadcast helper used by every K-FAC layer.
 
@@ -240,6 +365,22 @@ class TorchDistributedCommunicator:
         self._bucket_cap_bytes = int(bucket_cap_mb * 1000 * 1000)
         self._allreduce_buckets: dict[Any, AllreduceTensorBucket | None] = {}
         self._broadcast_buckets: dict[Any, BroadcastTensorBucket] = {}
+        self._packed: dict[Any, PackedFactorBuffer] = {}
+
+    def packed_buffer(self, group: dist.ProcessGroup | None, dtype: torch.dtype,
+                      device: torch.device) -> PackedFactorBuffer:
+        """The persistent packed-factor buffer of ``group``."""
+        key = (group, dtype, str(device))
+        buf = self._packed.get(key)
+        if buf is None:
+            buf = PackedFactorBuffer(group, self._bucket_cap_bytes)
+            self._packed[key] = buf
+        return buf
+
+    def packed_result(self, buf: PackedFactorBuffer, key: Any,
+                      finalize: Callable[[], torch.Tensor]) -> AsyncTensor:
+        """Handle resolving to ``finalize()`` once the slot is reduced."""
+        return AsyncTensor(finalize=finalize, bucket=_SlotHandle(buf, key))  # type: ignore[arg-type]
 
     @property
     def bucket_cap_bytes(self) -> int:
@@ -403,12 +544,15 @@ class TorchDistributedCommunicator:
             bucket.broadcast()
 
     def flush_allreduce_buckets(self) -> None:
-        """Launch every partially filled bucket (collective on all ranks)."""
+        """Launch every partially filled bucket and every packed-factor
+        buffer with marked slots (collective on all ranks)."""
         for key in list(self._allreduce_buckets):
             bucket = self._allreduce_buckets[key]
             if bucket is not None:
                 bucket.allreduce()
                 self._allreduce_buckets[key] = None
+        for buf in self._packed.values():
+            buf.launch()
 
 
 class BroadcastTensorBucket:

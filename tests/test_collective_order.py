@@ -36,7 +36,10 @@ class _Net(torch.nn.Module):
         return self.fc2(x)
 
 
-def _record(frac: float, method: str, bucket_mb: float, steps: int) -> None:
+def _record(frac: float, method: str, bucket_mb: float, steps: int, packed: str = '0') -> None:
+    import os
+
+    os.environ['KFAC_PACKED_FACTORS'] = packed
     world = dist.get_world_size()
     rank = dist.get_rank()
     calls: list[tuple] = []
@@ -103,13 +106,14 @@ def _record(frac: float, method: str, bucket_mb: float, steps: int) -> None:
 
 
 @pytest.mark.parametrize(
-    'frac,method,bucket_mb',
+    'frac,method,bucket_mb,packed',
     [
-        (0.5, 'eigen', 25.0),     # HYBRID-OPT: inverse + gradient broadcasts
-        (0.5, 'eigen', 0.001),    # one bucket per tensor
-        (0.25, 'inverse', 25.0),  # MEM-OPT
-        (1.0, 'inverse', 0.0),    # COMM-OPT, unbucketed all-reduce
+        (0.5, 'eigen', 25.0, '0'),     # HYBRID-OPT: inverse + gradient broadcasts
+        (0.5, 'eigen', 0.001, '0'),    # one bucket per tensor
+        (0.25, 'inverse', 25.0, '0'),  # MEM-OPT
+        (1.0, 'inverse', 0.0, '0'),    # COMM-OPT, unbucketed all-reduce
+        (0.5, 'eigen', 0.01, '1'),     # persistent packed-factor buffer, chunked
     ],
 )
-def test_collective_sequences_match(frac, method, bucket_mb):
-    run_distributed(_record, 4, frac, method, bucket_mb, 9)
+def test_collective_sequences_match(frac, method, bucket_mb, packed):
+    run_distributed(_record, 4, frac, method, bucket_mb, 9, packed)
