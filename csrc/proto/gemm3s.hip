@@ -40,8 +40,8 @@
 // rows as v1.  Epilogues: eigenvalue scaling (S = dGdA, or 1/(dG dA^T +
 // damping)), then either fp32 (the preconditioned gradient P) or the split
 // image of the result (the next GEMM's operand).
-#include "common.h"
-#include "descs.h"
+#include "../common.h"
+#include "../descs.h"
 
 namespace kfac {
 

@@ -308,9 +308,13 @@ class KFACBaseLayer:
         """The factor all-reduce goes through the persistent packed buffer:
         symmetric factors, more than one rank, fp32, and a GPU
         (``KFAC_PACKED_FACTORS``: auto = GPU only, 1 = also the CPU
-        emulation used by the gloo tests, 0 = off)."""
+        emulation used by the gloo tests, 0 = off).  The slot bookkeeping is
+        host-side, so auto stays off under the opt-in multi-rank step graphs
+        (``KFAC_STEP_GRAPHS_MULTI=1``), whose replays would skip it."""
         mode = os.environ.get('KFAC_PACKED_FACTORS', 'auto')
         if mode == '0' or not self._pack_factors() or get_world_size(group) == 1:
+            return False
+        if mode == 'auto' and os.environ.get('KFAC_STEP_GRAPHS_MULTI', '0') == '1':
             return False
         if self.factor_dtype not in (None, torch.float32):
             return False

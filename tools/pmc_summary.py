@@ -6,7 +6,8 @@ gpu_r2_pmc.sh) and writes a CSV plus a markdown table:
 
 * time: summed dispatch durations of the sq pass (counter passes serialise
   dispatches, so absolute times are profiled times);
-* clock: GRBM_GUI_ACTIVE / 8 XCDs / duration (reads high below ~0.3 ms);
+* (GRBM_GUI_ACTIVE is collected but not turned into a clock: summed over
+  serialised dispatches and hardware units it does not give one);
 * MFMA pipe utilisation: SQ_VALU_MFMA_BUSY_CYCLES / (duration x 2.4 GHz x
   1024 SIMDs), and MFMA TFLOP/s from SQ_INSTS_VALU_MFMA_MOPS_* (x 512 FLOP);
 * HBM: FETCH_SIZE / WRITE_SIZE in KB (FETCH_SIZE under-counts wide
@@ -73,9 +74,6 @@ def load(base: str, prefix: str) -> dict:
     for k, t in times.items():
         c = counters.get(k, {})
         row = {'kernel': k, 'dispatches': counts[k], 'time_ms': round(t, 3)}
-        gpu_cycles = c.get('GRBM_GUI_ACTIVE', 0.0) / XCDS
-        if t > 0 and gpu_cycles:
-            row['clock_ghz'] = round(gpu_cycles / (t * 1e-3) / 1e9, 2)
         if t > 0:
             # MFMA pipe busy fraction at the nominal 2.4 GHz (a lower bound
             # when the chip clocks down under load)
@@ -106,7 +104,7 @@ def load(base: str, prefix: str) -> dict:
 def main() -> None:
     base, prefix, dest = sys.argv[1], sys.argv[2], sys.argv[3]
     rows = sorted(load(base, prefix).values(), key=lambda r: -r['time_ms'])
-    keys = ['kernel', 'dispatches', 'time_ms', 'clock_ghz', 'mfma_util', 'mfma_tflops',
+    keys = ['kernel', 'dispatches', 'time_ms', 'mfma_util', 'mfma_tflops',
             'fetch_gbs', 'write_gbs', 'l2_hit', 'lds_conflict', 'fetch_kb', 'write_kb',
             'mfma_mops_bf16', 'mfma_mops_f32', 'waves']
     with open(dest + '.csv', 'w', newline='') as f:
@@ -115,11 +113,11 @@ def main() -> None:
         for r in rows:
             w.writerow(r)
     with open(dest + '.md', 'w') as f:
-        f.write('| kernel | n | ms | GHz | MFMA util | MFMA TF/s | fetch GB/s | write GB/s | L2 hit | LDS confl |\n')
-        f.write('|---|---|---|---|---|---|---|---|---|---|\n')
+        f.write('| kernel | n | ms | MFMA util | MFMA TF/s | fetch GB/s | write GB/s | L2 hit | LDS confl |\n')
+        f.write('|---|---|---|---|---|---|---|---|---|\n')
         for r in rows[:25]:
-            f.write('| {} | {} | {} | {} | {} | {} | {} | {} | {} | {} |\n'.format(
-                r['kernel'], r['dispatches'], r['time_ms'], r.get('clock_ghz', ''),
+            f.write('| {} | {} | {} | {} | {} | {} | {} | {} | {} |\n'.format(
+                r['kernel'], r['dispatches'], r['time_ms'],
                 r.get('mfma_util', ''), r.get('mfma_tflops', ''), r.get('fetch_gbs', ''),
                 r.get('write_gbs', ''), r.get('l2_hit', ''), r.get('lds_conflict', '')))
     print(json.dumps(rows[:12], indent=None)[:4000])
