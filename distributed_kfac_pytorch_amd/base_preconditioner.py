@@ -352,6 +352,12 @@ class BaseKFACPreconditioner:
         self._update_factors_in_hook = update_factors_in_hook
         self._steps = 0
         self._mini_steps: dict[str, int] = defaultdict(int)
+        # backward-hook count per layer, kept apart from the forward count so
+        # a schedule that runs several forwards before their backwards (a
+        # GPipe / 1F1B pipeline) still folds G exactly once per step; with
+        # interleaved forward / backward it equals the reference's shared
+        # counter (kfac/base_preconditioner.py:_save_grad_output)
+        self._mini_steps_g: dict[str, int] = defaultdict(int)
         self._kl_acc: torch.Tensor | None = None
         self._kl_scale: torch.Tensor | None = None
         self._multi_apply: Any = None
@@ -600,6 +606,7 @@ class BaseKFACPreconditioner:
                 decay = self.factor_decay
                 for name, layer in ordered:
                     self._mini_steps[name] = 0
+                    self._mini_steps_g[name] = 0
                     layer.update_a_factor(alpha=decay)
                     layer.reduce_a_factor(self._assignment.factor_group(name, 'A'))
                     layer.update_g_factor(alpha=decay)
@@ -639,6 +646,7 @@ class BaseKFACPreconditioner:
 
         self._steps += 1
         self._mini_steps = defaultdict(int)
+        self._mini_steps_g = defaultdict(int)
 
     def _precondition_all(self, ordered: list[tuple[str, KFACBaseLayer]]) -> None:
         """Precondition this rank's layers; broadcast results if needed."""
@@ -889,9 +897,10 @@ class BaseKFACPreconditioner:
         name, layer = self._layers[module]
         if isinstance(grad_output, torch.Tensor):
             grad_output = (grad_output,)
+        self._mini_steps_g[name] += 1
         in_hook = (
             self._update_factors_in_hook
-            and self._mini_steps[name] % self._accumulation_steps == 0
+            and self._mini_steps_g[name] % self._accumulation_steps == 0
         )
         if in_hook and self._accumulation_steps == 1 and isinstance(grad_output[0], torch.Tensor):
             decay = self.factor_decay

@@ -167,6 +167,7 @@ class GraphedTrainStep:
         if p is not None:
             p._steps += 1
             p._mini_steps = defaultdict(int)
+            p._mini_steps_g = defaultdict(int)
 
     def _capturable(self) -> bool:
         p = self.preconditioner
@@ -224,6 +225,7 @@ class GraphedTrainStep:
             # capture ran the step's host code without executing it
             p._steps = saved
             p._mini_steps = defaultdict(int)
+            p._mini_steps_g = defaultdict(int)
         self.graphs[kind] = g
         self.outputs[kind] = loss
         self.grads[kind] = [q.grad for q in self._params()]

@@ -90,6 +90,50 @@ class GPTNeoXBlock(torch.nn.Module):
         )
 
 
+EMBED_SEED = 7919
+HEAD_SEED = 7927
+
+
+def _seeded_embedding(vocab: int, hidden: int, seed: int) -> torch.nn.Embedding:
+    # independent of the global RNG, so a pipeline stage that builds only
+    # some of the layers gets the same weights as the whole model
+    e = torch.nn.Embedding(vocab, hidden)
+    with torch.no_grad():
+        e.weight.normal_(generator=torch.Generator().manual_seed(seed))
+    return e
+
+
+def _seeded_head(hidden: int, vocab: int, seed: int) -> torch.nn.Linear:
+    lin = torch.nn.Linear(hidden, vocab, bias=False)
+    bound = 1.0 / hidden ** 0.5
+    with torch.no_grad():
+        lin.weight.uniform_(-bound, bound, generator=torch.Generator().manual_seed(seed))
+    return lin
+
+
+class GPTNeoXEmbedding(torch.nn.Module):
+    """First pipeline layer: token embedding."""
+
+    def __init__(self, vocab: int, hidden: int) -> None:
+        super().__init__()
+        self.embed_in = _seeded_embedding(vocab, hidden, EMBED_SEED)
+
+    def forward(self, tokens: torch.Tensor) -> torch.Tensor:
+        return self.embed_in(tokens)
+
+
+class GPTNeoXHead(torch.nn.Module):
+    """Last pipeline layer: final LayerNorm + LM head (logits)."""
+
+    def __init__(self, hidden: int, vocab: int) -> None:
+        super().__init__()
+        self.final_layer_norm = torch.nn.LayerNorm(hidden)
+        self.embed_out = _seeded_head(hidden, vocab, HEAD_SEED)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return self.embed_out(self.final_layer_norm(x))
+
+
 class GPTNeoX(torch.nn.Module):
     def __init__(
         self,
@@ -100,18 +144,35 @@ class GPTNeoX(torch.nn.Module):
         group: dist.ProcessGroup | None = None,
     ) -> None:
         super().__init__()
-        self.embed_in = torch.nn.Embedding(vocab, hidden)
+        self.embed_in = _seeded_embedding(vocab, hidden, EMBED_SEED)
         self.layers = torch.nn.ModuleList(
             [GPTNeoXBlock(hidden, heads, group, seed=100 * i) for i in range(layers)],
         )
         self.final_layer_norm = torch.nn.LayerNorm(hidden)
-        self.embed_out = torch.nn.Linear(hidden, vocab, bias=False)
+        self.embed_out = _seeded_head(hidden, vocab, HEAD_SEED)
 
     def forward(self, tokens: torch.Tensor) -> torch.Tensor:
         x = self.embed_in(tokens)
         for blk in self.layers:
             x = blk(x)
         return self.embed_out(self.final_layer_norm(x))
+
+
+def gpt_neox_pipeline_layers(
+    vocab: int = 50304,
+    hidden: int = 768,
+    layers: int = 12,
+    heads: int = 12,
+    group: dist.ProcessGroup | None = None,
+) -> list:
+    """Layer constructors for ``neox.pipeline.PipelineModule``: embedding,
+    the blocks, the head -- weight for weight the layers of ``GPTNeoX`` with
+    the same arguments, whatever the stage partition."""
+    out: list = [lambda: GPTNeoXEmbedding(vocab, hidden)]
+    for i in range(layers):
+        out.append(lambda i=i: GPTNeoXBlock(hidden, heads, group, seed=100 * i))
+    out.append(lambda: GPTNeoXHead(hidden, vocab))
+    return out
 
 
 def gpt_neox_125m(group: dist.ProcessGroup | None = None, vocab: int = 50304) -> GPTNeoX:

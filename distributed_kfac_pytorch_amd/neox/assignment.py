@@ -71,8 +71,19 @@ class GPTNeoXAssignment(WorkAssignment):
         elif set(self.pipe_parallel_peers) == set(self.data_parallel_peers):
             self.pipe_parallel_peer_group = data_parallel_group
         else:
+            # every rank must enter every group creation, in the same order
+            # (torch.distributed.new_group); the reference creates only its
+            # own stage's group (kfac/gpt_neox/assignment.py:86-92), which
+            # deadlocks once pp > 1 and the stage peers are neither the DP
+            # nor the MP group
             make = group_func if group_func is not None else dist.new_group
-            self.pipe_parallel_peer_group = make(self.pipe_parallel_peers)
+            self.pipe_parallel_peer_group = None
+            for stage in range(topology.get_dim('pipe')):
+                peers = [r for r in range(topology.world_size())
+                         if topology.get_coord(r).pipe == stage]
+                g = make(peers)
+                if stage == self.pipe_parallel_rank:
+                    self.pipe_parallel_peer_group = g
 
         loads = [0.0] * len(self.pipe_parallel_peers)
         self._inv_assignments: dict[str, dict[str, int]] = {

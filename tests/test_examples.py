@@ -115,3 +115,13 @@ def test_gpt_neox_cli_tp(tmp_path):
     assert [line['step'] for line in lines if 'step' in line] == [2, 4]
     assert lines[-1]['tokens_per_s'] > 0
     assert len(list(tmp_path.iterdir())) == 8  # one factor file per TP layer
+
+
+def test_gpt_neox_cli_pipeline(tmp_path):
+    """pp 2 x mp 2 (4 gloo ranks): GPipe schedule, K-FAC per stage."""
+    lines = _run(['examples/torch_gpt_neox.py', '--pp', '2', '--mp', '2', '--micro-batches', '2',
+                  '--steps', '4', '--seq-len', '16', '--micro-batch', '4',
+                  '--factor-update-steps', '1', '--inv-update-steps', '2',
+                  '--log-interval', '2', '--no-cuda', '--backend', 'gloo'], nproc=4)
+    assert [line['step'] for line in lines if 'step' in line] == [2, 4]
+    assert lines[-1]['tokens_per_s'] > 0

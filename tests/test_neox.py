@@ -330,3 +330,120 @@ def test_preconditioner_validation():
     with pytest.warns(UserWarning):
         p.factor_checkpoint_dir = '/nonexistent/kfac'
         p.load_factors_from_dir()
+
+
+# --------------------------------------------------------- pipeline parallel
+def _pipe_build(pp: int, mp: int, dp: int, rank: int):
+    from distributed_kfac_pytorch_amd.models.gpt_neox import gpt_neox_pipeline_layers
+
+    topo = PipeModelDataParallelTopology(num_pp=pp, num_mp=mp, num_dp=dp)
+    groups = {'model': None, 'data': None, 'pipe': None}
+    if dist.is_initialized():
+        for axis in ('model', 'data', 'pipe'):
+            for ranks in topo.get_axis_comm_lists(axis):
+                g = dist.new_group(ranks)
+                if rank in ranks:
+                    groups[axis] = g
+    model = PipelineModule(
+        gpt_neox_pipeline_layers(vocab=32, hidden=16, layers=3, heads=4, group=groups['model']),
+        topo, rank=rank,
+    )
+    return model, topo, groups
+
+
+def _pipe_steps(model, pre, batches, micro: int, lr: float = 0.2) -> list:
+    losses = []
+    for tokens in batches:
+        model.zero_grad()
+        loss = model.train_batch(
+            tokens[:, :-1], tokens[:, 1:],
+            lambda out, y: torch.nn.functional.cross_entropy(out.flatten(0, 1), y.flatten()),
+            micro_batches=micro, activation_shape=(tokens.shape[0] // micro, tokens.shape[1] - 1, 16),
+        )
+        pre.step()
+        with torch.no_grad():
+            for p in model.parameters():
+                p -= lr * p.grad
+        losses.append(None if loss is None else float(loss))
+    return losses
+
+
+def _pipe_reference(batches, micro):
+    model, _, _ = _pipe_build(1, 1, 1, 0)
+    pre = GPTNeoXKFACPreconditioner(model, factor_update_steps=1, inv_update_steps=2,
+                                   lr=0.2, kl_clip=0.01, accumulation_steps=micro)
+    losses = _pipe_steps(model, pre, batches, micro)
+    return losses, [[p.detach().clone() for p in layer.parameters()] for layer in model.layers]
+
+
+def _pp2_matches_pp1(batches, micro, ref_losses, ref_params):
+    rank = dist.get_rank()
+    model, topo, groups = _pipe_build(2, 1, 1, rank)
+    pre = GPTNeoXKFACPreconditioner(
+        model, factor_update_steps=1, inv_update_steps=2, lr=0.2, kl_clip=0.01,
+        accumulation_steps=micro, model_parallel_group=groups['model'],
+        data_parallel_group=groups['data'], pipeline_parallel_group=groups['pipe'],
+    )
+    # stage 0: embedding + block 0 (+ block 1); stage 1: the rest + head
+    assert len(pre._layers) == 4 * (model.parts[rank + 1] - model.parts[rank]
+                                    - int(rank == 0) - int(rank == 1))
+    losses = _pipe_steps(model, pre, batches, micro)
+    if model.is_last_stage:
+        for a, b in zip(losses, ref_losses):
+            assert abs(a - b) < 1e-5, (losses, ref_losses)
+    lo = model.parts[model.stage_id]
+    for j, layer in enumerate(model.layers):
+        for p, q in zip(layer.parameters(), ref_params[lo + j]):
+            torch.testing.assert_close(p.detach(), q, rtol=1e-4, atol=1e-6)
+
+
+def test_pipeline_pp2_matches_single_stage():
+    g = torch.Generator().manual_seed(11)
+    batches = [torch.randint(0, 32, (4, 9), generator=g) for _ in range(4)]
+    ref_losses, ref_params = _pipe_reference(batches, 2)
+    assert ref_losses[-1] < ref_losses[0]
+    run_distributed(_pp2_matches_pp1, 2, batches, 2, ref_losses, ref_params)
+
+
+def _pp2_trains(mp: int, dp: int):
+    from distributed_kfac_pytorch_amd.neox.pipeline import allreduce_gradients
+
+    torch.set_num_threads(1)
+    rank = dist.get_rank()
+    model, topo, groups = _pipe_build(2, mp, dp, rank)
+    pre = GPTNeoXKFACPreconditioner(
+        model, factor_update_steps=1, inv_update_steps=2, lr=0.2, accumulation_steps=2,
+        model_parallel_group=groups['model'], data_parallel_group=groups['data'],
+        pipeline_parallel_group=groups['pipe'],
+    )
+    coord = topo.get_coord(rank)
+    g = torch.Generator().manual_seed(coord.data)
+    tokens = torch.randint(0, 32, (4, 9), generator=g)
+    losses = []
+    for _ in range(8):
+        model.zero_grad()
+        loss = model.train_batch(
+            tokens[:, :-1], tokens[:, 1:],
+            lambda out, y: torch.nn.functional.cross_entropy(out.flatten(0, 1), y.flatten()),
+            micro_batches=2, activation_shape=(2, 8, 16),
+        )
+        allreduce_gradients(model, groups['data'])
+        pre.step()
+        with torch.no_grad():
+            for p in model.parameters():
+                p -= 0.2 * p.grad
+        if loss is not None:
+            losses.append(float(loss))
+    if model.is_last_stage:
+        assert losses[-1] < losses[0], losses
+    # data-parallel replicas of a stage shard stay identical
+    for p in model.parameters():
+        q = p.detach().clone()
+        dist.broadcast(q, src=topo.get_rank(pipe=coord.pipe, data=0, model=coord.model),
+                       group=groups['data'])
+        assert torch.allclose(q, p.detach(), atol=1e-5)
+
+
+@pytest.mark.parametrize('mp,dp', [(2, 1), (1, 2), (2, 2)])
+def test_pipeline_pp2_training(mp, dp):
+    run_distributed(_pp2_trains, 2 * mp * dp, mp, dp)
