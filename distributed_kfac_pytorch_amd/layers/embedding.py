@@ -120,7 +120,8 @@ class _DiagonalAMixin:
     def reduce_a_factor(self, group: Any = None) -> None:  # type: ignore[override]
         if self.a_factor is None:  # type: ignore[attr-defined]
             raise RuntimeError('a_factor is None, cannot reduce')
-        self.a_factor = self._allreduce()(self.a_factor, average=True, symmetric=False, group=group)  # type: ignore[attr-defined]
+        self.a_factor = self._allreduce()(  # type: ignore[attr-defined]
+            self.a_factor, average=True, symmetric=False, group=group)
 
     def _a_to_ref(self, a: torch.Tensor) -> torch.Tensor:
         return a

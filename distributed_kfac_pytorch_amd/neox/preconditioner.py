@@ -134,7 +134,10 @@ class GPTNeoXKFACPreconditioner(BaseKFACPreconditioner):
         for name, layer in kfac_layers.values():
             logger.log(loglevel, f'Registered name="{name}": {layer!r} on global-rank={get_rank()}')
 
-        cost = (lambda n: float(n) ** 3) if assignment_strategy == AssignmentStrategy.COMPUTE else (lambda n: float(n) ** 2)
+        power = 3 if assignment_strategy == AssignmentStrategy.COMPUTE else 2
+
+        def cost(n: int) -> float:
+            return float(n) ** power
         work = {
             name: {
                 'A': cost(layer.module.a_factor_shape[0]),

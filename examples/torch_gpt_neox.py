@@ -162,7 +162,9 @@ def main(argv: list[str] | None = None) -> dict[str, float]:
     return out
 
 
-def _train_pipeline(args, model, topo, cfg, mp_group, dp_group, pipe_group) -> dict[str, float]:  # type: ignore[no-untyped-def]
+def _train_pipeline(  # type: ignore[no-untyped-def]
+    args, model, topo, cfg, mp_group, dp_group, pipe_group,
+) -> dict[str, float]:
     """pp > 1: GPipe micro-batch schedule (``PipelineModule.train_batch``),
     data-parallel gradient average per stage, K-FAC per stage with the
     micro-batches as accumulation steps and the KL clip summed over the

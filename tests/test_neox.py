@@ -143,7 +143,7 @@ def _tp_vs_dense():
     x = torch.randn(5, 6, generator=torch.Generator().manual_seed(1))
     y = row(torch.relu(col(x)))
     yd = torch.nn.functional.linear(
-        torch.relu(torch.nn.functional.linear(x, dcol.weight.detach() if False else _full(3, 8, 6)[0], _full(3, 8, 6)[1])),
+        torch.relu(torch.nn.functional.linear(x, _full(3, 8, 6)[0], _full(3, 8, 6)[1])),
         _full(4, 6, 8)[0], _full(4, 6, 8)[1],
     )
     assert torch.allclose(y, yd, atol=1e-5)

@@ -7,7 +7,6 @@ import warnings
 
 import pytest
 import torch
-import torch.distributed as dist
 
 import distributed_kfac_pytorch_amd as kfac
 from distributed_kfac_pytorch_amd.base_preconditioner import BaseKFACPreconditioner

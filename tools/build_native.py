@@ -3,8 +3,9 @@
 Drives ``hipcc --offload-arch=gfx950`` directly (no hipify, no JIT cache):
 every ``csrc/*.hip`` kernel file is compiled to an object, the
 ``csrc/*.cpp`` host files (bindings, rocSOLVER tier -- the only torch-aware
-translation units) are compiled against the installed PyTorch-ROCm headers, and everything is linked into one shared object next
-to the Python package so it travels with the repo snapshot to the GPU box.
+translation units) are compiled against the installed PyTorch-ROCm headers,
+and everything is linked into one shared object next to the Python package
+so it travels with the repo snapshot to the GPU box.
 
 Usage:  python tools/build_native.py [--force] [--jobs N] [--verbose]
 """
