@@ -163,3 +163,35 @@ def test_factor_side_stream_matches_inline(cuda, monkeypatch):
     with pytest.warns(UserWarning, match='modified in place'):
         pres[0].step()
     assert pres[0]._factor_stream_off
+
+
+@pytest.mark.parametrize('method', ['eigen', 'inverse'])
+def test_embedding_kfac_gpu_matches_cpu(cuda, method):
+    """nn.Embedding K-FAC (diagonal A, register_embeddings=True) on the GPU
+    path (native G SYRK, grouped / per-layer preconditioning, multi-tensor
+    apply) against the CPU reference math."""
+    from distributed_kfac_pytorch_amd.models.transformer import TransformerLM
+
+    torch.manual_seed(0)
+    cpu = TransformerLM(ntoken=50, d_model=32, nhead=4, d_hid=32, nlayers=1, dropout=0.0)
+    gpu = copy.deepcopy(cpu).to(cuda)
+    kw = dict(factor_update_steps=1, inv_update_steps=2, compute_method=method, lr=0.1,
+              kl_clip=0.001, register_embeddings=True)
+    pc = kfac.KFACPreconditioner(cpu, **kw)
+    pg = kfac.KFACPreconditioner(gpu, **kw)
+    assert any('Embedding' in type(l).__name__ for _, l in pg._layers.values())
+    g = torch.Generator().manual_seed(2)
+    for _ in range(4):
+        tok = torch.randint(0, 50, (6, 9), generator=g)
+        for model, pre, t in ((cpu, pc, tok), (gpu, pg, tok.to(cuda))):
+            model.zero_grad()
+            out = model(t[:, :-1])
+            torch.nn.functional.cross_entropy(out.reshape(-1, 50), t[:, 1:].reshape(-1)).backward()
+            pre.step()
+        for a, b in zip(cpu.parameters(), gpu.parameters()):
+            err = (a.grad - b.grad.cpu()).abs().max() / a.grad.abs().max().clamp_min(1e-12)
+            assert err < 2e-3, float(err)
+        with torch.no_grad():
+            for a, b in zip(cpu.parameters(), gpu.parameters()):
+                a -= 0.1 * a.grad
+                b -= 0.1 * b.grad
