@@ -29,7 +29,7 @@ int64_t syrk_workspace_floats(int64_t D, int64_t splits);
 void syrk(int in_dtype, const void* x, int64_t N, int64_t K, int64_t ldx,
           bool bias, float* C, int64_t D, int64_t ldc, float alpha,
           float beta, int splits, hipStream_t s, const ConvGeom* geom,
-          float* ws);
+          float* ws, const float* ascale);
 // im2col.hip
 void im2col_nhwc(int dtype, const void* x, int64_t B, int64_t H, int64_t W,
                  int64_t C, int64_t sB, int64_t sH, int64_t sW, int kh, int kw,
@@ -187,8 +187,18 @@ int64_t syrk_out_ld(const at::Tensor& C, int64_t D) {
   return C.stride(0);
 }
 
+// ascale: optional 1-element fp32 device tensor multiplying alpha (read by
+// the kernel: no host sync for a device-side AMP loss-scale correction)
+const float* syrk_ascale(const c10::optional<at::Tensor>& ascale, const at::Tensor& C) {
+  if (!ascale.has_value() || !ascale->defined()) return nullptr;
+  TORCH_CHECK(ascale->scalar_type() == at::kFloat && ascale->numel() >= 1 &&
+                  ascale->device() == C.device(),
+              "alpha_scale must be a float32 tensor on the output's device");
+  return ascale->data_ptr<float>();
+}
+
 void syrk(const at::Tensor& x, at::Tensor& C, bool bias, double alpha,
-          double beta, int64_t splits) {
+          double beta, int64_t splits, const c10::optional<at::Tensor>& ascale) {
   check_cuda(x, "x");
   check_cuda(C, "C");
   TORCH_CHECK(x.dim() == 2, "x must be 2D [N, K]");
@@ -205,7 +215,8 @@ void syrk(const at::Tensor& x, at::Tensor& C, bool bias, double alpha,
   at::Tensor ws = syrk_ws(C, D, sp);
   kfac::syrk(dtype_tag(x), x.data_ptr(), N, K, ldx, bias,
              C.data_ptr<float>(), D, ldc, (float)alpha, (float)beta,
-             sp, cur_stream(), nullptr, ws.defined() ? ws.data_ptr<float>() : nullptr);
+             sp, cur_stream(), nullptr, ws.defined() ? ws.data_ptr<float>() : nullptr,
+             syrk_ascale(ascale, C));
 }
 
 // C[D,D] = beta*C + alpha * P^T P with P the (implicit) patch matrix of an
@@ -214,7 +225,8 @@ void syrk(const at::Tensor& x, at::Tensor& C, bool bias, double alpha,
 // inside the SYRK tile loader (K-HIP-2: no im2col buffer).
 void syrk_conv(const at::Tensor& x, at::Tensor& C, int64_t kh, int64_t kw,
                int64_t sh, int64_t sw, int64_t ph, int64_t pw, bool bias,
-               double alpha, double beta, int64_t splits) {
+               double alpha, double beta, int64_t splits,
+               const c10::optional<at::Tensor>& ascale) {
   check_cuda(x, "x");
   check_cuda(C, "C");
   TORCH_CHECK(x.dim() == 4, "x must be [B, C, H, W]");
@@ -242,7 +254,7 @@ void syrk_conv(const at::Tensor& x, at::Tensor& C, int64_t kh, int64_t kw,
   at::Tensor ws = syrk_ws(C, D, sp);
   kfac::syrk(dtype_tag(x), x.data_ptr(), N, K, /*ldx=*/K, bias, C.data_ptr<float>(), D,
              ldc, (float)alpha, (float)beta, sp, cur_stream(), &g,
-             ws.defined() ? ws.data_ptr<float>() : nullptr);
+             ws.defined() ? ws.data_ptr<float>() : nullptr, syrk_ascale(ascale, C));
 }
 
 // --------------------------------------------------------------- im2col
@@ -793,11 +805,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("triu_unpack", &triu_unpack);
   m.def("scale_copy", &scale_copy);
   m.def("syrk", &syrk, py::arg("x"), py::arg("C"), py::arg("bias"),
-        py::arg("alpha"), py::arg("beta"), py::arg("splits") = 0);
+        py::arg("alpha"), py::arg("beta"), py::arg("splits") = 0,
+        py::arg("alpha_scale") = py::none());
   m.def("syrk_default_splits", &kfac::syrk_workspace_splits);
   m.def("syrk_conv", &syrk_conv, py::arg("x"), py::arg("C"), py::arg("kh"), py::arg("kw"),
         py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("bias"),
-        py::arg("alpha"), py::arg("beta"), py::arg("splits") = 0);
+        py::arg("alpha"), py::arg("beta"), py::arg("splits") = 0,
+        py::arg("alpha_scale") = py::none());
   m.def("im2col", &im2col);
   m.def("eigen_scale", &eigen_scale);
   m.def("kl_dot", &kl_dot);

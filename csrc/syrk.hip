@@ -373,8 +373,8 @@ template <typename TIn, typename Stage>
 __global__ void __launch_bounds__(NT)
 syrk_kernel(const void* __restrict__ X, int64_t N, int64_t K, int64_t ldx,
             int bias, float* __restrict__ C, int64_t D, int64_t ldc, int packed,
-            float alpha, float beta, int T, int splits, int64_t rows_per_split,
-            int vec_ok, ConvGeom geom, float* __restrict__ ws) {
+            float alpha, const float* __restrict__ ascale, float beta, int T, int splits,
+            int64_t rows_per_split, int vec_ok, ConvGeom geom, float* __restrict__ ws) {
   using LT = typename std::conditional<std::is_same<TIn, float>::value, float,
                                        short>::type;
   constexpr int LW = std::is_same<TIn, float>::value ? LDS_W32 : LDS_W16;
@@ -453,6 +453,9 @@ syrk_kernel(const void* __restrict__ X, int64_t N, int64_t K, int64_t ldx,
 
   // ---- epilogue.  C/D layout of a 32x32 MFMA tile: col = lane & 31,
   // row = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5).
+  // ascale: optional device factor of alpha (the AMP loss-scale correction
+  // 1/s^2, read here so the host never waits for the scaler)
+  if (ascale != nullptr && splits == 1) alpha *= ascale[0];
   const bool vec_mirror = ((D & 3) == 0) && ((ldc & 3) == 0) &&
                           ((reinterpret_cast<uintptr_t>(C) & 15) == 0);
 #pragma unroll
@@ -530,7 +533,8 @@ syrk_kernel(const void* __restrict__ X, int64_t N, int64_t K, int64_t ldx,
 __global__ void __launch_bounds__(256)
 splitk_reduce_kernel(const float* __restrict__ ws, int splits, int T,
                      float* __restrict__ C, int64_t D, int64_t ldc, int packed,
-                     float alpha, float beta, int T32) {
+                     float alpha, const float* __restrict__ ascale, float beta, int T32) {
+  if (ascale != nullptr) alpha *= ascale[0];
   __shared__ float tile[32][33];
   // blockIdx.x -> (bi, bj), bi <= bj, over the T32 x T32 sub-block grid
   int bi, bj;
@@ -625,7 +629,7 @@ int64_t syrk_workspace_floats(int64_t D, int64_t splits) {
 void syrk(int in_dtype, const void* x, int64_t N, int64_t K, int64_t ldx,
           bool bias, float* C, int64_t D, int64_t ldc, float alpha,
           float beta, int splits, hipStream_t s, const ConvGeom* geom,
-          float* ws) {
+          float* ws, const float* ascale) {
   const int packed = ldc == 0 ? 1 : 0;
   if (D <= 0) return;
   const int T = (int)ceil_div(D, BM);
@@ -640,29 +644,29 @@ void syrk(int in_dtype, const void* x, int64_t N, int64_t K, int64_t ldx,
                        ((reinterpret_cast<uintptr_t>(x) & 15) == 0);
     if (geom != nullptr)
       syrk_kernel<float, PatchStaging<float>><<<grid, dim3(NT), 0, s>>>(
-          x, N, K, ldx, bias ? 1 : 0, C, D, ldc, packed, alpha, beta, T, splits,
+          x, N, K, ldx, bias ? 1 : 0, C, D, ldc, packed, alpha, ascale, beta, T, splits,
           rows_per_split, vec_ok, g, ws);
     else
       syrk_kernel<float, DenseStaging<float>><<<grid, dim3(NT), 0, s>>>(
-          x, N, K, ldx, bias ? 1 : 0, C, D, ldc, packed, alpha, beta, T, splits,
+          x, N, K, ldx, bias ? 1 : 0, C, D, ldc, packed, alpha, ascale, beta, T, splits,
           rows_per_split, vec_ok, g, ws);
   } else {
     const int vec_ok = ((ldx & 7) == 0) &&
                        ((reinterpret_cast<uintptr_t>(x) & 15) == 0);
     if (geom != nullptr)
       syrk_kernel<bf16_t, PatchStaging<bf16_t>><<<grid, dim3(NT), 0, s>>>(
-          x, N, K, ldx, bias ? 1 : 0, C, D, ldc, packed, alpha, beta, T, splits,
+          x, N, K, ldx, bias ? 1 : 0, C, D, ldc, packed, alpha, ascale, beta, T, splits,
           rows_per_split, vec_ok, g, ws);
     else
       syrk_kernel<bf16_t, DenseStaging<bf16_t>><<<grid, dim3(NT), 0, s>>>(
-          x, N, K, ldx, bias ? 1 : 0, C, D, ldc, packed, alpha, beta, T, splits,
+          x, N, K, ldx, bias ? 1 : 0, C, D, ldc, packed, alpha, ascale, beta, T, splits,
           rows_per_split, vec_ok, g, ws);
   }
   if (splits > 1) {
     const int T32 = (int)ceil_div(D, 32);
     const unsigned blocks = (unsigned)((int64_t)T32 * (T32 + 1) / 2);
     splitk_reduce_kernel<<<dim3(blocks), dim3(256), 0, s>>>(
-        ws, splits, T, C, D, ldc, packed, alpha, beta, T32);
+        ws, splits, T, C, D, ldc, packed, alpha, ascale, beta, T32);
   }
 }
 

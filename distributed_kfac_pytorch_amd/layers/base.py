@@ -88,6 +88,9 @@ class KFACBaseLayer:
         self.tdc = tdc
         self.allreduce_method = allreduce_method
         self.factor_dtype = factor_dtype
+        # a GradScaler's scale tensor lives on the device: the G unscale
+        # 1/s^2 is computed and applied there (no host sync per layer)
+        self._scaler = grad_scaler if isinstance(grad_scaler, torch.amp.GradScaler) else None
         if isinstance(grad_scaler, torch.amp.GradScaler):
             grad_scaler = grad_scaler.get_scale
         self.grad_scaler: Callable[[], float] | None = grad_scaler
@@ -365,7 +368,8 @@ class KFACBaseLayer:
             buf, key, lambda: self._materialise(which, buf, key, 1.0)))
         return True
 
-    def _packed_update(self, which: str, x: torch.Tensor, alpha: float, beta: float) -> bool:
+    def _packed_update(self, which: str, x: torch.Tensor, alpha: float, beta: float,
+                       alpha_scale: torch.Tensor | None = None) -> bool:
         """Fused EMA straight into the packed slot: slot = (beta F_avg +
         alpha X^T X) / world, F_avg the slot's reduced value."""
         home = self._homes[which]
@@ -377,7 +381,8 @@ class KFACBaseLayer:
         if which == 'A':
             self.module.accumulate_a_factor(x, sl, alpha / world, beta / world)
         else:
-            self.module.accumulate_g_factor(x, sl, alpha / world, beta / world)
+            kw = {} if alpha_scale is None else {'alpha_scale': alpha_scale}
+            self.module.accumulate_g_factor(x, sl, alpha / world, beta / world, **kw)
         # the local (not yet reduced) factor, if anything reads it first
         self._set_factor(which, AsyncTensor(
             finalize=lambda: self._materialise(which, buf, key, float(world))))
@@ -419,6 +424,17 @@ class KFACBaseLayer:
         s = float(self.grad_scaler())
         return 1.0 / (s * s)
 
+    def _g_unscale_parts(self, device: torch.device) -> tuple[float, torch.Tensor | None]:
+        """(host factor, device factor) of the G unscale: a GradScaler whose
+        scale tensor is on ``device`` gives (1, 1/s^2 computed on the
+        device); otherwise the reference's host value (one sync)."""
+        sc = self._scaler
+        t = getattr(sc, '_scale', None) if sc is not None else None
+        if isinstance(t, torch.Tensor) and t.device == device and device.type == 'cuda':
+            inv = t.float().reciprocal()
+            return 1.0, (inv * inv).reshape(1)
+        return self._g_unscale(), None
+
     def save_layer_input(self, input: list[torch.Tensor]) -> None:
         """Accumulate the A contribution of one forward input."""
         self._save_a(input[0])
@@ -441,13 +457,14 @@ class KFACBaseLayer:
     def _save_g(self, g: torch.Tensor) -> None:
         dtype = self._storage_dtype(g)
         d = self.module.g_factor_shape[0]
-        alpha = self._g_unscale()
+        alpha, dev_scale = self._g_unscale_parts(g.device)
+        kw = {} if dev_scale is None else {'alpha_scale': dev_scale}
         if self._g_batch is None:
             self._g_batch = torch.empty(d, d, dtype=dtype, device=g.device)
-            self.module.accumulate_g_factor(g, self._g_batch, alpha, 0.0)
+            self.module.accumulate_g_factor(g, self._g_batch, alpha, 0.0, **kw)
             self._g_count = 1
         else:
-            self.module.accumulate_g_factor(g, self._g_batch, alpha, 1.0)
+            self.module.accumulate_g_factor(g, self._g_batch, alpha, 1.0, **kw)
             self._g_count += 1
 
     @staticmethod
@@ -514,14 +531,17 @@ class KFACBaseLayer:
             self._save_g(g)
             self.update_g_factor(alpha)
             return
-        if self._packed_update('G', g, (1.0 - alpha) * self._g_unscale(), alpha):
+        unscale, dev_scale = self._g_unscale_parts(g.device)
+        if self._packed_update('G', g, (1.0 - alpha) * unscale, alpha, dev_scale):
             return
         if self.g_factor is None:
             d = self.module.g_factor_shape[0]
             self.g_factor = self._new_identity(d, torch.float32, g.device)
+        kw = {} if dev_scale is None else {'alpha_scale': dev_scale}
         self.module.accumulate_g_factor(
             g,
             self.g_factor,
-            (1.0 - alpha) * self._g_unscale(),
+            (1.0 - alpha) * unscale,
             alpha,
+            **kw,
         )

@@ -63,10 +63,12 @@ class EmbeddingModuleHelper(ModuleHelper):
         else:
             out.mul_(beta).add_(counts, alpha=alpha / n)
 
-    def accumulate_g_factor(self, g: torch.Tensor, out: torch.Tensor, alpha: float = 1.0, beta: float = 0.0) -> None:
+    def accumulate_g_factor(self, g: torch.Tensor, out: torch.Tensor, alpha: float = 1.0,
+                            beta: float = 0.0, alpha_scale: torch.Tensor | None = None) -> None:
         g2 = g.reshape(-1, g.shape[-1])
         n = max(g2.shape[0], 1)
-        factor_ops.cov_accumulate_(out, g2, bias=False, alpha=alpha / n, beta=beta)
+        factor_ops.cov_accumulate_(out, g2, bias=False, alpha=alpha / n, beta=beta,
+                                   alpha_scale=alpha_scale)
 
     def get_a_factor(self, a: torch.Tensor) -> torch.Tensor:
         out = torch.empty(self.module.num_embeddings, dtype=torch.float32, device=a.device)

@@ -68,6 +68,7 @@ class ModuleHelper:
         out: torch.Tensor,
         alpha: float = 1.0,
         beta: float = 0.0,
+        alpha_scale: torch.Tensor | None = None,
     ) -> None:
         raise NotImplementedError
 
@@ -207,10 +208,12 @@ class LinearModuleHelper(ModuleHelper):
         out: torch.Tensor,
         alpha: float = 1.0,
         beta: float = 0.0,
+        alpha_scale: torch.Tensor | None = None,
     ) -> None:
         g2 = g.reshape(-1, g.shape[-1])
         n = max(g2.shape[0], 1)
-        factor_ops.cov_accumulate_(out, g2, bias=False, alpha=alpha / n, beta=beta)
+        factor_ops.cov_accumulate_(out, g2, bias=False, alpha=alpha / n, beta=beta,
+                                   alpha_scale=alpha_scale)
 
     def get_a_factor(self, a: torch.Tensor) -> torch.Tensor:
         if a.is_cuda:
@@ -347,6 +350,7 @@ class Conv2dModuleHelper(ModuleHelper):
         out: torch.Tensor,
         alpha: float = 1.0,
         beta: float = 0.0,
+        alpha_scale: torch.Tensor | None = None,
     ) -> None:
         spatial = g.shape[2] * g.shape[3]
         rows = factor_ops.rows_nhwc(g)
@@ -357,6 +361,7 @@ class Conv2dModuleHelper(ModuleHelper):
             bias=False,
             alpha=alpha / (n * float(spatial) ** 2),
             beta=beta,
+            alpha_scale=alpha_scale,
         )
 
     def get_a_factor(self, a: torch.Tensor) -> torch.Tensor:

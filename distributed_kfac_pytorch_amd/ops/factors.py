@@ -31,12 +31,15 @@ def _torch_cov_accumulate_(
     bias: bool,
     alpha: float,
     beta: float,
+    alpha_scale: torch.Tensor | None = None,
 ) -> None:
     xc = x.to(out.dtype)
     if bias:
         xc = torch.cat([xc, xc.new_ones(xc.shape[0], 1)], dim=1)
     cov = xc.t() @ xc
     cov = (cov + cov.t()) / 2.0
+    if alpha_scale is not None:
+        cov = cov * alpha_scale.to(cov.dtype)
     if beta == 0.0:
         torch.mul(cov, alpha, out=out)
     else:
@@ -70,8 +73,11 @@ def cov_accumulate_(
     bias: bool = False,
     alpha: float = 1.0,
     beta: float = 0.0,
+    alpha_scale: torch.Tensor | None = None,
 ) -> torch.Tensor:
-    """In-place ``out = beta*out + alpha*Xt^T Xt`` (see module docstring)."""
+    """In-place ``out = beta*out + alpha*Xt^T Xt`` (see module docstring).
+    ``alpha_scale``: optional 1-element device tensor multiplying ``alpha``
+    (the AMP loss-scale correction, applied without a host sync)."""
     if x.dim() != 2:
         raise ValueError(f'expected a 2D input, got shape {tuple(x.shape)}')
     d = x.shape[1] + int(bias)
@@ -88,12 +94,13 @@ def cov_accumulate_(
             xin = xin.float()
         if xin.stride(1) != 1 or (xin.shape[0] > 1 and xin.stride(0) < xin.shape[1]):
             xin = xin.contiguous()
-        native().syrk(xin, out, bias, float(alpha), float(beta))
+        native().syrk(xin, out, bias, float(alpha), float(beta), 0, alpha_scale)
         return out
     if out.dim() == 1:
-        _packed_emulate_(out, lambda dense: _torch_cov_accumulate_(dense, x, bias, alpha, beta))
+        _packed_emulate_(out, lambda dense: _torch_cov_accumulate_(
+            dense, x, bias, alpha, beta, alpha_scale))
         return out
-    _torch_cov_accumulate_(out, x, bias, alpha, beta)
+    _torch_cov_accumulate_(out, x, bias, alpha, beta, alpha_scale)
     return out
 
 

@@ -176,7 +176,7 @@ def test_embedding_kfac_gpu_matches_cpu(cuda, method):
     cpu = TransformerLM(ntoken=50, d_model=32, nhead=4, d_hid=32, nlayers=1, dropout=0.0)
     gpu = copy.deepcopy(cpu).to(cuda)
     kw = dict(factor_update_steps=1, inv_update_steps=2, compute_method=method, lr=0.1,
-              kl_clip=0.001, register_embeddings=True)
+              kl_clip=0.001, register_embeddings=True, skip_layers=['self_attn'])
     pc = kfac.KFACPreconditioner(cpu, **kw)
     pg = kfac.KFACPreconditioner(gpu, **kw)
     assert any('Embedding' in type(l).__name__ for _, l in pg._layers.values())
@@ -195,3 +195,37 @@ def test_embedding_kfac_gpu_matches_cpu(cuda, method):
             for a, b in zip(cpu.parameters(), gpu.parameters()):
                 a -= 0.1 * a.grad
                 b -= 0.1 * b.grad
+
+
+def test_grad_scaler_unscale_on_device_no_sync(cuda):
+    """With a GradScaler the G contributions are unscaled by 1/s^2 on the
+    device (the scale tensor feeds the SYRK's alpha): same factors as an
+    unscaled run, and the backward hooks never synchronise the host."""
+    torch.manual_seed(0)
+    net = _net().to(cuda)
+    ref = copy.deepcopy(net)
+    scaler = torch.amp.GradScaler('cuda', init_scale=2.0 ** 12)
+    kw = dict(factor_update_steps=1, inv_update_steps=1000, lr=0.1, kl_clip=None)
+    p_ref = kfac.KFACPreconditioner(ref, **kw)
+    p_amp = kfac.KFACPreconditioner(net, grad_scaler=scaler, **kw)
+    x = torch.randn(8, 3, 14, 14, device=cuda)
+    y = torch.randint(0, 10, (8,), device=cuda)
+    for step in range(3):
+        ref.zero_grad()
+        torch.nn.functional.cross_entropy(ref(x), y).backward()
+        net.zero_grad()
+        loss = torch.nn.functional.cross_entropy(net(x), y)
+        scaled = scaler.scale(loss)
+        torch.cuda.synchronize()
+        if step > 0:  # the scaler's tensor exists after the first scale()
+            torch.cuda.set_sync_debug_mode('error')
+        try:
+            scaled.backward()
+        finally:
+            torch.cuda.set_sync_debug_mode('default')
+        p_ref._join_factor_streams()
+        p_amp._join_factor_streams()
+        for (_, a), (_, b) in zip(p_ref._layers.values(), p_amp._layers.values()):
+            torch.testing.assert_close(b.g_factor, a.g_factor, rtol=1e-5, atol=1e-7)
+        p_ref.step()
+        p_amp.step()
