@@ -29,7 +29,7 @@ int64_t syrk_workspace_floats(int64_t D, int64_t splits);
 void syrk(int in_dtype, const void* x, int64_t N, int64_t K, int64_t ldx,
           bool bias, float* C, int64_t D, int64_t ldc, float alpha,
           float beta, int splits, hipStream_t s, const ConvGeom* geom,
-          float* ws, const float* ascale);
+          float* ws, const float* ascale, bool fp32_exact);
 // im2col.hip
 void im2col_nhwc(int dtype, const void* x, int64_t B, int64_t H, int64_t W,
                  int64_t C, int64_t sB, int64_t sH, int64_t sW, int kh, int kw,
@@ -198,7 +198,8 @@ const float* syrk_ascale(const c10::optional<at::Tensor>& ascale, const at::Tens
 }
 
 void syrk(const at::Tensor& x, at::Tensor& C, bool bias, double alpha,
-          double beta, int64_t splits, const c10::optional<at::Tensor>& ascale) {
+          double beta, int64_t splits, const c10::optional<at::Tensor>& ascale,
+          bool fp32_exact) {
   check_cuda(x, "x");
   check_cuda(C, "C");
   TORCH_CHECK(x.dim() == 2, "x must be 2D [N, K]");
@@ -216,7 +217,7 @@ void syrk(const at::Tensor& x, at::Tensor& C, bool bias, double alpha,
   kfac::syrk(dtype_tag(x), x.data_ptr(), N, K, ldx, bias,
              C.data_ptr<float>(), D, ldc, (float)alpha, (float)beta,
              sp, cur_stream(), nullptr, ws.defined() ? ws.data_ptr<float>() : nullptr,
-             syrk_ascale(ascale, C));
+             syrk_ascale(ascale, C), fp32_exact);
 }
 
 // C[D,D] = beta*C + alpha * P^T P with P the (implicit) patch matrix of an
@@ -226,7 +227,7 @@ void syrk(const at::Tensor& x, at::Tensor& C, bool bias, double alpha,
 void syrk_conv(const at::Tensor& x, at::Tensor& C, int64_t kh, int64_t kw,
                int64_t sh, int64_t sw, int64_t ph, int64_t pw, bool bias,
                double alpha, double beta, int64_t splits,
-               const c10::optional<at::Tensor>& ascale) {
+               const c10::optional<at::Tensor>& ascale, bool fp32_exact) {
   check_cuda(x, "x");
   check_cuda(C, "C");
   TORCH_CHECK(x.dim() == 4, "x must be [B, C, H, W]");
@@ -254,7 +255,8 @@ void syrk_conv(const at::Tensor& x, at::Tensor& C, int64_t kh, int64_t kw,
   at::Tensor ws = syrk_ws(C, D, sp);
   kfac::syrk(dtype_tag(x), x.data_ptr(), N, K, /*ldx=*/K, bias, C.data_ptr<float>(), D,
              ldc, (float)alpha, (float)beta, sp, cur_stream(), &g,
-             ws.defined() ? ws.data_ptr<float>() : nullptr, syrk_ascale(ascale, C));
+             ws.defined() ? ws.data_ptr<float>() : nullptr, syrk_ascale(ascale, C),
+             fp32_exact);
 }
 
 // --------------------------------------------------------------- im2col
@@ -806,12 +808,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("scale_copy", &scale_copy);
   m.def("syrk", &syrk, py::arg("x"), py::arg("C"), py::arg("bias"),
         py::arg("alpha"), py::arg("beta"), py::arg("splits") = 0,
-        py::arg("alpha_scale") = py::none());
+        py::arg("alpha_scale") = py::none(), py::arg("fp32_exact") = false);
   m.def("syrk_default_splits", &kfac::syrk_workspace_splits);
   m.def("syrk_conv", &syrk_conv, py::arg("x"), py::arg("C"), py::arg("kh"), py::arg("kw"),
         py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("bias"),
         py::arg("alpha"), py::arg("beta"), py::arg("splits") = 0,
-        py::arg("alpha_scale") = py::none());
+        py::arg("alpha_scale") = py::none(), py::arg("fp32_exact") = false);
   m.def("im2col", &im2col);
   m.def("eigen_scale", &eigen_scale);
   m.def("kl_dot", &kl_dot);

@@ -351,6 +351,52 @@ struct DenseStaging : Staging<TIn> {
   }
 };
 
+// fp32 inputs on bf16 MFMA ("bf16x3"): the staged fp32 tile is split on
+// the way into LDS, x = hi + lo (hi = bf16_rn(x), lo = bf16_rn(x - hi)),
+// into two bf16 planes per operand, and x_i x_j is accumulated as
+// lo.hi + hi.lo + hi.hi -- three 32x32x16 bf16 MFMAs per fragment pair
+// instead of eight fp32 32x32x2 MFMAs of the same work, with an error of a
+// few 1e-6 relative per product (the dropped lo.lo term and the rounding
+// of lo), fp32-class for a covariance.  KFAC_SYRK_FP32=exact keeps the
+// exact-product fp32 MFMA path.
+__device__ __forceinline__ void split_f4(const float4 v, v4i16& hi, v4i16& lo) {
+  typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const f2 x01 = {v.x, v.y}, x23 = {v.z, v.w};
+  const uint32_t h01 = __builtin_bit_cast(uint32_t, __builtin_convertvector(x01, bf2));
+  const uint32_t h23 = __builtin_bit_cast(uint32_t, __builtin_convertvector(x23, bf2));
+  const f2 r01 = {v.x - __uint_as_float(h01 << 16), v.y - __uint_as_float(h01 & 0xFFFF0000u)};
+  const f2 r23 = {v.z - __uint_as_float(h23 << 16), v.w - __uint_as_float(h23 & 0xFFFF0000u)};
+  const uint32_t l01 = __builtin_bit_cast(uint32_t, __builtin_convertvector(r01, bf2));
+  const uint32_t l23 = __builtin_bit_cast(uint32_t, __builtin_convertvector(r23, bf2));
+  hi = __builtin_bit_cast(v4i16, make_uint2(h01, h23));
+  lo = __builtin_bit_cast(v4i16, make_uint2(l01, l23));
+}
+
+// Wraps an fp32 staging (dense or implicit-im2col: both hold 4 float4 per
+// operand, rows rloc + 8p, columns 4 * (t & 31)) and stores split planes:
+// operand base -> hi plane [BK][LDS_W16], lo plane right after it.
+template <typename Base>
+struct SplitStaging : Base {
+  __device__ __forceinline__ void store(short* Li, short* Lj, bool diag) {
+    const int t = threadIdx.x;
+    const int chunk = t & 31, rloc = t >> 5;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int off = (rloc + 8 * p) * LDS_W16 + chunk * 4;
+      v4i16 h, lo;
+      split_f4(this->r[0][p], h, lo);
+      *reinterpret_cast<v4i16*>(Li + off) = h;
+      *reinterpret_cast<v4i16*>(Li + BK * LDS_W16 + off) = lo;
+      if (!diag) {
+        split_f4(this->r[1][p], h, lo);
+        *reinterpret_cast<v4i16*>(Lj + off) = h;
+        *reinterpret_cast<v4i16*>(Lj + BK * LDS_W16 + off) = lo;
+      }
+    }
+  }
+};
+
 // bf16 operand fragment for a 32-wide column block `cb` at k offset `kk`:
 // lane l gets X[k = kk + 8h + j][col = cb + (l & 31)], j = 0..7, h = l >> 5,
 // via two ds_read_b64_tr_b16 (4 k-rows each).
@@ -369,18 +415,19 @@ __device__ __forceinline__ v8bf16 frag_bf16(const short* L, int cb, int kk) {
   return __builtin_bit_cast(v8bf16, c);
 }
 
-template <typename TIn, typename Stage>
+template <typename TIn, typename Stage, bool SPLIT = false>
 __global__ void __launch_bounds__(NT)
 syrk_kernel(const void* __restrict__ X, int64_t N, int64_t K, int64_t ldx,
             int bias, float* __restrict__ C, int64_t D, int64_t ldc, int packed,
             float alpha, const float* __restrict__ ascale, float beta, int T, int splits,
             int64_t rows_per_split, int vec_ok, ConvGeom geom, float* __restrict__ ws) {
-  using LT = typename std::conditional<std::is_same<TIn, float>::value, float,
-                                       short>::type;
-  constexpr int LW = std::is_same<TIn, float>::value ? LDS_W32 : LDS_W16;
-  __shared__ __attribute__((aligned(16))) LT lds[2 * BK * LW];
+  constexpr bool F32 = std::is_same<TIn, float>::value && !SPLIT;
+  using LT = typename std::conditional<F32, float, short>::type;
+  constexpr int LW = F32 ? LDS_W32 : LDS_W16;
+  constexpr int PLANES = SPLIT ? 2 : 1;  // bf16 hi (+ lo) planes per operand
+  __shared__ __attribute__((aligned(16))) LT lds[2 * PLANES * BK * LW];
   LT* Li = lds;
-  LT* Lj = lds + BK * LW;
+  LT* Lj = lds + PLANES * BK * LW;
 
   const int tile = blockIdx.x / splits;
   const int split = blockIdx.x % splits;
@@ -418,7 +465,31 @@ syrk_kernel(const void* __restrict__ X, int64_t N, int64_t K, int64_t ldx,
     if (more)
       st.load(X, ldx, n_begin + (kt + 1) * BK, n_end, K, bias, vec_ok, c0i,
               c0j, diag, geom);
-    if constexpr (std::is_same<TIn, float>::value) {
+    if constexpr (SPLIT) {
+      const short* Lih = (const short*)Li;
+      const short* Lil = Lih + BK * LW;
+      const short* Lbh = (const short*)Lb;
+      const short* Lbl = Lbh + BK * LW;
+#pragma unroll
+      for (int kk = 0; kk < BK; kk += 16) {
+        v8bf16 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          ah[q] = frag_bf16(Lih, wr * 64 + 32 * q, kk);
+          al[q] = frag_bf16(Lil, wr * 64 + 32 * q, kk);
+          bh[q] = frag_bf16(Lbh, wc * 64 + 32 * q, kk);
+          bl[q] = frag_bf16(Lbl, wc * 64 + 32 * q, kk);
+        }
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int b = 0; b < 2; ++b) {
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[a], bh[b], acc[a][b], 0, 0, 0);
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bl[b], acc[a][b], 0, 0, 0);
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bh[b], acc[a][b], 0, 0, 0);
+          }
+      }
+    } else if constexpr (F32) {
       const int h = l >> 5, r = l & 31;
 #pragma unroll
       for (int kk = 0; kk < BK; kk += 2) {
@@ -629,7 +700,7 @@ int64_t syrk_workspace_floats(int64_t D, int64_t splits) {
 void syrk(int in_dtype, const void* x, int64_t N, int64_t K, int64_t ldx,
           bool bias, float* C, int64_t D, int64_t ldc, float alpha,
           float beta, int splits, hipStream_t s, const ConvGeom* geom,
-          float* ws, const float* ascale) {
+          float* ws, const float* ascale, bool fp32_exact) {
   const int packed = ldc == 0 ? 1 : 0;
   if (D <= 0) return;
   const int T = (int)ceil_div(D, BM);
@@ -642,14 +713,18 @@ void syrk(int in_dtype, const void* x, int64_t N, int64_t K, int64_t ldx,
   if (in_dtype == kF32) {
     const int vec_ok = ((ldx & 3) == 0) &&
                        ((reinterpret_cast<uintptr_t>(x) & 15) == 0);
-    if (geom != nullptr)
-      syrk_kernel<float, PatchStaging<float>><<<grid, dim3(NT), 0, s>>>(
-          x, N, K, ldx, bias ? 1 : 0, C, D, ldc, packed, alpha, ascale, beta, T, splits,
-          rows_per_split, vec_ok, g, ws);
-    else
-      syrk_kernel<float, DenseStaging<float>><<<grid, dim3(NT), 0, s>>>(
-          x, N, K, ldx, bias ? 1 : 0, C, D, ldc, packed, alpha, ascale, beta, T, splits,
-          rows_per_split, vec_ok, g, ws);
+#define SYRK_F32(STAGE, SPLIT_)                                                     \
+  syrk_kernel<float, STAGE, SPLIT_><<<grid, dim3(NT), 0, s>>>(                      \
+      x, N, K, ldx, bias ? 1 : 0, C, D, ldc, packed, alpha, ascale, beta, T, splits, \
+      rows_per_split, vec_ok, g, ws)
+    if (geom != nullptr) {
+      if (fp32_exact) SYRK_F32(PatchStaging<float>, false);
+      else SYRK_F32(SplitStaging<PatchStaging<float>>, true);
+    } else {
+      if (fp32_exact) SYRK_F32(DenseStaging<float>, false);
+      else SYRK_F32(SplitStaging<DenseStaging<float>>, true);
+    }
+#undef SYRK_F32
   } else {
     const int vec_ok = ((ldx & 7) == 0) &&
                        ((reinterpret_cast<uintptr_t>(x) & 15) == 0);

@@ -18,6 +18,7 @@ symmetric fp32 result with the EMA / averaging weights folded into
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -44,6 +45,12 @@ def _torch_cov_accumulate_(
         torch.mul(cov, alpha, out=out)
     else:
         out.mul_(beta).add_(cov, alpha=alpha)
+
+
+def fp32_exact() -> bool:
+    """fp32 SYRK inputs: exact-product fp32 MFMA (``KFAC_SYRK_FP32=exact``)
+    instead of the default three-term bf16 split (csrc/syrk.hip)."""
+    return os.environ.get('KFAC_SYRK_FP32', 'bf16x3').lower() == 'exact'
 
 
 def packed_dim(out: torch.Tensor) -> int:
@@ -94,7 +101,7 @@ def cov_accumulate_(
             xin = xin.float()
         if xin.stride(1) != 1 or (xin.shape[0] > 1 and xin.stride(0) < xin.shape[1]):
             xin = xin.contiguous()
-        native().syrk(xin, out, bias, float(alpha), float(beta), 0, alpha_scale)
+        native().syrk(xin, out, bias, float(alpha), float(beta), 0, alpha_scale, fp32_exact())
         return out
     if out.dim() == 1:
         _packed_emulate_(out, lambda dense: _torch_cov_accumulate_(
@@ -135,7 +142,8 @@ def conv_cov_accumulate_(
     ):
         return False
     native().syrk_conv(x, out, kernel[0], kernel[1], stride[0], stride[1],
-                       padding[0], padding[1], bias, float(alpha), float(beta))
+                       padding[0], padding[1], bias, float(alpha), float(beta), 0, None,
+                       fp32_exact())
     return True
 
 

@@ -505,3 +505,19 @@ def test_syrk_conv_packed_triangle_matches_dense(cuda):
     assert factors.conv_cov_accumulate_(packed, x, (3, 3), (1, 1), (1, 1), bias=True,
                                         alpha=0.01, beta=0.5)
     torch.testing.assert_close(packed, comm_pack.triu_pack(dense), rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize('exact', [False, True])
+def test_syrk_fp32_input_modes(cuda, exact):
+    """fp32 SYRK inputs: the default bf16x3 split (three bf16 MFMAs per
+    fragment pair) stays within a few 1e-6 of the fp64 covariance; the
+    exact-product fp32 MFMA mode within fp32 accumulation error."""
+    torch.manual_seed(4)
+    lib = _native.native()
+    x = 3 * torch.randn(3000, 200, device=cuda)
+    out = torch.empty(201, 201, device=cuda)
+    lib.syrk(x, out, True, 1.0 / 3000, 0.0, 0, None, exact)
+    ref = _ref_cov(x, True) / 3000
+    rel = (out.double() - ref).abs().max().item() / ref.abs().max().item()
+    assert rel < (2e-6 if exact else 1e-5), rel
+    assert torch.equal(out, out.t())
