@@ -73,6 +73,15 @@ void apply_multi(const LayerDesc* descs, int nlayers, int64_t total_blocks,
 int gemm3_grid(int total_tiles);
 void gemm3_grouped(const GemmDesc* table, int nlayers, int total_tiles,
                    bool a_kc, bool b_kc, hipStream_t s);
+// gemm3s.hip
+int gemm3s_align();
+int gemm3s_tile_m();
+int gemm3s_tile_n();
+int gemm3s_grid(int total_tiles);
+int64_t split_blocks_for(int64_t rows, int64_t total_cols);
+void gemm3s_grouped(const Gemm3sDesc* table, int nlayers, int total_tiles, bool a_mc,
+                    bool b_mc, bool out_split, hipStream_t s);
+void split_pad_multi(const SplitDesc* table, int n, int64_t total_blocks, hipStream_t s);
 // bnact.hip
 void bn_partition(int64_t M, int C, int64_t* rows_per_block, int* nblk);
 int bn_max_c();
@@ -522,6 +531,168 @@ void kl_reduce_partials(const at::Tensor& acc, int64_t nparts, at::Tensor& out) 
                            cur_stream());
 }
 
+// ------------------------------------------------------- gemm3s (split images)
+// A split image is a contiguous bf16 tensor [2, R, L]: plane 0 = hi, 1 = lo.
+namespace {
+int64_t ru(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+void check_image(const at::Tensor& t, const char* what) {
+  check_cuda(t, what);
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16 && t.dim() == 3 && t.size(0) == 2 &&
+                  t.is_contiguous(),
+              what, ": split image must be a contiguous bf16 [2, R, L] tensor");
+  TORCH_CHECK(t.size(2) % 8 == 0 && (reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0,
+              what, ": image rows must be 16-byte multiples, base 16-byte aligned");
+}
+
+// (rows, cols) the tile loads of one operand reach: k-contig [tile rows][K],
+// m-contig [K][tile cols]
+void check_extent(const at::Tensor& img, bool mc, int64_t mn, int64_t K, int64_t tile,
+                  const char* what) {
+  const int64_t R = img.size(1), L = img.size(2);
+  const int64_t need_r = mc ? ru(K, 32) : ru(mn, tile);
+  const int64_t need_l = mc ? ru(mn, tile) : ru(K, 32);
+  TORCH_CHECK(R >= need_r && L >= need_l, what, ": image [", R, ", ", L,
+              "] too small for the tile loads (needs [", need_r, ", ", need_l, "])");
+}
+}  // namespace
+
+// Descriptor table of one grouped gemm3s launch; meta = (M, N, K) per GEMM.
+// The K padding of every image (columns / rows K..ru(K, 32)) must be zero:
+// images are allocated zeroed and only their logical part is ever written.
+std::tuple<at::Tensor, int64_t, at::Tensor> build_gemm3s_table(
+    const std::vector<at::Tensor>& As, const std::vector<at::Tensor>& Bs,
+    const std::vector<at::Tensor>& Cs, const std::vector<c10::optional<at::Tensor>>& Ss,
+    const std::vector<c10::optional<at::Tensor>>& dgs,
+    const std::vector<c10::optional<at::Tensor>>& das, const std::vector<int64_t>& meta,
+    const std::vector<double>& dampings, bool a_mc, bool b_mc, bool out_split,
+    const c10::optional<at::Tensor>& host_buf) {
+  const size_t n = As.size();
+  TORCH_CHECK(Bs.size() == n && Cs.size() == n && Ss.size() == n && dgs.size() == n &&
+                  das.size() == n && dampings.size() == n && meta.size() == 3 * n,
+              "build_gemm3s_table: list sizes");
+  const int64_t tm = kfac::gemm3s_tile_m(), tn = kfac::gemm3s_tile_n();
+  std::vector<kfac::Gemm3sDesc> host(n);
+  int tiles = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const int64_t M = meta[3 * i], N = meta[3 * i + 1], K = meta[3 * i + 2];
+    TORCH_CHECK(M > 0 && N > 0 && K > 0 && M < (1 << 30) && N < (1 << 30) && K < (1 << 30));
+    check_image(As[i], "A");
+    check_image(Bs[i], "B");
+    check_extent(As[i], a_mc, M, K, tm, "A");
+    check_extent(Bs[i], b_mc, N, K, tn, "B");
+    kfac::Gemm3sDesc d{};
+    d.A = (const uint16_t*)As[i].data_ptr();
+    d.B = (const uint16_t*)Bs[i].data_ptr();
+    d.a_plane = As[i].size(1) * As[i].size(2);
+    d.b_plane = Bs[i].size(1) * Bs[i].size(2);
+    d.lda = As[i].size(2);
+    d.ldb = Bs[i].size(2);
+    const auto& C = Cs[i];
+    if (out_split) {
+      check_image(C, "C");
+      TORCH_CHECK(C.size(1) >= M && C.size(2) >= N, "C image too small");
+      d.c_plane = C.size(1) * C.size(2);
+      d.ldc = C.size(2);
+    } else {
+      check_cuda(C, "C");
+      TORCH_CHECK(C.scalar_type() == at::kFloat && C.dim() == 2 && C.stride(1) == 1 &&
+                      C.size(0) >= M && C.size(1) >= N,
+                  "fp32 C must be [>= M, >= N] with unit column stride");
+      d.c_plane = 0;
+      d.ldc = C.stride(0);
+    }
+    d.C = C.data_ptr();
+    d.S = nullptr;
+    d.lds = 0;
+    if (Ss[i].has_value() && Ss[i]->defined()) {
+      const auto& S = *Ss[i];
+      TORCH_CHECK(S.scalar_type() == at::kFloat && S.dim() == 2 && S.stride(1) == 1 &&
+                      S.size(0) >= M && S.size(1) >= N,
+                  "S must be fp32 [>= M, >= N] with unit column stride");
+      d.S = S.data_ptr<float>();
+      d.lds = S.stride(0);
+    }
+    d.dg = d.da = nullptr;
+    if (dgs[i].has_value() && dgs[i]->defined()) {
+      TORCH_CHECK(das[i].has_value() && das[i]->defined(), "dg needs da");
+      TORCH_CHECK(dgs[i]->scalar_type() == at::kFloat && dgs[i]->is_contiguous() &&
+                      dgs[i]->numel() >= M && das[i]->scalar_type() == at::kFloat &&
+                      das[i]->is_contiguous() && das[i]->numel() >= N,
+                  "dg / da must be contiguous fp32 vectors of length >= M / N");
+      d.dg = dgs[i]->data_ptr<float>();
+      d.da = das[i]->data_ptr<float>();
+    }
+    d.damping = (float)dampings[i];
+    d.M = (int32_t)M;
+    d.N = (int32_t)N;
+    d.K = (int32_t)K;
+    d.tiles_n = (int32_t)((N + tn - 1) / tn);
+    d.tile_start = tiles;
+    tiles += (int)((M + tm - 1) / tm) * d.tiles_n;
+    host[i] = d;
+  }
+  const int64_t nbytes = (int64_t)(n * sizeof(kfac::Gemm3sDesc));
+  at::Tensor dev_t, cpu;
+  if (n > 0) std::tie(dev_t, cpu) = upload_table(host.data(), nbytes, As[0].device(), host_buf);
+  return {dev_t, tiles, cpu};
+}
+
+void gemm3s_grouped(const at::Tensor& table, int64_t n, int64_t tiles, bool a_mc, bool b_mc,
+                    bool out_split) {
+  c10::hip::HIPGuardMasqueradingAsCUDA g(table.device());
+  kfac::gemm3s_grouped((const kfac::Gemm3sDesc*)table.data_ptr(), (int)n, (int)tiles, a_mc,
+                       b_mc, out_split, cur_stream());
+}
+
+// fp32 [rows][cols] (+ extra column from a vector) -> split images
+std::tuple<at::Tensor, int64_t, at::Tensor> build_split_table(
+    const std::vector<at::Tensor>& srcs, const std::vector<c10::optional<at::Tensor>>& extras,
+    const std::vector<at::Tensor>& dsts, const c10::optional<at::Tensor>& host_buf) {
+  const size_t n = srcs.size();
+  TORCH_CHECK(extras.size() == n && dsts.size() == n, "build_split_table: list sizes");
+  std::vector<kfac::SplitDesc> host(n);
+  int64_t blocks = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const auto& x = srcs[i];
+    check_cuda(x, "src");
+    TORCH_CHECK(x.scalar_type() == at::kFloat && x.dim() == 2 && x.stride(1) == 1,
+                "split source must be fp32 2-D with unit column stride");
+    check_image(dsts[i], "dst");
+    const bool ex = extras[i].has_value() && extras[i]->defined();
+    const int64_t rows = x.size(0), cols = x.size(1), tot = cols + (ex ? 1 : 0);
+    TORCH_CHECK(dsts[i].size(1) >= rows && dsts[i].size(2) >= ru(tot, 4),
+                "split image too small for its source");
+    if (ex) {
+      TORCH_CHECK(extras[i]->scalar_type() == at::kFloat && extras[i]->is_contiguous() &&
+                      extras[i]->numel() == rows,
+                  "extra column must be a contiguous fp32 vector of length rows");
+    }
+    kfac::SplitDesc d{};
+    d.src = x.data_ptr<float>();
+    d.extra = ex ? extras[i]->data_ptr<float>() : nullptr;
+    d.dst = (uint16_t*)dsts[i].data_ptr();
+    d.lds = x.stride(0);
+    d.ldd = dsts[i].size(2);
+    d.plane = dsts[i].size(1) * dsts[i].size(2);
+    d.rows = (int32_t)rows;
+    d.cols = (int32_t)cols;
+    d.vec = (x.stride(0) % 4 == 0 && (reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0) ? 1 : 0;
+    d.block_start = blocks;
+    blocks += kfac::split_blocks_for(rows, tot);
+    host[i] = d;
+  }
+  const int64_t nbytes = (int64_t)(n * sizeof(kfac::SplitDesc));
+  at::Tensor dev_t, cpu;
+  if (n > 0) std::tie(dev_t, cpu) = upload_table(host.data(), nbytes, srcs[0].device(), host_buf);
+  return {dev_t, blocks, cpu};
+}
+
+void split_pad_multi(const at::Tensor& table, int64_t n, int64_t blocks) {
+  c10::hip::HIPGuardMasqueradingAsCUDA g(table.device());
+  kfac::split_pad_multi((const kfac::SplitDesc*)table.data_ptr(), (int)n, blocks, cur_stream());
+}
+
 void apply_multi(const at::Tensor& table, int64_t nlayers,
                  int64_t total_blocks, const c10::optional<at::Tensor>& scale) {
   c10::hip::HIPGuardMasqueradingAsCUDA g(table.device());
@@ -851,6 +1022,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("A_hls") = std::vector<c10::optional<at::Tensor>>(),
         py::arg("B_hls") = std::vector<c10::optional<at::Tensor>>());
   m.def("gemm3_grouped", &gemm3_grouped);
+  m.def("gemm3s_align", &kfac::gemm3s_align);
+  m.def("build_gemm3s_table", &build_gemm3s_table);
+  m.def("gemm3s_grouped", &gemm3s_grouped);
+  m.def("build_split_table", &build_split_table);
+  m.def("split_pad_multi", &split_pad_multi);
   // GIL released: one host thread per eigensolver lane (the sweep loop reads
   // its convergence flags back once per sweep)
   m.def("block_jacobi_eigh", &block_jacobi_eigh, py::call_guard<py::gil_scoped_release>(),

@@ -40,8 +40,8 @@
 // rows as v1.  Epilogues: eigenvalue scaling (S = dGdA, or 1/(dG dA^T +
 // damping)), then either fp32 (the preconditioned gradient P) or the split
 // image of the result (the next GEMM's operand).
-#include "../common.h"
-#include "../descs.h"
+#include "common.h"
+#include "descs.h"
 
 namespace kfac {
 
@@ -382,6 +382,8 @@ constexpr int TNS = GEMM3S_NSTAGE;
 // split images are padded to this many rows / columns (every tile config's
 // tile edge divides it, so no DMA of an edge tile leaves the image)
 int gemm3s_align() { return 256; }
+int gemm3s_tile_m() { return TBM; }
+int gemm3s_tile_n() { return TBN; }
 
 int gemm3s_grid(int total_tiles) {
   const int per = 8 * CH;

@@ -198,7 +198,7 @@ class StepGraphs:
                 return False
             damping = pre.damping
             if pre._grouped is None:
-                pre._grouped = pops.GroupedPrecondition()
+                pre._grouped = pops.make_grouped()
             # grouped MFMA GEMMs (4 launches for all layers); tables are built
             # here, outside the capture
             grouped = pre._grouped.prepare(workers, damping)
@@ -656,7 +656,7 @@ class BaseKFACPreconditioner:
         grouped = False
         if workers and workers[0].module.device.type == 'cuda':
             if self._grouped is None:
-                self._grouped = pops.GroupedPrecondition()
+                self._grouped = pops.make_grouped()
             grouped = self._grouped.run(workers, damping)
         for name, layer in ordered:
             if not grouped and self._assignment.is_grad_worker(name):

@@ -209,7 +209,7 @@ class GPTNeoXKFACPreconditioner(BaseKFACPreconditioner):
         grouped = False
         if mine and mine[0].module.device.type == 'cuda':
             if self._grouped is None:
-                self._grouped = pops.GroupedPrecondition()
+                self._grouped = pops.make_grouped()
             grouped = self._grouped.run(mine, damping)
         if not grouped:
             for layer in mine:

@@ -1,4 +1,4 @@
-// Standalone check + timing of the pre-split grouped GEMM (csrc/proto/gemm3s.hip).
+// Standalone check + timing of the pre-split grouped GEMM (csrc/gemm3s.hip).
 //   gemm3s_bench [neox|resnet|big] [a_mc b_mc out_split]
 // Builds random fp32 operands, splits them into images with split_pad_multi,
 // runs the grouped GEMM, checks layer 0 against a naive fp64-accumulated
@@ -8,7 +8,7 @@
 #include <cstdio>
 #include <cstring>
 #include <vector>
-#include "../csrc/proto/gemm3s.hip"
+#include "../csrc/gemm3s.hip"
 
 #define CK(x) do { hipError_t err_ = (x); if (err_ != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(err_), __LINE__); return 1; } } while (0)
 
