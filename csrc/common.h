@@ -57,6 +57,29 @@ __device__ __forceinline__ float wave_reduce_sum(float v) {
   return v;
 }
 
+// Full-wave float sum, returned wave-uniform, with no LDS round trip: DPP
+// quad / half-row / row mirrors leave every lane with its 16-lane row sum,
+// then the four row sums are read out with v_readlane.  ds_bpermute-based
+// __shfl_xor reductions cost an LDS round trip per step, and the compiler
+// does not overlap independent ones (sytrd col step: 65 reductions, 12 us).
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __builtin_bit_cast(
+      float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, true));
+}
+
+__device__ __forceinline__ float wave_sum_uniform(float v) {
+  v += dpp_mov<0xb1>(v);   // quad_perm [1, 0, 3, 2]
+  v += dpp_mov<0x4e>(v);   // quad_perm [2, 3, 0, 1]
+  v += dpp_mov<0x141>(v);  // row_half_mirror
+  v += dpp_mov<0x140>(v);  // row_mirror
+  const int b = __builtin_bit_cast(int, v);
+  return (__builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 0)) +
+          __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 16))) +
+         (__builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 32)) +
+          __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 48)));
+}
+
 __device__ __forceinline__ double wave_reduce_sum(double v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);

@@ -372,6 +372,14 @@ constexpr int TBM = 128, TBN = 128, TWM = 2, TWN = 2;
 constexpr int TBM = 256, TBN = 128, TWM = 4, TWN = 2;
 #elif GEMM3S_TILE == 3
 constexpr int TBM = 128, TBN = 128, TWM = 4, TWN = 2;
+#elif GEMM3S_TILE == 4
+constexpr int TBM = 256, TBN = 128, TWM = 2, TWN = 2;
+#elif GEMM3S_TILE == 5
+constexpr int TBM = 128, TBN = 128, TWM = 1, TWN = 2;
+#elif GEMM3S_TILE == 6
+constexpr int TBM = 128, TBN = 256, TWM = 2, TWN = 2;
+#elif GEMM3S_TILE == 7
+constexpr int TBM = 128, TBN = 256, TWM = 2, TWN = 4;
 #else
 constexpr int TBM = 256, TBN = 256, TWM = 2, TWN = 4;
 #endif

@@ -30,8 +30,12 @@ struct HandleState {
   at::Tensor workspace;
 };
 
+// Intentionally leaked: destroying the map at static-destruction time would
+// free device workspaces after the HIP runtime / torch allocator have been
+// torn down (heap corruption at interpreter exit).
 std::mutex g_mu;
-std::unordered_map<hipStream_t, HandleState> g_handles;
+std::unordered_map<hipStream_t, HandleState>& g_handles =
+    *new std::unordered_map<hipStream_t, HandleState>();
 
 #define ROCBLAS_OK(expr)                                                   \
   do {                                                                     \

@@ -36,7 +36,8 @@ namespace kfac {
 constexpr int SY_NB = 32;                 // panel width
 constexpr int SY_T = 256;                 // threads per block
 constexpr int SY_P1 = 2 * SY_NB + 4;      // partial stride: xn2, dW[NB], dV[NB]
-constexpr int SY_ROWS = 8;                // symv rows per workgroup (2 per wave)
+constexpr int SY_ROWS = 32;               // symv rows per workgroup
+constexpr int SY_RPW = SY_ROWS / (SY_T / 64);  // symv rows per wave (8)
 constexpr int SY_MAXN = 8192;             // v staged in LDS (32 KiB)
 constexpr int SY_MAXCH = SY_MAXN / SY_T;  // col-step chunks
 constexpr int SY_MAXROWBLK = SY_MAXN / SY_ROWS;
@@ -49,8 +50,31 @@ int sytrd_maxrowblk() { return SY_MAXROWBLK; }
 
 namespace {
 
+// The descriptor's pointers are generic; every access goes through these
+// global-address-space views so the compiler emits global_* (not flat_*)
+// memory instructions: flat loads also count against lgkmcnt, so each LDS
+// wait would drain every outstanding matrix load.
+#define GLOBAL __attribute__((address_space(1)))
+struct GView {
+  GLOBAL float* A;
+  GLOBAL float* Wt;
+  GLOBAL float* d;
+  GLOBAL float* e;
+  GLOBAL float* tau;
+  GLOBAL float* part1;
+  GLOBAL float* part2;
+  GLOBAL float* sc;
+  int n;
+};
+
+__device__ __forceinline__ GView gview(const SytrdDesc& s) {
+  return {(GLOBAL float*)s.A,     (GLOBAL float*)s.Wt,    (GLOBAL float*)s.d,
+          (GLOBAL float*)s.e,     (GLOBAL float*)s.tau,   (GLOBAL float*)s.part1,
+          (GLOBAL float*)s.part2, (GLOBAL float*)s.sc,    s.n};
+}
+
 __device__ __forceinline__ float block_sum(float v, float* red) {
-  v = wave_reduce_sum(v);
+  v = wave_sum_uniform(v);
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   __syncthreads();
   if (l == 0) red[w] = v;
@@ -65,7 +89,7 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 // column k-1 (panel end).  grid (chunks, batch).
 __global__ void __launch_bounds__(SY_T) sytrd_col_kernel(
     const SytrdDesc* __restrict__ descs, int k, int p, int fin_only) {
-  const SytrdDesc D = descs[blockIdx.y];
+  const GView D = gview(descs[blockIdx.y]);
   const int n = D.n;
   if (k >= n) return;
   const int r0 = k + blockIdx.x * SY_T;
@@ -76,38 +100,61 @@ __global__ void __launch_bounds__(SY_T) sytrd_col_kernel(
   __shared__ float red[SY_T / 64];
   __shared__ float cW[SY_NB], cV[SY_NB];
   __shared__ float wred[SY_T / 64][SY_P1];
+  const bool fin = i > 0;  // column k-1 to finalise
 
-  float alpha2 = 0.f, sprev = 0.f;
-  if (i > 0) {
+  // ---- every global load of this thread first, all in flight together
+  // (rows p + j < n and Wt rows j < NB are always in bounds; values past the
+  // panel's current width are masked after the load, never multiplied in)
+  float s2 = 0.f;
+  if (fin) {
     // partial w.v of column k-1: rows k..n-1 in blocks of SY_ROWS
     const int cnt = (int)ceil_div(n - k, SY_ROWS);
-    float s = 0.f;
-    for (int t = threadIdx.x; t < cnt; t += SY_T) s += D.part2[t];
-    s = block_sum(s, red);
-    const float tp = D.sc[0];
-    sprev = D.sc[1];
-    alpha2 = -0.5f * tp * s;
+    for (int t = threadIdx.x; t < cnt; t += SY_T) s2 += D.part2[t];
   }
-  if ((int)threadIdx.x < i && !fin_only) {
-    const int j = threadIdx.x;
-    float w = D.Wt[(int64_t)j * n + k];
-    float v;
-    if (j == i - 1) {
-      w += alpha2;  // finalised W[k, i-1]; V_{i-1}[k] = 1 (implicit)
-      v = 1.f;
-    } else {
-      v = D.A[(int64_t)(p + j) * n + k];
+  const float tp = fin ? D.sc[0] : 0.f;
+  const float sprev = fin ? D.sc[1] : 0.f;
+  const int j0 = threadIdx.x;
+  float cw_raw = 0.f, cv_raw = 0.f;
+  if (j0 < i && !fin_only) {
+    cw_raw = D.Wt[(int64_t)j0 * n + k];
+    cv_raw = j0 == i - 1 ? 1.f : D.A[(int64_t)(p + j0) * n + k];  // V_{i-1}[k] = 1
+  }
+  float vraw = 0.f, wraw = 0.f;
+  if (act && fin) {
+    vraw = r == k ? 1.f : D.A[(int64_t)(k - 1) * n + r];
+    wraw = D.Wt[(int64_t)(i - 1) * n + r];
+  }
+  float vj[SY_NB], wj[SY_NB];
+  float a = 0.f;
+#pragma unroll
+  for (int j = 0; j < SY_NB; ++j) {
+    vj[j] = 0.f;
+    wj[j] = 0.f;
+  }
+  if (act && !fin_only) {
+    a = D.A[(int64_t)k * n + r];
+#pragma unroll
+    for (int j = 0; j < SY_NB; ++j) {
+      const int pj = p + j < n ? p + j : n - 1;
+      vj[j] = D.A[(int64_t)pj * n + r];
+      wj[j] = D.Wt[(int64_t)j * n + r];
     }
-    cW[j] = w;
-    cV[j] = v;
+  }
+
+  float alpha2 = 0.f;
+  if (fin) alpha2 = -0.5f * tp * block_sum(s2, red);
+  if (j0 < SY_NB && !fin_only) {
+    // finalised W[k, i-1] gets the -tau/2 (w.v) v correction
+    cW[j0] = j0 < i ? cw_raw + (j0 == i - 1 ? alpha2 : 0.f) : 0.f;
+    cV[j0] = j0 < i ? cv_raw : 0.f;
   }
   __syncthreads();
 
   float vprev = 0.f, wprev = 0.f;
-  if (act && i > 0) {
-    vprev = (r == k) ? 1.f : D.A[(int64_t)(k - 1) * n + r] * sprev;
+  if (act && fin) {
+    vprev = r == k ? 1.f : vraw * sprev;
     if (r > k) D.A[(int64_t)(k - 1) * n + r] = vprev;
-    wprev = D.Wt[(int64_t)(i - 1) * n + r] + alpha2 * vprev;
+    wprev = wraw + alpha2 * vprev;
     // W[k, i-1] is finalised by every block on its own (cW above) and not
     // read again by later col / symv steps: writing it here would race with
     // those reads.  The panel-end trailing update does read it (r = q).
@@ -115,22 +162,17 @@ __global__ void __launch_bounds__(SY_T) sytrd_col_kernel(
   }
   if (fin_only) return;
 
-  float vj[SY_NB], wj[SY_NB];
-  float a = 0.f;
   if (act) {
-    a = D.A[(int64_t)k * n + r];
 #pragma unroll
     for (int j = 0; j < SY_NB; ++j) {
-      if (j < i) {
-        if (j == i - 1) {
-          vj[j] = vprev;
-          wj[j] = wprev;
-        } else {
-          vj[j] = D.A[(int64_t)(p + j) * n + r];
-          wj[j] = D.Wt[(int64_t)j * n + r];
-        }
-        a -= vj[j] * cW[j] + wj[j] * cV[j];
+      if (j == i - 1) {
+        vj[j] = vprev;
+        wj[j] = wprev;
+      } else if (j >= i) {
+        vj[j] = 0.f;
+        wj[j] = 0.f;
       }
+      a -= vj[j] * cW[j] + wj[j] * cV[j];
     }
     D.A[(int64_t)k * n + r] = a;
     if (r == k) D.d[k] = a;
@@ -139,17 +181,16 @@ __global__ void __launch_bounds__(SY_T) sytrd_col_kernel(
   // partial sums over the reflector tail x = a[k+2:n]
   const float x = (act && r >= k + 2) ? a : 0.f;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-  float s0 = wave_reduce_sum(x * x);
+  float s0 = wave_sum_uniform(x * x);
   if (l == 0) wred[w][0] = s0;
 #pragma unroll
   for (int j = 0; j < SY_NB; ++j) {
-    if (j < i) {
-      float sw = wave_reduce_sum(x != 0.f ? wj[j] * x : 0.f);
-      float sv = wave_reduce_sum(x != 0.f ? vj[j] * x : 0.f);
-      if (l == 0) {
-        wred[w][1 + j] = sw;
-        wred[w][1 + SY_NB + j] = sv;
-      }
+    // independent reductions (j >= i contribute zeros and are not stored)
+    const float sw = wave_sum_uniform(wj[j] * x);
+    const float sv = wave_sum_uniform(vj[j] * x);
+    if (l == 0 && j < i) {
+      wred[w][1 + j] = sw;
+      wred[w][1 + SY_NB + j] = sv;
     }
   }
   __syncthreads();
@@ -167,31 +208,62 @@ __global__ void __launch_bounds__(SY_T) sytrd_col_kernel(
 // symv step for column k (k <= n-2).  grid (row blocks, batch).
 __global__ void __launch_bounds__(SY_T) sytrd_symv_kernel(
     const SytrdDesc* __restrict__ descs, int k, int p) {
-  const SytrdDesc D = descs[blockIdx.y];
+  const GView D = gview(descs[blockIdx.y]);
   const int n = D.n;
   if (k >= n - 1) return;
   const int row0 = k + 1 + blockIdx.x * SY_ROWS;
   if (row0 >= n) return;
   const int i = k - p;
-  const int m = n - k - 1;  // length of v (rows/cols k+1..n-1)
-  __shared__ float sv[SY_MAXN];
+  __shared__ __attribute__((aligned(16))) float sv[SY_MAXN];
+  __shared__ float ptmp[SY_MAXCH * SY_P1];
   __shared__ float tot[SY_P1];
-  __shared__ float t1[SY_NB], t2[SY_NB];
+  __shared__ float t1[SY_NB], t2[SY_NB], wk1[SY_NB], ak1[SY_NB];
   __shared__ float red[SY_T / 64];
   __shared__ float scal[3];
 
-  // reduce the col-step partials of column k
+  // ---- every global load except the matrix rows first, in flight together:
+  // the col-step partials of column k, the pivot, the panel entries of
+  // column k+1, the raw reflector row (scaled later: v = [1, scale * a]),
+  // and this wave's rows' panel entries for the V t1 + W t2 correction
   const int nch = (int)ceil_div(n - k, SY_T);
-  for (int t = threadIdx.x; t < 1 + 2 * SY_NB; t += SY_T) {
-    const int j = (t - 1) % SY_NB;
-    if (t > 0 && j >= i) continue;
+  for (int t = threadIdx.x; t < nch * SY_P1; t += SY_T) ptmp[t] = D.part1[t];
+  const float alpha = D.A[(int64_t)k * n + k + 1];
+  if ((int)threadIdx.x < i) {
+    const int j = threadIdx.x;
+    wk1[j] = D.Wt[(int64_t)j * n + k + 1];
+    ak1[j] = D.A[(int64_t)(p + j) * n + k + 1];
+  }
+  // v staged 16-B aligned: column col at sv[col - base], base = (k+1)
+  // rounded down to 4; columns <= k+1 hold 0 (column k+1, v = 1, is added
+  // per row from A[r][k+1] below)
+  const int base = (k + 1) & ~3;
+  const int span = n - base;
+  const GLOBAL float* arow = D.A + (int64_t)k * n;
+  for (int c = threadIdx.x; c < span; c += SY_T) {
+    const int col = base + c;
+    sv[c] = col <= k + 1 ? 0.f : arow[col];
+  }
+  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int rw = row0 + wv * SY_RPW;
+  float pv[SY_RPW], pk1[SY_RPW];
+#pragma unroll
+  for (int h = 0; h < SY_RPW; ++h) {
+    const int r = rw + h < n ? rw + h : n - 1;
+    pv[h] = 0.f;
+    if (l < i) pv[h] = D.A[(int64_t)(p + l) * n + r];
+    else if (l >= 32 && l - 32 < i) pv[h] = D.Wt[(int64_t)(l - 32) * n + r];
+    pk1[h] = D.A[(int64_t)r * n + k + 1];
+  }
+  __syncthreads();
+
+  // reduce the partials, then the reflector scalars
+  for (int t = threadIdx.x; t < SY_P1; t += SY_T) {
     float s = 0.f;
-    for (int c = 0; c < nch; ++c) s += D.part1[(int64_t)c * SY_P1 + t];
+    for (int c = 0; c < nch; ++c) s += ptmp[c * SY_P1 + t];
     tot[t] = s;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    const float alpha = D.A[(int64_t)k * n + k + 1];
     const float xn2 = tot[0];
     float tau_k, beta, scale;
     if (xn2 == 0.f) {
@@ -216,38 +288,52 @@ __global__ void __launch_bounds__(SY_T) sytrd_symv_kernel(
   const float tau_k = scal[0], scale = scal[1];
   if ((int)threadIdx.x < i) {
     const int j = threadIdx.x;
-    t1[j] = D.Wt[(int64_t)j * n + k + 1] + scale * tot[1 + j];
-    t2[j] = D.A[(int64_t)(p + j) * n + k + 1] + scale * tot[1 + SY_NB + j];
+    t1[j] = wk1[j] + scale * tot[1 + j];
+    t2[j] = ak1[j] + scale * tot[1 + SY_NB + j];
   }
-  const float* arow = D.A + (int64_t)k * n + k + 1;
-  for (int c = threadIdx.x; c < m; c += SY_T) sv[c] = c == 0 ? 1.f : arow[c] * scale;
   __syncthreads();
 
-  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+  // SY_RPW rows per wave, all in flight together: one 16-B load per lane
+  // per row per 256 columns (rows are 16-B aligned when n % 4 == 0)
+  float acc[SY_RPW];
+#pragma unroll
+  for (int h = 0; h < SY_RPW; ++h) acc[h] = 0.f;
+  if ((n & 3) == 0) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    const int nq = span >> 2;
+    for (int q = l; q < nq; q += 64) {
+      const f4 vv = *reinterpret_cast<const f4*>(sv + 4 * q);
+#pragma unroll
+      for (int h = 0; h < SY_RPW; ++h) {
+        if (rw + h < n) {
+          const f4 a4 = *(const GLOBAL f4*)(D.A + (int64_t)(rw + h) * n + base + 4 * q);
+          acc[h] += (a4.x * vv.x + a4.y * vv.y) + (a4.z * vv.z + a4.w * vv.w);
+        }
+      }
+    }
+  } else {
+    for (int c = l; c < span; c += 64) {
+      const float vc = sv[c];
+#pragma unroll
+      for (int h = 0; h < SY_RPW; ++h)
+        if (rw + h < n) acc[h] += D.A[(int64_t)(rw + h) * n + base + c] * vc;
+    }
+  }
   float pd = 0.f;
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int r = row0 + wv * 2 + h;
+  for (int h = 0; h < SY_RPW; ++h) {
+    const int r = rw + h;
     if (r >= n) break;
-    const float* ar = D.A + (int64_t)r * n + k + 1;
-    float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
-    int c = l;
-    for (; c + 192 < m; c += 256) {
-      acc0 += ar[c] * sv[c];
-      acc1 += ar[c + 64] * sv[c + 64];
-      acc2 += ar[c + 128] * sv[c + 128];
-      acc3 += ar[c + 192] * sv[c + 192];
-    }
-    for (; c < m; c += 64) acc0 += ar[c] * sv[c];
-    float y = wave_reduce_sum((acc0 + acc1) + (acc2 + acc3));
-    float corr = 0.f;
-    if (l < i) corr = D.A[(int64_t)(p + l) * n + r] * t1[l];
-    else if (l >= 32 && l - 32 < i) corr = D.Wt[(int64_t)(l - 32) * n + r] * t2[l - 32];
-    corr = wave_reduce_sum(corr);
+    // y = A22 v with v = [1, scale * a]
+    const float y = pk1[h] + scale * wave_sum_uniform(acc[h]);
+    float cp = 0.f;
+    if (l < i) cp = pv[h] * t1[l];
+    else if (l >= 32 && l - 32 < i) cp = pv[h] * t2[l - 32];
+    const float corr = wave_sum_uniform(cp);
     const float wr = tau_k * (y - corr);
     if (l == 0) {
       D.Wt[(int64_t)i * n + r] = wr;
-      pd += wr * sv[r - k - 1];
+      pd += wr * (r == k + 1 ? 1.f : scale * sv[r - base]);
     }
   }
   pd = block_sum(pd, red);
@@ -258,7 +344,7 @@ __global__ void __launch_bounds__(SY_T) sytrd_symv_kernel(
 // grid (col tiles, row tiles, batch), 64x64 tiles, 16x16 threads x 4x4.
 __global__ void __launch_bounds__(SY_T) sytrd_syr2k_kernel(
     const SytrdDesc* __restrict__ descs, int q, int p) {
-  const SytrdDesc D = descs[blockIdx.z];
+  const GView D = gview(descs[blockIdx.z]);
   const int n = D.n;
   if (q >= n) return;
   const int r0 = q + blockIdx.y * 64, c0 = q + blockIdx.x * 64;

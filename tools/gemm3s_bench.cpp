@@ -1,5 +1,7 @@
 // Standalone check + timing of the pre-split grouped GEMM (csrc/gemm3s.hip).
-//   gemm3s_bench [neox|resnet|big] [a_mc b_mc out_split]
+//   gemm3s_bench [neox|resnet|big] [a_mc b_mc out_split [a|g]]
+// The last argument picks the inner dimension: K = a (the T1 / T4 tables,
+// 2 g a^2 flops per layer) or K = g (T2 / T3, 2 g^2 a).
 // Builds random fp32 operands, splits them into images with split_pad_multi,
 // runs the grouped GEMM, checks layer 0 against a naive fp64-accumulated
 // GEMM and reports the time of the GEMM launch alone.
@@ -44,6 +46,7 @@ int main(int argc, char** argv) {
   const bool amc = argc > 2 ? atoi(argv[2]) != 0 : false;
   const bool bmc = argc > 3 ? atoi(argv[3]) != 0 : true;
   const bool osplit = argc > 4 ? atoi(argv[4]) != 0 : false;
+  const bool kg = argc > 5 && argv[5][0] == 'g';
   std::vector<L> layers;
   if (!strcmp(set, "neox")) {
     layers = {{2304, 769, 12}, {768, 769, 12}, {3072, 769, 12}, {768, 3073, 12}};
@@ -66,7 +69,7 @@ int main(int argc, char** argv) {
   int64_t c0_plane = 0, c0_ld = 0;
   for (auto& l : layers) {
     for (int c = 0; c < l.cnt; ++c) {
-      const int M = l.g, N = l.a, K = l.a;
+      const int M = l.g, N = l.a, K = kg ? l.g : l.a;
       const int ar = amc ? K : M, ac = amc ? M : K;   // XA shape
       const int br = bmc ? K : N, bc = bmc ? N : K;   // XB shape
       float *XA, *XB;
@@ -163,9 +166,9 @@ int main(int argc, char** argv) {
   float sms;
   CK(hipEventElapsedTime(&sms, s, e));
   sms /= iters;
-  printf("{\"set\": \"%s\", \"a_mc\": %d, \"b_mc\": %d, \"out_split\": %d, \"tiles\": %d, \"ms\": %.4f, "
+  printf("{\"set\": \"%s\", \"k\": \"%s\", \"a_mc\": %d, \"b_mc\": %d, \"out_split\": %d, \"tiles\": %d, \"ms\": %.4f, "
          "\"fp32_tflops\": %.1f, \"bf16_mfma_tflops\": %.1f, \"rel_err\": %.3e, \"split_all_ms\": %.4f}\n",
-         set, amc ? 1 : 0, bmc ? 1 : 0, osplit ? 1 : 0, tiles, ms, flops / ms / 1e9,
+         set, kg ? "g" : "a", amc ? 1 : 0, bmc ? 1 : 0, osplit ? 1 : 0, tiles, ms, flops / ms / 1e9,
          3 * flops / ms / 1e9, maxerr / maxref, sms);
   return (maxerr / maxref < 5e-5) ? 0 : 2;
 }
