@@ -36,7 +36,7 @@ namespace kfac {
 constexpr int SY_NB = 32;                 // panel width
 constexpr int SY_T = 256;                 // threads per block
 constexpr int SY_P1 = 2 * SY_NB + 4;      // partial stride: xn2, dW[NB], dV[NB]
-constexpr int SY_ROWS = 32;               // symv rows per workgroup
+constexpr int SY_ROWS = 16;               // symv rows per workgroup
 constexpr int SY_RPW = SY_ROWS / (SY_T / 64);  // symv rows per wave (8)
 constexpr int SY_MAXN = 8192;             // v staged in LDS (32 KiB)
 constexpr int SY_MAXCH = SY_MAXN / SY_T;  // col-step chunks

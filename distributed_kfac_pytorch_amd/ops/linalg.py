@@ -10,9 +10,13 @@ sizes (all K-FAC factors a rank owns) with as little latency as possible:
   tridiagonalisation (csrc/sytrd.hip): every such factor of every bucket
   advances one column per launch pair in ONE chain, then each matrix is
   finished by rocSOLVER ``stedc`` + ``ormtr`` (the second half of syevd) on
-  the lanes below.  Opt-in: on MI355X it is correct to ~1e-6 but not yet
-  faster than syevd on the ResNet-50 factor mix (526 vs 397 ms; the stedc +
-  ormtr tail alone sums to ~330 ms, profiles/eigh_sytrd_mi355x.jsonl);
+  the lanes below.  Opt-in: on MI355X it is correct to ~1e-6 and its
+  3 x 4608 chain now matches rocSOLVER's (164 vs 165 ms,
+  profiles/sytrd_per_column_trace_r2.txt), but the refresh of the real
+  step-100 ResNet-50 factors is still slower than the default (375 ms at
+  n >= 4000, 411 ms at n >= 2000, vs 353 ms for warm-tested syevd:
+  profiles/refresh_probe_r2_sytrd_tier.jsonl) -- the chain pays ~16 us of
+  kernel-boundary floor per column, and its stedc + ormtr tail follows it;
 * other n: direct batched rocSOLVER ``syevd`` calls from C++
   (csrc/solver.cpp) which, unlike ``torch.linalg.eigh``, never synchronise
   the host;

@@ -99,6 +99,9 @@ def main() -> None:
     ap.add_argument('--steps', type=int, default=100)
     ap.add_argument('--per-bucket', type=int, default=1)
     ap.add_argument('--modes', type=int, default=4)
+    ap.add_argument('--mode-list', default='',
+                    help='comma-separated modes, e.g. auto_warm,sytrd4000_warm (overrides --modes)')
+    ap.add_argument('--reps', type=int, default=2)
     args = ap.parse_args()
     mats, warm = snapshot(args.steps)
     sizes = defaultdict(int)
@@ -109,12 +112,20 @@ def main() -> None:
     def run(mode: str):  # type: ignore[no-untyped-def]
         os.environ['KFAC_EIGH_BLOCK'] = '0' if mode == 'syevd' else '1'
         os.environ['KFAC_EIGH_LARGE'] = 'block' if mode.startswith('block') else 'syevd'
-        w = list(warm) if mode in ('block_warm', 'auto_warm') else None
+        if mode.startswith('sytrd'):
+            # native batched tridiagonalisation for n >= the number in the name
+            os.environ['KFAC_EIGH'] = 'sytrd'
+            os.environ['KFAC_SYTRD_MIN_N'] = mode[len('sytrd'):].split('_')[0]
+        else:
+            os.environ['KFAC_EIGH'] = 'auto'
+        w = list(warm) if mode.endswith('_warm') else None
         linalg.last_stats.clear()
         return linalg.eigh_many([m.clone() for m in mats], w)
 
-    for mode in ('syevd', 'auto_warm', 'block_warm', 'block_cold')[: args.modes]:
-        ms, res = timed(lambda: run(mode))
+    modes = (args.mode_list.split(',') if args.mode_list else
+             ['syevd', 'auto_warm', 'block_warm', 'block_cold'][: args.modes])
+    for mode in modes:
+        ms, res = timed(lambda: run(mode), args.reps)
         rec = {'mode': mode, 'mix_ms': round(ms, 1)}
         if linalg.last_stats.get('accepted'):
             rec['accepted'] = len(linalg.last_stats['accepted']) // 3
