@@ -284,6 +284,7 @@ def run(args: argparse.Namespace, use_kfac: bool, rank: int, world: int,
     out = {'seconds': elapsed, 'ms_per_step': elapsed / args.steps * 1e3,
            'kind_ms': {k: round(v, 3) for k, v in by_kind.items() if v > 0.0},
            'kind_counts': {k: kinds.count(k) for k in ('plain', 'factor', 'inverse')},
+           'inverse_ms_each': [round(t, 1) for t, kk in zip(per_step, kinds) if kk == 'inverse'],
            'align_steps': align}
     if precond is not None:
         # period-averaged step time at the reference cadence: one refresh,
@@ -393,7 +394,7 @@ def main() -> None:
     if base is not None and 'step_graphs' in base:
         line['sgd_step_graphs'] = base['step_graphs']
     for k in ('phase_ms_per_step', 'phase_counts', 'kfac_layers', 'step_graphs',
-              'kfac_memory_mb', 'kfac_steps_end', 'align_steps'):
+              'kfac_memory_mb', 'kfac_steps_end', 'align_steps', 'inverse_ms_each'):
         if k in res:
             line[k] = res[k]
     if rank == 0:
