@@ -45,6 +45,7 @@ import distributed_kfac_pytorch_amd as kfac  # noqa: E402
 from distributed_kfac_pytorch_amd import tracing  # noqa: E402
 from distributed_kfac_pytorch_amd.graphs import GraphedTrainStep  # noqa: E402
 from distributed_kfac_pytorch_amd.models.resnet import get_model  # noqa: E402
+from distributed_kfac_pytorch_amd.ops.cast import enable_fused_weight_cast  # noqa: E402
 
 # The reference publishes no number.  Measured on MI355X: the
 # upstream kfac_pytorch package, same config and harness (shipped MIOpen
@@ -89,6 +90,9 @@ def parse_args() -> argparse.Namespace:
                         '(distributed_kfac_pytorch_amd.graphs.GraphedTrainStep; '
                         'single-rank jobs only, second-order update steps stay '
                         'eager); 0: every step eager')
+    p.add_argument('--fused-weight-cast', type=int, default=1,
+                   help='1: autocast weight casts by fused multi-tensor launches '
+                        '(ops/cast.py; same values), 0: autocast per-weight casts')
     p.add_argument('--cudnn-benchmark', type=int, default=0,
                    help='1: MIOpen find in every process (noisy); 0: immediate mode '
                         'with the shipped tuning db (miopen_db/)')
@@ -153,6 +157,10 @@ def run(args: argparse.Namespace, use_kfac: bool, rank: int, world: int,
     cl = not args.no_channels_last
     if cl:
         model = model.to(memory_format=torch.channels_last)
+    if args.fused_weight_cast and args.impl == 'native' and not args.fp32:
+        # bf16 weight copies / fp32 weight gradients by multi-tensor launches
+        # instead of autocast's per-weight casts (ops/cast.py)
+        enable_fused_weight_cast(model)
     if world > 1:
         model = torch.nn.parallel.DistributedDataParallel(
             model, device_ids=[dev.index], gradient_as_bucket_view=True,
@@ -368,6 +376,7 @@ def main() -> None:
                 'kl_clip': args.kfac_kl_clip,
             },
             'channels_last': not args.no_channels_last,
+            'fused_weight_cast': bool(args.fused_weight_cast) and not args.fp32,
         },
         'timing': (
             'period-averaged: the timed window of exactly `steps` steps starts on '

@@ -82,6 +82,9 @@ int64_t split_blocks_for(int64_t rows, int64_t total_cols);
 void gemm3s_grouped(const Gemm3sDesc* table, int nlayers, int total_tiles, bool a_mc,
                     bool b_mc, bool out_split, hipStream_t s);
 void split_pad_multi(const SplitDesc* table, int n, int64_t total_blocks, hipStream_t s);
+// cast.hip
+int64_t cast_blocks_for(int64_t n);
+void cast_multi(const CastDesc* table, int n, int64_t total_blocks, bool to_bf16, hipStream_t s);
 // bnact.hip
 void bn_partition(int64_t M, int C, int64_t* rows_per_block, int* nblk);
 int bn_max_c();
@@ -688,6 +691,49 @@ std::tuple<at::Tensor, int64_t, at::Tensor> build_split_table(
   return {dev_t, blocks, cpu};
 }
 
+// Multi-tensor cast table: srcs[i] (fp32 or bf16) -> dsts[i] (the other
+// dtype), element by element in STORAGE order, so the pairs must share shape
+// and strides and be dense (non-overlapping, no gaps).
+std::tuple<at::Tensor, int64_t, at::Tensor> build_cast_table(
+    const std::vector<at::Tensor>& srcs, const std::vector<at::Tensor>& dsts,
+    const c10::optional<at::Tensor>& host_buf) {
+  const size_t n = srcs.size();
+  TORCH_CHECK(dsts.size() == n, "build_cast_table: list sizes");
+  std::vector<kfac::CastDesc> host(n);
+  int64_t blocks = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const auto& x = srcs[i];
+    const auto& y = dsts[i];
+    check_cuda(x, "src");
+    check_cuda(y, "dst");
+    const bool f2b = x.scalar_type() == at::kFloat && y.scalar_type() == at::kBFloat16;
+    const bool b2f = x.scalar_type() == at::kBFloat16 && y.scalar_type() == at::kFloat;
+    TORCH_CHECK(f2b || b2f, "cast pairs must be fp32 -> bf16 or bf16 -> fp32");
+    TORCH_CHECK(i == 0 || (f2b == (srcs[0].scalar_type() == at::kFloat)),
+                "one cast direction per table");
+    TORCH_CHECK(x.sizes() == y.sizes() && x.strides() == y.strides(),
+                "cast pair ", i, ": shapes and strides must match");
+    TORCH_CHECK(x.is_non_overlapping_and_dense(), "cast pair ", i, ": source must be dense");
+    kfac::CastDesc d{};
+    d.src = x.data_ptr();
+    d.dst = y.data_ptr();
+    d.n = x.numel();
+    d.vec = ((reinterpret_cast<uintptr_t>(x.data_ptr()) | reinterpret_cast<uintptr_t>(y.data_ptr())) & 15) == 0;
+    d.block_start = blocks;
+    blocks += kfac::cast_blocks_for(d.n);
+    host[i] = d;
+  }
+  const int64_t nbytes = (int64_t)(n * sizeof(kfac::CastDesc));
+  at::Tensor dev_t, cpu;
+  if (n > 0) std::tie(dev_t, cpu) = upload_table(host.data(), nbytes, srcs[0].device(), host_buf);
+  return {dev_t, blocks, cpu};
+}
+
+void cast_multi(const at::Tensor& table, int64_t n, int64_t blocks, bool to_bf16) {
+  c10::hip::HIPGuardMasqueradingAsCUDA g(table.device());
+  kfac::cast_multi((const kfac::CastDesc*)table.data_ptr(), (int)n, blocks, to_bf16, cur_stream());
+}
+
 void split_pad_multi(const at::Tensor& table, int64_t n, int64_t blocks) {
   c10::hip::HIPGuardMasqueradingAsCUDA g(table.device());
   kfac::split_pad_multi((const kfac::SplitDesc*)table.data_ptr(), (int)n, blocks, cur_stream());
@@ -1027,6 +1073,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm3s_grouped", &gemm3s_grouped);
   m.def("build_split_table", &build_split_table);
   m.def("split_pad_multi", &split_pad_multi);
+  m.def("build_cast_table", &build_cast_table);
+  m.def("cast_multi", &cast_multi);
   // GIL released: one host thread per eigensolver lane (the sweep loop reads
   // its convergence flags back once per sweep)
   m.def("block_jacobi_eigh", &block_jacobi_eigh, py::call_guard<py::gil_scoped_release>(),

@@ -96,4 +96,15 @@ struct SytrdDesc {
   int32_t n, pad;
 };
 
+// multi-tensor dtype cast (csrc/cast.hip): one tensor's storage-order
+// elements, fp32 <-> bf16
+struct CastDesc {
+  const void* src;
+  void* dst;
+  int64_t n;            // elements
+  int64_t block_start;  // first block of this tensor in the launch
+  int32_t vec;          // both pointers 16-B aligned: 8-element vector path
+  int32_t pad;
+};
+
 }  // namespace kfac
