@@ -680,8 +680,12 @@ int64_t syrk_workspace_splits(int64_t N, int64_t D) {
   const int64_t max_by_ws = (int64_t(32) << 20) / (4 * tiles * BM * BM);
   if (splits > max_by_ws) splits = max_by_ws;
   // the reduction re-reads every slab once: beyond ~64 slabs per tile it
-  // costs more than the extra parallelism gains (PMC: profiles/pmc)
-  if (splits > 64) splits = 64;
+  // costs more than the extra parallelism gains (PMC: profiles/pmc) --
+  // unless the triangle has so few tiles that 64 splits cannot fill the
+  // chip (the 147-wide A factor of ResNet's 7x7 stem: 3 tiles x 64 splits
+  // = 192 blocks for 401k rows)
+  const int64_t cap = tiles * 64 >= target_blocks / 2 ? 64 : ceil_div(target_blocks, tiles);
+  if (splits > cap) splits = cap;
   if (splits < 2) splits = 1;
   return splits;
 }
