@@ -56,7 +56,8 @@ constexpr int SK = 32;              // k per stage
 #endif
 constexpr int CH = GEMM3S_CH;
 constexpr int GM = GEMM3S_GM;
-// diagnostic builds only (tools/gemm3s_bench.cpp): 1 = no DMA, 3 = no MFMA
+// diagnostic builds only (tools/gemm3s_bench.cpp): 1 = no DMA, 3 = no MFMA,
+// 4 = no epilogue stores
 #ifndef GEMM3S_DIAG
 #define GEMM3S_DIAG 0
 #endif
@@ -281,31 +282,101 @@ gemm3s_kernel(const Gemm3sDesc* __restrict__ descs, int nlayers, int total_tiles
   }
 
   // epilogue: C/D layout col = lane & 31, row = (e & 3) + 8 (e >> 2) + 4 (lane >> 5)
+  if constexpr (GEMM3S_DIAG == 4) {
+    // diagnostic: no epilogue stores (every accumulator stays live through
+    // a store the compiler cannot prove dead)
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) t += acc[i][j][e];
+    if (d.M < 0) ((GLOBAL float*)d.C)[threadIdx.x] = t;
+    return;
+  }
+  // Shuffled through LDS, 32 rows of the wave tile at a time: the MFMA
+  // layout gives each lane one column, so direct stores are 2-B (split) or
+  // 4-B writes per lane; re-read row-contiguous, every lane stores 8
+  // consecutive outputs with 16-B writes (diagnostic build 4 measured the
+  // direct-store epilogue at ~35 % of the ResNet-50 chain).  Out-of-range
+  // outputs are exactly 0 (zero-padded operands); split images take them
+  // into their zero padding, the fp32 output is bounds-checked.
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int CPR = WTN / 8;           // 8-wide chunks per row
+  constexpr int RPI = 64 / CPR;          // rows per read instruction
+  static_assert(NW * 32 * WTN * 4 <= NSTAGE * STAGE * 2, "epilogue tile must fit the stage LDS");
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();  // every wave is done with the stage buffers
+  float* region = reinterpret_cast<float*>(lds) + w * (32 * WTN);
+  const int mw0 = m0 + wr * WTM, nw0 = n0 + wc * WTN;
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
-      const int n = n0 + wc * (BN / WN) + j * 32 + (l & 31);
-      if (n >= d.N) continue;
-      const float dan = d.da != nullptr ? ((const GLOBAL float*)d.da)[n] : 0.f;
+      const int cl = j * 32 + (l & 31);
+      const int n = nw0 + cl;
+      const bool nok = n < d.N;
+      const float dan = (d.da != nullptr && nok) ? ((const GLOBAL float*)d.da)[n] : 0.f;
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        const int m = m0 + wr * (BM / WM) + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (l >> 5);
-        if (m >= d.M) continue;
+        const int rl = (e & 3) + 8 * (e >> 2) + 4 * (l >> 5);
+        const int m = mw0 + i * 32 + rl;
         float v = acc[i][j][e];
-        if (d.S != nullptr) v *= ((const GLOBAL float*)d.S)[(int64_t)m * d.lds + n];
-        else if (d.dg != nullptr) v = v / (((const GLOBAL float*)d.dg)[m] * dan + d.damping);
-        if constexpr (OUT_SPLIT) {
+        if (!nok || m >= d.M) {
+          v = 0.f;
+        } else if (d.S != nullptr) {
+          v *= ((const GLOBAL float*)d.S)[(int64_t)m * d.lds + n];
+        } else if (d.dg != nullptr) {
+          v = v / (((const GLOBAL float*)d.dg)[m] * dan + d.damping);
+        }
+        region[rl * WTN + cl] = v;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int t = 0; t < 32 / RPI; ++t) {
+      const int rl = t * RPI + l / CPR;
+      const int c8 = (l % CPR) * 8;
+      typedef float f4 __attribute__((ext_vector_type(4)));
+      const f4 x0 = *reinterpret_cast<const f4*>(region + rl * WTN + c8);
+      const f4 x1 = *reinterpret_cast<const f4*>(region + rl * WTN + c8 + 4);
+      const int m = mw0 + i * 32 + rl;
+      const int n = nw0 + c8;
+      const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+      if constexpr (OUT_SPLIT) {
+        // whole chunk, padding included (the image rows / columns are
+        // padded to 256 and these values are 0 there)
+        typedef unsigned short u8v __attribute__((ext_vector_type(8)));
+        u8v hv, lv;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
           uint16_t h, lo;
-          split1(v, h, lo);
-          GLOBAL uint16_t* c = (GLOBAL uint16_t*)d.C;
-          c[(int64_t)m * d.ldc + n] = h;
-          c[d.c_plane + (int64_t)m * d.ldc + n] = lo;
-        } else {
-          ((GLOBAL float*)d.C)[(int64_t)m * d.ldc + n] = v;
+          split1(v[q], h, lo);
+          hv[q] = h;
+          lv[q] = lo;
+        }
+        GLOBAL uint16_t* c = (GLOBAL uint16_t*)d.C + (int64_t)m * d.ldc + n;
+        *(GLOBAL u8v*)c = hv;
+        *(GLOBAL u8v*)(c + d.c_plane) = lv;
+      } else {
+        if (m < d.M) {
+          GLOBAL float* c = (GLOBAL float*)d.C + (int64_t)m * d.ldc + n;
+          if (n + 8 <= d.N && (d.ldc & 3) == 0 && (reinterpret_cast<uintptr_t>(d.C) & 15) == 0) {
+            *(GLOBAL f4*)c = x0;
+            *(GLOBAL f4*)(c + 4) = x1;
+          } else {
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+              if (n + q < d.N) c[q] = v[q];
+          }
         }
       }
     }
+    // the next row group overwrites the region: this wave's reads are done
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
   }
 }
 

@@ -5,7 +5,7 @@ cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
 : > gpurun_out/g3s_sweep.jsonl
 for v in ${VARIANTS:-t0 t4_s2 t4_s3 t5_s2 t5_s3 t6_s2 t6_s3 t7_s2 t7_s3}; do
  for cfg in "0 1 1 a" "1 1 1 g" "0 1 1 g" "0 0 0 a"; do
-  out=$(timeout -k 5 60 ./benchbin/g3s_$v ${SET:-resnet} $cfg) || { echo "fail $v $cfg: $out"; exit 1; }
+  out=$(timeout -k 5 60 ./benchbin/g3s_$v ${SET:-resnet} $cfg); rc=$?; if [ $rc != 0 ] && [ $rc != 2 ]; then echo "fail $v $cfg: $out"; exit 1; fi
   echo "{\"v\": \"$v\", ${out#\{}" >> gpurun_out/g3s_sweep.jsonl
  done
 done
