@@ -90,6 +90,8 @@ def parse_args() -> argparse.Namespace:
                         '(distributed_kfac_pytorch_amd.graphs.GraphedTrainStep; '
                         'single-rank jobs only, second-order update steps stay '
                         'eager); 0: every step eager')
+    p.add_argument('--sgd-impl', default='fused', choices=['fused', 'foreach'],
+                   help='torch.optim.SGD implementation (same math)')
     p.add_argument('--fused-weight-cast', type=int, default=1,
                    help='1: autocast weight casts by fused multi-tensor launches '
                         '(ops/cast.py; same values), 0: autocast per-weight casts')
@@ -166,9 +168,11 @@ def run(args: argparse.Namespace, use_kfac: bool, rank: int, world: int,
             model, device_ids=[dev.index], gradient_as_bucket_view=True,
         )
     lr = args.lr * world
-    # foreach: multi-tensor SGD step and a multi-tensor zero_grad
+    # fused: one-pass SGD kernels (weight decay + momentum + update per
+    # element); foreach: PyTorch's multi-pass multi-tensor SGD
+    kw = {'fused': True} if args.sgd_impl == 'fused' else {'foreach': True}
     opt = torch.optim.SGD(model.parameters(), lr=lr, momentum=0.9,
-                          weight_decay=5e-5, foreach=True)
+                          weight_decay=5e-5, **kw)
     precond = None
     impl = kfac
     if use_kfac and args.impl == 'reference':
@@ -377,6 +381,7 @@ def main() -> None:
             },
             'channels_last': not args.no_channels_last,
             'fused_weight_cast': bool(args.fused_weight_cast) and not args.fp32,
+            'sgd_impl': args.sgd_impl,
         },
         'timing': (
             'period-averaged: the timed window of exactly `steps` steps starts on '
