@@ -19,6 +19,9 @@
 // update, num_batches_tracked += 1.
 #include "common.h"
 
+#include <cstdlib>
+#include <cstring>
+
 namespace kfac {
 
 namespace {
@@ -317,6 +320,291 @@ __global__ void __launch_bounds__(BN_T) bn_bwd_apply_kernel(
   }
 }
 
+// ---- small-activation path (ResNet stages 2-4): two launches per
+// direction instead of three.  Partial sums are taken per (channel slice,
+// row chunk) block with few row chunks, so every apply block can reduce the
+// partials of its own channel slice (P x 64 x 2 floats) and finalise those
+// channels itself; the separate finalize launch -- ~5 us of fixed cost per
+// BN layer and direction on MI355X -- disappears.  Blocks in row chunk 0
+// publish the statistics (forward) or dweight / dbias (backward).
+constexpr int SB_CW = 64;    // channels per slice
+constexpr int SB_PMAX = 64;  // row chunks of the partial pass
+
+__device__ __host__ __forceinline__ int sliced_cw(int C) { return C < SB_CW ? C : SB_CW; }
+
+template <int MODE>
+__global__ void __launch_bounds__(BN_T) bn_partial_sliced_kernel(
+    const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
+    const uint16_t* __restrict__ y, const float* __restrict__ mean, int relu,
+    int64_t M, int C, int64_t rows_per_chunk, float* __restrict__ part) {
+  __shared__ float sh[2][BN_T * 8];  // [RT][cw] per statistic
+  const int cw = sliced_cw(C);
+  const int tpc = cw / 8, RT = BN_T / tpc;
+  const int tc = threadIdx.x % tpc, rt = threadIdx.x / tpc;
+  const int c0 = blockIdx.x * cw + tc * 8;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_chunk;
+  const int64_t r1 = r0 + rows_per_chunk < M ? r0 + rows_per_chunk : M;
+  float s0[8] = {}, s1[8] = {}, mu[8] = {};
+  if (MODE == 1) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) mu[i] = mean[c0 + i];
+  }
+  constexpr int U = 4;
+  for (int64_t rb = r0 + rt; rb < r1; rb += U * (int64_t)RT) {
+    float a[U][8], g[U][8], o[U][8];
+    bool ok[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t r = rb + (int64_t)u * RT;
+      ok[u] = r < r1;
+      if (ok[u]) {
+        const int64_t off = r * C + c0;
+        load8(x + off, a[u]);
+        if (MODE == 1) {
+          load8(dy + off, g[u]);
+          if (relu) load8(y + off, o[u]);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (!ok[u]) continue;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        if (MODE == 0) {
+          s0[i] += a[u][i];
+          s1[i] += a[u][i] * a[u][i];
+        } else {
+          const float gi = (!relu || o[u][i] > 0.f) ? g[u][i] : 0.f;
+          s0[i] += gi;
+          s1[i] += gi * (a[u][i] - mu[i]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    sh[0][rt * cw + tc * 8 + i] = s0[i];
+    sh[1][rt * cw + tc * 8 + i] = s1[i];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < cw; c += BN_T) {
+    float a = 0.f, b = 0.f;
+    for (int q = 0; q < RT; ++q) {
+      a += sh[0][q * cw + c];
+      b += sh[1][q * cw + c];
+    }
+    const int ch = blockIdx.x * cw + c;
+    part[((int64_t)blockIdx.y * 2) * C + ch] = a;
+    part[((int64_t)blockIdx.y * 2 + 1) * C + ch] = b;
+  }
+}
+
+// fp64 sums of the P partials of this block's channel slice -> tot[2][cw]
+__device__ __forceinline__ void sliced_reduce(const float* __restrict__ part, int P, int C, int cw,
+                                              double (*tot)[SB_CW]) {
+  __shared__ double ra[BN_T], rb[BN_T];
+  const int nsub = BN_T / cw;
+  const int ch = threadIdx.x % cw, sub = threadIdx.x / cw;
+  const int c = blockIdx.x * cw + ch;
+  double sa = 0.0, sb = 0.0;
+  for (int p = sub; p < P; p += nsub) {
+    sa += (double)part[((int64_t)p * 2) * C + c];
+    sb += (double)part[((int64_t)p * 2 + 1) * C + c];
+  }
+  ra[threadIdx.x] = sa;
+  rb[threadIdx.x] = sb;
+  __syncthreads();
+  if ((int)threadIdx.x < cw) {
+    double a = 0.0, b = 0.0;
+    for (int q = 0; q < nsub; ++q) {
+      a += ra[q * cw + threadIdx.x];
+      b += rb[q * cw + threadIdx.x];
+    }
+    tot[0][threadIdx.x] = a;
+    tot[1][threadIdx.x] = b;
+  }
+}
+
+// forward: finalise this slice's channels, then x*scale + shift (+ res) (ReLU)
+__global__ void __launch_bounds__(BN_T) bn_fwd_apply_sliced_kernel(
+    const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
+    const float* __restrict__ part, int P, int64_t M, int C, int64_t rows_per_chunk,
+    const float* __restrict__ weight, const float* __restrict__ bias,
+    float* __restrict__ running_mean, float* __restrict__ running_var,
+    int64_t* __restrict__ num_batches, float momentum, float eps, int relu,
+    float* __restrict__ stats, uint16_t* __restrict__ y) {
+  __shared__ double tot[2][SB_CW];
+  __shared__ float ssc[SB_CW], ssf[SB_CW];
+  const int cw = sliced_cw(C);
+  sliced_reduce(part, P, C, cw, tot);
+  __syncthreads();
+  if ((int)threadIdx.x < cw) {
+    const int c = blockIdx.x * cw + threadIdx.x;
+    const double mean = tot[0][threadIdx.x] / (double)M;
+    double var = tot[1][threadIdx.x] / (double)M - mean * mean;
+    if (var < 0.0) var = 0.0;
+    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+    const float w = weight ? weight[c] : 1.f;
+    const float b = bias ? bias[c] : 0.f;
+    const float scale = w * invstd;
+    const float shift = b - (float)mean * scale;
+    ssc[threadIdx.x] = scale;
+    ssf[threadIdx.x] = shift;
+    if (blockIdx.y == 0) {
+      stats[c] = (float)mean;
+      stats[C + c] = invstd;
+      stats[2 * C + c] = scale;
+      stats[3 * C + c] = shift;
+      if (running_mean) {
+        running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
+        const double unb = M > 1 ? var * (double)M / (double)(M - 1) : var;
+        running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unb;
+      }
+      if (num_batches && c == 0) num_batches[0] += 1;
+    }
+  }
+  __syncthreads();
+  const int tpc = cw / 8, RT = BN_T / tpc;
+  const int tc = threadIdx.x % tpc, rt = threadIdx.x / tpc;
+  const int c0 = blockIdx.x * cw + tc * 8;
+  float sc[8], sf[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    sc[i] = ssc[tc * 8 + i];
+    sf[i] = ssf[tc * 8 + i];
+  }
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_chunk;
+  const int64_t r1 = r0 + rows_per_chunk < M ? r0 + rows_per_chunk : M;
+  for (int64_t rb = r0 + rt; rb < r1; rb += 4 * (int64_t)RT) {
+    float a[4][8], r[4][8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t row = rb + (int64_t)u * RT;
+      if (row < r1) {
+        load8(x + row * C + c0, a[u]);
+        if (res) load8(res + row * C + c0, r[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t row = rb + (int64_t)u * RT;
+      if (row >= r1) continue;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float o = a[u][i] * sc[i] + sf[i];
+        if (res) o += r[u][i];
+        a[u][i] = relu ? fmaxf(o, 0.f) : o;
+      }
+      store8(y + row * C + c0, a[u]);
+    }
+  }
+}
+
+// backward: finalise dweight / dbias and the dx coefficients of this slice,
+// then dx = k1*dz + k2 + k3*(x - mean) (and d residual = dz)
+__global__ void __launch_bounds__(BN_T) bn_bwd_apply_sliced_kernel(
+    const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
+    const uint16_t* __restrict__ y, const float* __restrict__ part, int P, int64_t M, int C,
+    int64_t rows_per_chunk, const float* __restrict__ weight, const float* __restrict__ stats,
+    float* __restrict__ dweight, float* __restrict__ dbias, int relu,
+    uint16_t* __restrict__ dx, uint16_t* __restrict__ dres) {
+  __shared__ double tot[2][SB_CW];
+  __shared__ float sk1[SB_CW], sk2[SB_CW], sk3[SB_CW], smu[SB_CW];
+  const int cw = sliced_cw(C);
+  sliced_reduce(part, P, C, cw, tot);
+  __syncthreads();
+  if ((int)threadIdx.x < cw) {
+    const int c = blockIdx.x * cw + threadIdx.x;
+    const double sdz = tot[0][threadIdx.x], sdzx = tot[1][threadIdx.x];
+    const double invstd = stats[C + c];
+    const double w = weight ? weight[c] : 1.0;
+    if (blockIdx.y == 0) {
+      if (dweight) dweight[c] = (float)(sdzx * invstd);
+      if (dbias) dbias[c] = (float)sdz;
+    }
+    const double k1 = w * invstd;
+    sk1[threadIdx.x] = (float)k1;
+    sk2[threadIdx.x] = (float)(-k1 * sdz / (double)M);
+    sk3[threadIdx.x] = (float)(-k1 * invstd * invstd * sdzx / (double)M);
+    smu[threadIdx.x] = stats[c];
+  }
+  __syncthreads();
+  const int tpc = cw / 8, RT = BN_T / tpc;
+  const int tc = threadIdx.x % tpc, rt = threadIdx.x / tpc;
+  const int c0 = blockIdx.x * cw + tc * 8;
+  float mu[8], k1[8], k2[8], k3[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    mu[i] = smu[tc * 8 + i];
+    k1[i] = sk1[tc * 8 + i];
+    k2[i] = sk2[tc * 8 + i];
+    k3[i] = sk3[tc * 8 + i];
+  }
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_chunk;
+  const int64_t r1 = r0 + rows_per_chunk < M ? r0 + rows_per_chunk : M;
+  for (int64_t rb = r0 + rt; rb < r1; rb += 4 * (int64_t)RT) {
+    float a[4][8], g[4][8], o[4][8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t row = rb + (int64_t)u * RT;
+      if (row < r1) {
+        const int64_t off = row * C + c0;
+        load8(x + off, a[u]);
+        load8(dy + off, g[u]);
+        if (relu) load8(y + off, o[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t row = rb + (int64_t)u * RT;
+      if (row >= r1) continue;
+      const int64_t off = row * C + c0;
+      if (relu) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) g[u][i] = o[u][i] > 0.f ? g[u][i] : 0.f;
+      }
+      if (dres) store8(dres + off, g[u]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a[u][i] = k1[i] * g[u][i] + k2[i] + k3[i] * (a[u][i] - mu[i]);
+      store8(dx + off, a[u]);
+    }
+  }
+}
+
+// (partial chunks, apply chunks, rows per partial chunk, rows per apply
+// chunk) of the sliced path, or false when the activation is large enough
+// for the three-launch path (whose ~400 partial blocks keep HBM busy)
+bool sliced_plan(int64_t M, int C, int* P, int* Q, int64_t* rp, int64_t* rq) {
+  // KFAC_BN_SLICED=0: always the three-launch path (A/B runs)
+  static const bool enabled = [] {
+    const char* e = std::getenv("KFAC_BN_SLICED");
+    return e == nullptr || std::strcmp(e, "0") != 0;
+  }();
+  if (!enabled) return false;
+  // channel slices of 8 * 2^k channels (whole thread columns per block)
+  if (C > SB_CW ? C % SB_CW != 0 : (C != 8 && C != 16 && C != 32 && C != 64)) return false;
+  const int cw = sliced_cw(C);
+  const int nsl = C / cw;
+  const int rt = BN_T / (cw / 8);
+  int p = (int)ceil_div(256, nsl);
+  if (p > SB_PMAX) p = SB_PMAX;
+  if (p < 1) p = 1;
+  const int64_t rows = ceil_div(M, (int64_t)p);
+  // > 32 rows per thread, or too few partial blocks to stream the tensor:
+  // the three-launch path
+  if (rows > 32 * (int64_t)rt || (int64_t)nsl * ceil_div(M, rows) < 128) return false;
+  int q = (int)ceil_div(512, nsl);
+  const int64_t qmax = ceil_div(M, 4 * (int64_t)rt);  // >= one unrolled pass per thread
+  if (q > qmax) q = (int)qmax;
+  if (q < 1) q = 1;
+  *P = (int)ceil_div(M, rows);
+  *rp = rows;
+  *rq = ceil_div(M, (int64_t)q);
+  *Q = (int)ceil_div(M, *rq);
+  return true;
+}
+
 int apply_grid(int64_t M, int C) {
   const int rpi = BN_T / (C / 8);
   int64_t g = ceil_div(M, 4 * (int64_t)rpi);
@@ -327,6 +615,13 @@ int apply_grid(int64_t M, int C) {
 
 // rows per partial block and block count for [M, C]
 void bn_partition(int64_t M, int C, int64_t* rows_per_block, int* nblk) {
+  int P, Q;
+  int64_t rp, rq;
+  if (sliced_plan(M, C, &P, &Q, &rp, &rq)) {
+    *rows_per_block = rp;
+    *nblk = P;
+    return;
+  }
   // ~400 workgroups on the big activations (8 / 4 rows of loads in flight
   // per thread keep HBM busy; few partials keep the finalize short), at
   // least 32 rows and one full unrolled iteration per workgroup
@@ -344,6 +639,19 @@ void bn_forward(const uint16_t* x, const uint16_t* res, const float* weight,
                 const float* bias, float* running_mean, float* running_var,
                 int64_t* num_batches, float momentum, float eps, int relu, int64_t M,
                 int C, float* part, float* stats, uint16_t* y, hipStream_t s) {
+  {
+    int P, Q;
+    int64_t rp, rq;
+    if (sliced_plan(M, C, &P, &Q, &rp, &rq)) {
+      const unsigned nsl = (unsigned)(C / sliced_cw(C));
+      hipLaunchKernelGGL(bn_partial_sliced_kernel<0>, dim3(nsl, (unsigned)P), dim3(BN_T), 0, s,
+                         x, nullptr, nullptr, nullptr, 0, M, C, rp, part);
+      hipLaunchKernelGGL(bn_fwd_apply_sliced_kernel, dim3(nsl, (unsigned)Q), dim3(BN_T), 0, s,
+                         x, res, part, P, M, C, rq, weight, bias, running_mean, running_var,
+                         num_batches, momentum, eps, relu, stats, y);
+      return;
+    }
+  }
   int64_t rpb;
   int nblk;
   bn_partition(M, C, &rpb, &nblk);
@@ -362,6 +670,20 @@ void bn_backward(const uint16_t* x, const uint16_t* dy, const uint16_t* y,
                  const float* weight, const float* stats, int relu, int64_t M, int C,
                  float* part, float* coef, float* dweight, float* dbias, uint16_t* dx,
                  uint16_t* dres, hipStream_t s) {
+  {
+    int P, Q;
+    int64_t rp, rq;
+    if (sliced_plan(M, C, &P, &Q, &rp, &rq)) {
+      const unsigned nsl = (unsigned)(C / sliced_cw(C));
+      hipLaunchKernelGGL(bn_partial_sliced_kernel<1>, dim3(nsl, (unsigned)P), dim3(BN_T), 0, s,
+                         x, dy, y, stats, relu, M, C, rp, part);
+      hipLaunchKernelGGL(bn_bwd_apply_sliced_kernel, dim3(nsl, (unsigned)Q), dim3(BN_T), 0, s,
+                         x, dy, y, part, P, M, C, rq, weight, stats, dweight, dbias, relu, dx,
+                         dres);
+      (void)coef;  // the sliced path keeps its coefficients in LDS
+      return;
+    }
+  }
   int64_t rpb;
   int nblk;
   bn_partition(M, C, &rpb, &nblk);

@@ -15,8 +15,12 @@ def _cl(t: torch.Tensor) -> torch.Tensor:
     return t.contiguous(memory_format=torch.channels_last)
 
 
+# small activations take the two-launch sliced path (csrc/bnact.hip
+# sliced_plan), large ones the three-launch path: both are covered
 @pytest.mark.parametrize('shape', [(4, 64, 14, 14), (2, 256, 7, 9), (3, 2048, 4, 4),
-                                   (2, 16, 5, 5), (2, 24, 3, 3), (8, 128, 28, 28)])
+                                   (2, 16, 5, 5), (2, 24, 3, 3), (8, 128, 28, 28),
+                                   (32, 512, 7, 7), (32, 1024, 14, 14), (8, 64, 56, 56),
+                                   (16, 32, 32, 32)])
 @pytest.mark.parametrize('relu', [True, False])
 @pytest.mark.parametrize('residual', [True, False])
 def test_bn_act_matches_reference(cuda, shape, relu, residual):
