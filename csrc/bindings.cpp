@@ -101,6 +101,7 @@ void bn_backward(const uint16_t* x, const uint16_t* dy, const uint16_t* y,
 // solver.cpp
 std::vector<at::Tensor> rocsolver_eigh(at::Tensor A, int64_t algo,
                                        int64_t max_sweeps, double tol);
+int64_t sytrd_panel();
 int64_t sytrd_max_n();
 int64_t spd_lds_max_n();
 // eigh_block_host.cpp
@@ -110,6 +111,9 @@ std::vector<at::Tensor> block_jacobi_eigh(at::Tensor A, c10::optional<at::Tensor
 at::Tensor spd_inverse(at::Tensor F, double damping);
 std::vector<at::Tensor> spd_inverse_blocked(at::Tensor F, double damping);
 std::vector<at::Tensor> sytrd_reduce(std::vector<at::Tensor> stacks);
+std::vector<at::Tensor> tridiag_stedc(at::Tensor d, at::Tensor e);
+std::vector<at::Tensor> sytrd_begin(std::vector<at::Tensor> stacks);
+void sytrd_advance(at::Tensor descs, std::vector<int64_t> sizes, int64_t k0, int64_t k1);
 std::vector<at::Tensor> tridiag_eigvecs(at::Tensor A, at::Tensor d, at::Tensor e,
                                         at::Tensor tau);
 
@@ -1048,6 +1052,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("apply_multi", &apply_multi);
   // GIL released: several host threads can each drive rocSOLVER on their
   // own stream (rocSOLVER's syevd blocks its calling thread internally)
+  m.def("sytrd_nb", &sytrd_panel);
   m.def("sytrd_max_n", &sytrd_max_n);
   m.def("bn_act_supported", &bn_act_supported);
   m.def("bn_act_forward", &bn_act_forward);
@@ -1058,6 +1063,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("spd_inverse_blocked", &spd_inverse_blocked, py::call_guard<py::gil_scoped_release>());
   m.def("sytrd_reduce", &sytrd_reduce, py::call_guard<py::gil_scoped_release>());
   m.def("tridiag_eigvecs", &tridiag_eigvecs, py::call_guard<py::gil_scoped_release>());
+  m.def("tridiag_stedc", &tridiag_stedc, py::call_guard<py::gil_scoped_release>());
+  m.def("sytrd_begin", &sytrd_begin, py::call_guard<py::gil_scoped_release>());
+  m.def("sytrd_advance", &sytrd_advance, py::call_guard<py::gil_scoped_release>());
   m.def("rocsolver_eigh", &rocsolver_eigh, py::call_guard<py::gil_scoped_release>(),
         py::arg("A"), py::arg("algo") = 0,
         py::arg("max_sweeps") = 100, py::arg("tol") = 1e-7);

@@ -132,20 +132,22 @@ int sytrd_maxch();
 int sytrd_maxrowblk();
 void sytrd_batched(const SytrdDesc* descs_dev, const int* ns, int batch,
                    hipStream_t stream);
+void sytrd_batched_range(const SytrdDesc* descs_dev, const int* ns, int batch,
+                         int k_begin, int k_end, hipStream_t stream);
 }  // namespace kfac
 
 int64_t sytrd_max_n() { return kfac::sytrd_max_n(); }
+int64_t sytrd_panel() { return kfac::sytrd_nb(); }
 
 // stacks: list of [cnt, n, n] fp32 contiguous symmetric (overwritten).
-// Returns [d, e, tau] per stack, each [cnt, n] fp32.
-std::vector<at::Tensor> sytrd_reduce(std::vector<at::Tensor> stacks) {
+// Descriptor table + workspace for a reduction of `stacks`; returns
+// [descs (device bytes), work, d0, e0, tau0, d1, ...].  Nothing launched.
+static std::vector<at::Tensor> sytrd_setup(std::vector<at::Tensor>& stacks,
+                                           std::vector<int>& ns) {
   TORCH_CHECK(!stacks.empty());
   const auto opts = stacks[0].options();
-  c10::hip::HIPGuardMasqueradingAsCUDA g(stacks[0].device());
-  hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
   const int NB = kfac::sytrd_nb(), P1 = kfac::sytrd_p1();
   std::vector<at::Tensor> outs;
-  std::vector<int> ns;
   int64_t scratch = 0;
   for (auto& A : stacks) {
     TORCH_CHECK(A.is_cuda() && A.scalar_type() == at::kFloat && A.dim() == 3 &&
@@ -192,9 +194,41 @@ std::vector<at::Tensor> sytrd_reduce(std::vector<at::Tensor> stacks) {
   }
   auto dev = at::empty({host.numel()}, opts.dtype(at::kByte));
   dev.copy_(host, /*non_blocking=*/true);
-  kfac::sytrd_batched(reinterpret_cast<const kfac::SytrdDesc*>(dev.data_ptr()),
-                      ns.data(), batch, s);
+  outs.insert(outs.begin(), work);
+  outs.insert(outs.begin(), dev);
   return outs;
+}
+
+std::vector<at::Tensor> sytrd_reduce(std::vector<at::Tensor> stacks) {
+  c10::hip::HIPGuardMasqueradingAsCUDA g(stacks.at(0).device());
+  hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+  std::vector<int> ns;
+  auto all = sytrd_setup(stacks, ns);
+  if (ns.empty()) return {};
+  kfac::sytrd_batched(reinterpret_cast<const kfac::SytrdDesc*>(all[0].data_ptr()),
+                      ns.data(), (int)ns.size(), s);
+  return std::vector<at::Tensor>(all.begin() + 2, all.end());
+}
+
+// Segmented form: sytrd_begin() builds the state (kept alive by the caller
+// in the returned tensors: [descs, work, d0, e0, tau0, ...]); each
+// sytrd_advance(state, sizes, k0, k1) issues the panels covering columns
+// [k0, k1) (k0 a multiple of the panel width) on the current stream.  After
+// advancing past n, every matrix of size <= n is fully reduced.
+std::vector<at::Tensor> sytrd_begin(std::vector<at::Tensor> stacks) {
+  c10::hip::HIPGuardMasqueradingAsCUDA g(stacks.at(0).device());
+  std::vector<int> ns;
+  return sytrd_setup(stacks, ns);
+}
+
+void sytrd_advance(at::Tensor descs, std::vector<int64_t> sizes, int64_t k0, int64_t k1) {
+  TORCH_CHECK(k0 % kfac::sytrd_nb() == 0, "segments start on panel boundaries");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(descs.device());
+  hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+  std::vector<int> ns(sizes.begin(), sizes.end());
+  TORCH_CHECK((int64_t)ns.size() * (int64_t)sizeof(kfac::SytrdDesc) == descs.numel());
+  kfac::sytrd_batched_range(reinterpret_cast<const kfac::SytrdDesc*>(descs.data_ptr()),
+                            ns.data(), (int)ns.size(), (int)k0, (int)k1, s);
 }
 
 // A: [cnt, n, n] reduced by sytrd_reduce (reflectors); d, e, tau from it.
@@ -233,6 +267,42 @@ std::vector<at::Tensor> tridiag_eigvecs(at::Tensor A, at::Tensor d, at::Tensor e
   if (!st.workspace.defined() || (size_t)st.workspace.numel() < need) {
     st.workspace = at::empty({(int64_t)std::max<size_t>(need, 1)},
                              A.options().dtype(at::kByte));
+    ROCBLAS_OK(rocblas_set_workspace(st.handle, st.workspace.data_ptr(),
+                                     (size_t)st.workspace.numel()));
+  }
+  for (int64_t b = 0; b < cnt; ++b) ROCBLAS_OK(run(b));
+  return {d, Z.transpose(1, 2)};
+}
+
+// Eigenvectors of the tridiagonal matrices alone (rocSOLVER stedc, divide
+// and conquer): d, e [cnt, n] (d overwritten with the ascending eigenvalues,
+// e destroyed).  Returns (evals [cnt, n], Z [cnt, n, n] with the eigenvectors
+// of T in columns); the caller applies Q (ops/linalg.py apply_q_blocked: the
+// reflectors grouped into 256-wide UT blocks on fp32 GEMMs, replacing
+// rocSOLVER ormtr's 32-wide panel loop).
+std::vector<at::Tensor> tridiag_stedc(at::Tensor d, at::Tensor e) {
+  TORCH_CHECK(d.is_cuda() && d.dim() == 2 && d.is_contiguous() && e.is_contiguous() &&
+              d.scalar_type() == at::kFloat && e.sizes() == d.sizes());
+  const int64_t cnt = d.size(0), n = d.size(1);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(d.device());
+  hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+  auto Z = at::empty({cnt, n, n}, d.options());
+  auto info = at::empty({std::max<int64_t>(cnt, 1)}, d.options().dtype(at::kInt));
+  if (cnt == 0 || n == 0) return {d, Z.transpose(1, 2)};
+  HandleState& st = handle_for(s);
+  auto run = [&](int64_t b) -> rocblas_status {
+    return rocsolver_sstedc(st.handle, rocblas_evect_tridiagonal, (int)n,
+                            d.data_ptr<float>() + b * n, e.data_ptr<float>() + b * n,
+                            Z.data_ptr<float>() + b * n * n, (int)n,
+                            info.data_ptr<int>() + b);
+  };
+  size_t need = 0;
+  ROCBLAS_OK(rocblas_start_device_memory_size_query(st.handle));
+  run(0);
+  ROCBLAS_OK(rocblas_stop_device_memory_size_query(st.handle, &need));
+  if (!st.workspace.defined() || (size_t)st.workspace.numel() < need) {
+    st.workspace = at::empty({(int64_t)std::max<size_t>(need, 1)},
+                             d.options().dtype(at::kByte));
     ROCBLAS_OK(rocblas_set_workspace(st.handle, st.workspace.data_ptr(),
                                      (size_t)st.workspace.numel()));
   }

@@ -404,12 +404,14 @@ __global__ void __launch_bounds__(SY_T) sytrd_syr2k_kernel(
 // Host driver: descs is a device table of `batch` descriptors, ns the host
 // copy of their sizes.  Issues 2 launches per column of the largest matrix
 // plus 2 per panel, all on `stream`, no host sync.
-void sytrd_batched(const SytrdDesc* descs_dev, const int* ns, int batch,
-                   hipStream_t stream) {
+void sytrd_batched_range(const SytrdDesc* descs_dev, const int* ns, int batch,
+                         int k_begin, int k_end, hipStream_t stream) {
   int maxn = 0;
   for (int b = 0; b < batch; ++b) maxn = ns[b] > maxn ? ns[b] : maxn;
   if (maxn <= 0) return;
-  for (int p = 0; p < maxn; p += SY_NB) {
+  if (k_end > maxn) k_end = maxn;
+  // segments start on panel boundaries: panel [p, p+NB) is issued whole
+  for (int p = k_begin; p < k_end; p += SY_NB) {
     const int q = (p + SY_NB < maxn) ? p + SY_NB : maxn;
     for (int k = p; k < q; ++k) {
       const int rem = maxn - k;
@@ -430,6 +432,15 @@ void sytrd_batched(const SytrdDesc* descs_dev, const int* ns, int batch,
                          stream, descs_dev, q, p);
     }
   }
+}
+
+// Whole reduction in one call: 2 launches per column of the largest matrix
+// plus 2 per panel.  A matrix of size n is complete once the panels up to n
+// have been issued (later launches return early for it), which lets the
+// caller split the chain into segments and finish small matrices early.
+void sytrd_batched(const SytrdDesc* descs_dev, const int* ns, int batch,
+                   hipStream_t stream) {
+  sytrd_batched_range(descs_dev, ns, batch, 0, 1 << 30, stream);
 }
 
 }  // namespace kfac

@@ -6,17 +6,17 @@ sizes (all K-FAC factors a rank owns) with as little latency as possible:
 * matrices are bucketed by size; each bucket is ONE batched call;
 * n <= 64: the LDS-resident parallel Jacobi kernel (csrc/eigh_jacobi.hip),
   one matrix per workgroup;
-* with ``KFAC_EIGH=sytrd``, n >= ``KFAC_SYTRD_MIN_N``: the native batched
-  tridiagonalisation (csrc/sytrd.hip): every such factor of every bucket
-  advances one column per launch pair in ONE chain, then each matrix is
-  finished by rocSOLVER ``stedc`` + ``ormtr`` (the second half of syevd) on
-  the lanes below.  Opt-in: on MI355X it is correct to ~1e-6 and its
-  3 x 4608 chain now matches rocSOLVER's (164 vs 165 ms,
-  profiles/sytrd_per_column_trace_r2.txt), but the refresh of the real
-  step-100 ResNet-50 factors is still slower than the default (375 ms at
-  n >= 4000, 411 ms at n >= 2000, vs 353 ms for warm-tested syevd:
-  profiles/refresh_probe_r2_sytrd_tier.jsonl) -- the chain pays ~16 us of
-  kernel-boundary floor per column, and its stedc + ormtr tail follows it;
+* n >= ``KFAC_SYTRD_MIN_N`` (default tier, ``KFAC_EIGH_LARGE=sytrd``):
+  the native batched tridiagonalisation (csrc/sytrd.hip).  The factors are
+  grouped into chains by size (``KFAC_SYTRD_SPLIT``, default: n >= 4000 and
+  the rest), each chain on its own lane advancing every member one column
+  per launch pair; a chain is issued in segments ending where each bucket
+  ends, so the bucket's tail -- rocSOLVER ``stedc`` on T, then the blocked
+  UT back-transform ``apply_q_blocked`` (3 batched fp32 GEMMs per 256
+  reflectors; 4-8x faster than rocSOLVER ``ormtr``: 3 x 4608 in 11 vs
+  39 ms, profiles/tail_probe_r2.jsonl) -- runs on another lane while the
+  chain continues.  Real step-100 ResNet-50 refresh: 290 ms vs 355 ms for
+  syevd (profiles/refresh_probe_r2_chains.jsonl);
 * other n: direct batched rocSOLVER ``syevd`` calls from C++
   (csrc/solver.cpp) which, unlike ``torch.linalg.eigh``, never synchronise
   the host;
@@ -31,7 +31,9 @@ is invariant to that freedom.
 
 Environment knobs: ``KFAC_EIGH`` = auto | torch | syevd | syevj | syevdj
 (force one algorithm for n > 64; sytrd = native tridiagonalisation tier),
-``KFAC_SYTRD_MIN_N`` (smallest n for the sytrd tier), ``KFAC_EIGH_STREAMS`` (lanes, default 8),
+``KFAC_EIGH_LARGE`` (sytrd | syevd | block), ``KFAC_SYTRD_MIN_N`` (smallest n
+for the sytrd tier), ``KFAC_SYTRD_SPLIT`` (chain boundaries),
+``KFAC_EIGH_ORMTR`` (blocked | rocsolver), ``KFAC_EIGH_STREAMS`` (lanes, default 8),
 ``KFAC_EIGH_THREADS`` (0: issue every lane from the calling thread),
 ``KFAC_EIGH_SPLIT_N`` (factors at least this large are solved one per job),
 ``KFAC_JACOBI_SWEEPS`` / ``KFAC_JACOBI_TOL`` (small-n kernel).
@@ -58,7 +60,7 @@ JACOBI_MAX_N = int(os.environ.get('KFAC_JACOBI_MAX_N', '128'))
 
 def sytrd_min_n() -> int:
     """Smallest factor dimension sent to the native tridiagonalisation."""
-    return int(os.environ.get('KFAC_SYTRD_MIN_N', '512'))
+    return int(os.environ.get('KFAC_SYTRD_MIN_N', '2000'))
 
 
 logger = logging.getLogger(__name__)
@@ -168,14 +170,21 @@ def _accept_warm(stack: torch.Tensor, warm: torch.Tensor
 
 def large_algo() -> str:
     """Solver for factors above the LDS Jacobi tier that the warm-start
-    acceptance test did not settle: ``KFAC_EIGH_LARGE`` = syevd | block.
+    acceptance test did not settle: ``KFAC_EIGH_LARGE`` = sytrd | syevd |
+    block.
 
-    Default syevd: on the real ResNet-50 step-100 refresh the native block
+    Default sytrd: factors with n >= ``KFAC_SYTRD_MIN_N`` (2000) go through
+    the native tridiagonalisation chains with the blocked back-transform,
+    the rest through batched syevd on the other lanes -- the real ResNet-50
+    step-100 refresh takes 290 ms against 355 ms with syevd alone
+    (profiles/refresh_probe_r2_chains.jsonl).
+
+    block: on the real ResNet-50 step-100 refresh the native block
     Jacobi (warm) needs 6-12 sweeps on the large A factors (the step-0
     basis of a rank-deficient early factor is a poor start) and the mix
     takes 1002 ms against 395 ms for syevd at equal accuracy
     (profiles/refresh_probe_r2_resnet50_step100.jsonl)."""
-    return os.environ.get('KFAC_EIGH_LARGE', 'syevd')
+    return os.environ.get('KFAC_EIGH_LARGE', 'sytrd')
 
 
 def _large_bucket(stack: torch.Tensor, warm: torch.Tensor | None
@@ -273,8 +282,64 @@ def eigh_many(
     return [o for o in out if o is not None]
 
 
+def _settle_warm(gpu: list, stacks: dict, warms: dict, out: dict) -> list:
+    """Warm-start acceptance (``_accept_warm``'s test) for every warm bucket
+    the sytrd tier would otherwise reduce, with ONE host read-back for all
+    of them: accepted factors keep their previous basis (eigenvalues are
+    the fresh Rayleigh quotients) and leave the bucket."""
+    cand = [(k, v) for k, v in gpu if k[2] and k in warms and JACOBI_MAX_N < k[0]
+            <= WARM_ACCEPT_MAX_N and block_jacobi_enabled_for_sytrd()]
+    if not cand:
+        return gpu
+    flags, stats = [], []
+    for key, _ in cand:
+        st, w = stacks[key], warms[key]
+        aq = torch.bmm(st, w)
+        r = (w * aq).sum(1)
+        res = (aq - w * r.unsqueeze(1)).flatten(1).norm(dim=1)
+        flags.append(res <= WARM_ACCEPT_TOL * st.flatten(1).norm(dim=1))
+        stats.append(r)
+    ok_all = torch.cat(flags).tolist()
+    new_gpu, pos = [], 0
+    cand_keys = {k for k, _ in cand}
+    for key, idxs in gpu:
+        if key not in cand_keys:
+            new_gpu.append((key, idxs))
+            continue
+        j = [k for k, _ in cand].index(key)
+        ok = ok_all[pos:pos + len(idxs)]
+        pos += len(idxs)
+        acc = [i for i, v in enumerate(ok) if v]
+        last_stats.setdefault('accepted', []).extend([key[0]] * len(acc))
+        if acc:
+            sel = torch.tensor(acc, device=stacks[key].device)
+            rs, order = stats[j].index_select(0, sel).sort(dim=1)
+            q = warms[key].index_select(0, sel)
+            q = q.gather(2, order.unsqueeze(1).expand(-1, q.shape[1], -1))
+            for t, i in enumerate(acc):
+                out[idxs[i]] = (rs[t], q[t])
+        keep = [i for i, v in enumerate(ok) if not v]
+        if not keep:
+            continue
+        if acc:
+            sel = torch.tensor(keep, device=stacks[key].device)
+            stacks[key] = stacks[key].index_select(0, sel).contiguous()
+            warms[key] = warms[key].index_select(0, sel).contiguous()
+            idxs = [idxs[i] for i in keep]
+        new_gpu.append((key, idxs))
+    return new_gpu
+
+
+def block_jacobi_enabled_for_sytrd() -> bool:
+    """Warm acceptance in front of the sytrd tier (``KFAC_EIGH_BLOCK=0``
+    turns it off, as for the block-Jacobi tier)."""
+    return os.environ.get('KFAC_EIGH_BLOCK', '1') != '0'
+
+
 def _use_sytrd(n: int) -> bool:
-    if os.environ.get('KFAC_EIGH', 'auto') != 'sytrd' or n < sytrd_min_n():
+    mode = os.environ.get('KFAC_EIGH', 'auto')
+    on = mode == 'sytrd' or (mode == 'auto' and large_algo() == 'sytrd')
+    if not on or n < sytrd_min_n():
         return False
     lib = native()
     return lib is not None and n <= int(lib.sytrd_max_n())
@@ -299,7 +364,7 @@ def _jobs(gpu: list) -> list[tuple[tuple, list[int], int, int]]:
 
 def _run_lane(stream: torch.cuda.Stream, jobs: list, stacks: dict,
               warms: dict | None = None) -> list:
-    with torch.cuda.stream(stream):
+    with _lane_lock(stream), torch.cuda.stream(stream):
         res = []
         for key, _, lo, hi in jobs:
             w = warms.get(key) if warms else None
@@ -337,12 +402,14 @@ def _launch_jobs(
     dependent tiny kernels on the GPU as well.
     """
     main = torch.cuda.current_stream(dev)
+    out: dict[int, tuple[torch.Tensor, torch.Tensor]] = {}
+    if warms and any(_use_sytrd(k[0]) for k, _ in gpu):
+        gpu = _settle_warm(gpu, stacks, warms, out)
     ready = torch.cuda.Event()
     ready.record(main)
     streams = _side_streams(dev)
     big = [(k, v) for k, v in gpu if _use_sytrd(k[0])]
     rest = [(k, v) for k, v in gpu if not _use_sytrd(k[0])]
-    out: dict[int, tuple[torch.Tensor, torch.Tensor]] = {}
     if big:
         out.update(_launch_sytrd(big, rest, stacks, main, ready, streams))
         return out
@@ -373,22 +440,82 @@ def _launch_jobs(
     return out
 
 
-def _sytrd_lane(stream: torch.cuda.Stream, keys: list, stacks: dict) -> list:
-    with torch.cuda.stream(stream):
-        return native().sytrd_reduce([stacks[k] for k in keys])
+def _q_back_transform() -> str:
+    """Back-transform of the sytrd tier: ``KFAC_EIGH_ORMTR`` = blocked
+    (apply_q_blocked, default) | rocsolver (ormtr)."""
+    return os.environ.get('KFAC_EIGH_ORMTR', 'blocked')
 
 
-def _tridiag_lane(stream: torch.cuda.Stream, jobs: list, stacks: dict,
-                  red: dict) -> list:
+_lane_locks: dict[int, Any] = {}
+
+
+def _lane_lock(stream: torch.cuda.Stream) -> Any:
+    """One host thread at a time per lane: the rocSOLVER handle (and its
+    workspace) is cached per stream and is not thread-safe."""
+    import threading
+
+    return _lane_locks.setdefault(stream.cuda_stream, threading.Lock())
+
+
+def _tail_job(stream: torch.cuda.Stream, ev: torch.cuda.Event, red: torch.Tensor,
+              d: torch.Tensor, e: torch.Tensor, tau: torch.Tensor
+              ) -> tuple[torch.Tensor, torch.Tensor]:
+    """Finish one reduced bucket on ``stream`` once the chain reached it:
+    eigenpairs of T (rocSOLVER stedc), then X = Q Z."""
+    with _lane_lock(stream), torch.cuda.stream(stream):
+        stream.wait_event(ev)
+        for t in (red, d, e, tau):  # produced on the chain lane
+            t.record_stream(stream)
+        if _q_back_transform() == 'rocsolver':
+            return native().tridiag_eigvecs(red, d, e, tau)
+        w, z = native().tridiag_stedc(d, e)
+        return w, apply_q_blocked(red, tau, z)
+
+
+def _chain_groups(keys: list) -> list[list]:
+    """Split the sytrd-tier buckets into independent chains (one lane
+    each) at the sizes in ``KFAC_SYTRD_SPLIT`` (comma-separated).  Each chain costs ~24 us
+    of kernel-boundary latency per column of its largest matrix, so two
+    chains on two hardware queues overlap each other's gaps, while the
+    smaller matrices no longer add their symv traffic to the largest chain."""
+    cuts = sorted((int(c) for c in os.environ.get('KFAC_SYTRD_SPLIT', '4000').split(',')
+                   if c), reverse=True)
+    groups, left = [], list(keys)
+    for c in cuts:
+        groups.append([k for k in left if k[0] >= c])
+        left = [k for k in left if k[0] < c]
+    groups.append(left)
+    return [g for g in groups if g]
+
+
+def _run_chain(stream: torch.cuda.Stream, keys: list, stacks: dict,
+               tail_lane: dict, pool: Any) -> list:
+    """Issue one chain (ascending n) in segments; after each bucket's last
+    panel, hand that bucket's tail to its lane behind an event."""
+    lib = native()
+    nb = int(lib.sytrd_nb())
+    keys = sorted(keys, key=lambda k: k[0])
+    out = []
     with torch.cuda.stream(stream):
-        res = []
-        for key, _, lo, hi in jobs:
-            d, e, tau = red[key]
-            for t in (d, e, tau):  # allocated on lane 0, read here
-                t.record_stream(stream)
-            res.append(native().tridiag_eigvecs(
-                stacks[key][lo:hi], d[lo:hi], e[lo:hi], tau[lo:hi]))
-        return res
+        state = lib.sytrd_begin([stacks[k] for k in keys])
+        descs = state[0]
+        sizes = [k[0] for k in keys for _ in range(stacks[k].shape[0])]
+        k0 = 0
+        for j, key in enumerate(keys):
+            k1 = -(-key[0] // nb) * nb
+            if k1 > k0:
+                lib.sytrd_advance(descs, sizes, k0, k1)
+                k0 = k1
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            d, e, tau = state[2 + 3 * j:5 + 3 * j]
+            args = (tail_lane[key], ev, stacks[key], d, e, tau)
+            out.append((key, pool.submit(_tail_job, *args) if pool else _tail_job(*args)))
+        for t in state[:2]:
+            t.record_stream(stream)
+        for k in keys:
+            stacks[k].record_stream(stream)
+    return out
 
 
 def _launch_sytrd(
@@ -399,61 +526,107 @@ def _launch_sytrd(
     ready: torch.cuda.Event,
     streams: list[torch.cuda.Stream],
 ) -> dict[int, tuple[torch.Tensor, torch.Tensor]]:
-    """Large buckets: ONE native tridiagonalisation chain on lane 0 while the
-    other lanes run the small buckets' syevd; then every large matrix is
-    finished (stedc + ormtr) as its own job, LPT over all lanes."""
+    """Large buckets: native tridiagonalisation chains (``_chain_groups``),
+    one lane each, issued in segments that end where each bucket's size
+    ends.  As soon as a segment is enqueued, an event marks it and that
+    bucket's tail (stedc + back-transform, ``_tail_job``) is issued on
+    another lane behind the event, so tails run while the chains are still
+    reducing the larger factors.  The small buckets' syevd share the
+    non-chain lanes.  Only as many lanes as the process has hardware queues
+    (``GPU_MAX_HW_QUEUES``, HIP's default 4) are used: streams beyond that
+    share a queue with a chain lane, and work queued behind a chain waits
+    for it in order."""
+    hwq = int(os.environ.get('GPU_MAX_HW_QUEUES', '4'))
+    streams = streams[:max(2, min(len(streams), hwq))]
     for s in streams:
         s.wait_event(ready)
-    keys = [k for k, _ in big]
+    groups = _chain_groups([k for k, _ in big])
+    nchain = min(len(groups), len(streams) - 1)
+    if nchain < len(groups):  # too few lanes: one chain
+        groups = [sum(groups, [])]
+        nchain = 1
+    chains = streams[:nchain]
+    others = streams[nchain:]
     small_jobs = sorted(_jobs(rest), key=lambda j: -_bucket_cost(j[0][0], j[3] - j[2]))
-    lanes: list[list] = [[] for _ in streams[1:]]
-    loads = [0.0] * len(lanes)
+    lanes: list[list] = [[] for _ in others]
+    loads = [0.0] * len(others)
     for job in small_jobs:
         k = loads.index(min(loads))
         loads[k] += _bucket_cost(job[0][0], job[3] - job[2])
         lanes[k].append(job)
-    active = [(s, ln) for s, ln in zip(streams[1:], lanes) if ln]
-    if _threads_enabled() and active:
-        pool = _executor(len(active) + 1)
-        fut_red = pool.submit(_sytrd_lane, streams[0], keys, stacks)
-        futs = [pool.submit(_run_lane, s, ln, stacks) for s, ln in active]
-        flat = fut_red.result()
-        results = [f.result() for f in futs]
-    else:
-        flat = _sytrd_lane(streams[0], keys, stacks)
-        results = [_run_lane(s, ln, stacks) for s, ln in active]
-    red = {k: tuple(flat[3 * i:3 * i + 3]) for i, k in enumerate(keys)}
-    reduced = torch.cuda.Event()
-    reduced.record(streams[0])
-    # phase 2: per-matrix stedc + ormtr jobs over every lane
-    tjobs = [(key, idxs, b, b + 1) for key, idxs in big for b in range(len(idxs))]
-    tjobs.sort(key=lambda j: -_bucket_cost(j[0][0], 1))
-    tl: list[list] = [[] for _ in streams]
-    tload = [0.0] * len(streams)
-    for job in tjobs:
-        k = tload.index(min(tload))
-        tload[k] += _bucket_cost(job[0][0], 1)
-        tl[k].append(job)
-    tactive = [(s, ln) for s, ln in zip(streams, tl) if ln]
-    for s, _ in tactive:
-        s.wait_event(reduced)
-    if _threads_enabled() and len(tactive) > 1:
-        pool = _executor(len(tactive))
-        tf = [pool.submit(_tridiag_lane, s, ln, stacks, red) for s, ln in tactive]
-        tres = [f.result() for f in tf]
-    else:
-        tres = [_tridiag_lane(s, ln, stacks, red) for s, ln in tactive]
+    tail_lane = {}
+    for key in sorted((k for k, _ in big), key=lambda k: -_bucket_cost(
+            k[0], stacks[k].shape[0])):
+        k = loads.index(min(loads))
+        loads[k] += _bucket_cost(key[0], stacks[key].shape[0]) / 4  # tail only
+        tail_lane[key] = others[k]
+    threads = _threads_enabled()
+    pool = _executor(len(others) + nchain + len(big)) if threads else None
+    active = [(s, ln) for s, ln in zip(others, lanes) if ln]
+    futs = [pool.submit(_run_lane, s, ln, stacks) for s, ln in active] if pool else []
+    cf = [pool.submit(_run_chain, c, g, stacks, tail_lane, pool) if pool else
+          _run_chain(c, g, stacks, tail_lane, None) for c, g in zip(chains, groups)]
+    results = [f.result() for f in futs] if pool else [
+        _run_lane(s, ln, stacks) for s, ln in active]
+    tails = [(key, f.result() if pool else f)
+             for key, f in sum((c.result() if pool else c for c in cf), [])]
     out: dict[int, tuple[torch.Tensor, torch.Tensor]] = {}
-    for (s, ln), res in list(zip(active, results)) + list(zip(tactive, tres)):
+    for s in streams:  # every lane's work is enqueued by now
         main.wait_stream(s)
+    for (s, ln), res in zip(active, results):
         for (key, idxs, lo, hi), (evals, evecs) in zip(ln, res):
             evals.record_stream(main)
             evecs.record_stream(main)
             for k in range(hi - lo):
                 out[idxs[lo + k]] = (evals[k], evecs[k])
-    for k in keys:
-        stacks[k].record_stream(streams[0])
+    idx_of = dict(big)
+    for key, (evals, evecs) in tails:
+        evals.record_stream(main)
+        evecs.record_stream(main)
+        for k, i in enumerate(idx_of[key]):
+            out[i] = (evals[k], evecs[k])
     return out
+
+
+def apply_q_blocked(red: torch.Tensor, tau: torch.Tensor, z: torch.Tensor,
+                    nb: int = 256) -> torch.Tensor:
+    """``Q Z`` for the reflectors the native tridiagonalisation left in
+    ``red`` (reflector k in ROW k: v[k+1] = 1 implicit, v[k+2:] stored;
+    Q = H_0 H_1 ... H_{n-2}, H_k = I - tau_k v_k v_k^T) -- the back-transform
+    of the eigenvectors ``z`` of T (columns) into eigenvectors of A.
+
+    rocSOLVER's ormtr applies the reflectors in 32-wide panels with ~10
+    small kernels each; here ``nb`` reflectors form one UT block
+    ``I - V T V^T`` with ``T = (striu(V^T V) + diag(1/tau))^-1`` (the
+    identity behind LAPACK's larft), so each block costs three batched fp32
+    GEMMs over every factor of the size at once and one small triangular
+    solve.  Blocks run last to first; block p touches rows p+1..n-1 only.
+    tau = 0 (nothing to annihilate: H = I) zeroes the reflector.  No host
+    synchronisation.  Returns X [cnt, n, n], eigenvectors in columns."""
+    c, n, _ = red.shape
+    x = z.contiguous().clone() if z.is_contiguous() else z.contiguous()
+    if n < 2:
+        return x
+    vt = torch.triu(red, diagonal=2)
+    idx = torch.arange(n - 1, device=red.device)
+    vt[:, idx, idx + 1] = 1.0
+    live = (tau != 0).to(red.dtype)
+    vt.mul_(live.unsqueeze(-1))
+    eye = torch.eye(nb, device=red.device, dtype=red.dtype)
+    for p in reversed(range(0, n - 1, nb)):
+        q = min(p + nb, n - 1)
+        b = q - p
+        v = vt[:, p:q, p + 1:]  # [c, b, m]: V_b^T restricted to rows >= p+1
+        g = torch.bmm(v, v.transpose(1, 2))
+        t_ = tau[:, p:q]
+        dinv = torch.where(t_ == 0, torch.ones_like(t_), 1.0 / torch.where(
+            t_ == 0, torch.ones_like(t_), t_))
+        u = torch.triu(g, diagonal=1) + torch.diag_embed(dinv)
+        tm = torch.linalg.solve_triangular(u, eye[:b, :b].expand(c, b, b), upper=True)
+        xs = x[:, p + 1:, :]
+        w = torch.bmm(tm, torch.bmm(v, xs))
+        xs.baddbmm_(v.transpose(1, 2), w, alpha=-1.0)
+    return x
 
 
 def _threads_enabled() -> bool:

@@ -259,12 +259,15 @@ def test_sytrd_reduce_reconstructs(cuda):
             assert err < 1e-5 * a0[b].abs().max().item(), (n, b, err)
 
 
+@pytest.mark.parametrize('back', ['blocked', 'rocsolver'])
 @pytest.mark.parametrize('sizes', [(65, 96, 97, 130, 257), (513, 1000, 64, 700, 2049)])
-def test_eigh_many_sytrd_tier(cuda, monkeypatch, sizes):
-    """eigh_many through the native sytrd tier (+ rocSOLVER stedc/ormtr),
-    including rank-deficient K-FAC-like factors, vs a float64 reference."""
+def test_eigh_many_sytrd_tier(cuda, monkeypatch, sizes, back):
+    """eigh_many through the native sytrd tier (segmented chain; stedc, then
+    the blocked UT back-transform or rocSOLVER ormtr), including
+    rank-deficient K-FAC-like factors, vs a float64 reference."""
     monkeypatch.setenv('KFAC_EIGH', 'sytrd')
     monkeypatch.setenv('KFAC_SYTRD_MIN_N', '65')
+    monkeypatch.setenv('KFAC_EIGH_ORMTR', back)
     torch.manual_seed(7)
     mats = []
     for j, n in enumerate(sizes):
@@ -275,6 +278,31 @@ def test_eigh_many_sytrd_tier(cuda, monkeypatch, sizes):
     res = linalg.eigh_many(mats)
     for m, (d, q) in zip(mats, res):
         assert d.shape == (m.shape[0],) and q.shape == m.shape
+        _check_eigpairs(m, d, q)
+
+
+def test_eigh_many_sytrd_warm_acceptance(cuda, monkeypatch):
+    """Default large tier with warm bases: a factor its previous basis still
+    diagonalises is settled by the acceptance test (no reduction), the
+    others go through the chain; every result matches float64."""
+    monkeypatch.setenv('KFAC_EIGH_LARGE', 'sytrd')
+    monkeypatch.setenv('KFAC_SYTRD_MIN_N', '129')
+    torch.manual_seed(11)
+    mats, warm = [], []
+    for j, n in enumerate((200, 200, 300, 130)):
+        x = torch.randn(n, 2 * n, device=cuda)
+        m = x @ x.t() / (2 * n) + 1e-3 * torch.eye(n, device=cuda)
+        mats.append(m)
+        if j == 0:
+            warm.append(torch.linalg.eigh(m.double())[1].float())  # exact basis
+        else:
+            warm.append(torch.linalg.eigh(m + 0.1 * torch.eye(n, device=cuda)
+                                          + 0.05 * torch.randn(n, n, device=cuda).mT
+                                          @ torch.randn(n, n, device=cuda) / n)[1])
+    linalg.last_stats.clear()
+    res = linalg.eigh_many(mats, warm)
+    assert linalg.last_stats.get('accepted', []).count(200) >= 1
+    for m, (d, q) in zip(mats, res):
         _check_eigpairs(m, d, q)
 
 

@@ -53,6 +53,8 @@ def snapshot(steps: int):  # type: ignore[no-untyped-def]
         if i == 0:
             for name, l in pre._layers.values():
                 qs[name] = (l.qa.clone(), l.qg.clone())
+    if steps == 0:  # cold: the step-0 factors (no previous basis)
+        qs = None
     # factors as they stand at the next refresh: run the step-100 forward /
     # backward (factor hooks fire) without the K-FAC step
     opt.zero_grad()
@@ -63,7 +65,7 @@ def snapshot(steps: int):  # type: ignore[no-untyped-def]
     mats, warm = [], []
     for name, l in pre._layers.values():
         mats += [l.a_factor.float().clone(), l.g_factor.float().clone()]
-        warm += [qs[name][0], qs[name][1]]
+        warm += [qs[name][0], qs[name][1]] if qs is not None else [None, None]
     return mats, warm
 
 
@@ -115,10 +117,14 @@ def main() -> None:
         if mode.startswith('sytrd'):
             # native batched tridiagonalisation for n >= the number in the name
             os.environ['KFAC_EIGH'] = 'sytrd'
-            os.environ['KFAC_SYTRD_MIN_N'] = mode[len('sytrd'):].split('_')[0]
+            spec = mode[len('sytrd'):].split('_')[0]  # e.g. 1000x4000-2000
+            os.environ['KFAC_SYTRD_MIN_N'] = spec.split('x')[0]
+            os.environ['KFAC_SYTRD_SPLIT'] = (spec.split('x')[1].replace('-', ',')
+                                              if 'x' in spec else '4000')
         else:
             os.environ['KFAC_EIGH'] = 'auto'
-        w = list(warm) if mode.endswith('_warm') else None
+        os.environ['KFAC_EIGH_ORMTR'] = 'rocsolver' if '_ormtr' in mode else 'blocked'
+        w = list(warm) if '_warm' in mode else None
         linalg.last_stats.clear()
         return linalg.eigh_many([m.clone() for m in mats], w)
 
