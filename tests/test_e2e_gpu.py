@@ -229,3 +229,32 @@ def test_grad_scaler_unscale_on_device_no_sync(cuda):
             torch.testing.assert_close(b.g_factor, a.g_factor, rtol=1e-5, atol=1e-7)
         p_ref.step()
         p_amp.step()
+
+
+@pytest.mark.parametrize('method', ['eigen', 'inverse'])
+def test_early_precondition_overlap_is_exact(cuda, monkeypatch, method):
+    """Preconditioning the last layers during backward on a side stream
+    (KFAC_PRECOND_OVERLAP) yields bitwise the same training trajectory as
+    preconditioning every layer in step()."""
+    monkeypatch.setattr(torch.backends.cudnn, 'deterministic', True)  # MIOpen wrw
+    runs = {}
+    for flag in ('1', '0'):
+        monkeypatch.setenv('KFAC_PRECOND_OVERLAP', flag)
+        model = _net().to(cuda)
+        pre = kfac.KFACPreconditioner(model, factor_update_steps=1, inv_update_steps=3,
+                                      compute_method=method, lr=0.1, kl_clip=0.001)
+        opt = torch.optim.SGD(model.parameters(), lr=0.1)
+        torch.manual_seed(3)
+        for _ in range(7):
+            x = torch.randn(8, 3, 14, 14, device=cuda)
+            y = torch.randint(0, 10, (8,), device=cuda)
+            opt.zero_grad()
+            torch.nn.functional.cross_entropy(model(x), y).backward()
+            pre.step()
+            opt.step()
+        torch.cuda.synchronize()
+        if flag == '1':
+            assert pre._early is not None and pre._early['names'], 'no early group'
+        runs[flag] = [p.detach().clone() for p in model.parameters()]
+    for a, b in zip(runs['1'], runs['0']):
+        assert torch.equal(a, b)
