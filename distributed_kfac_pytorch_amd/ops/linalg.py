@@ -287,8 +287,11 @@ def _settle_warm(gpu: list, stacks: dict, warms: dict, out: dict) -> list:
     the sytrd tier would otherwise reduce, with ONE host read-back for all
     of them: accepted factors keep their previous basis (eigenvalues are
     the fresh Rayleigh quotients) and leave the bucket."""
+    # chain members are not candidates: a fixed chain membership keeps its
+    # captured graphs (one per signature) valid from refresh to refresh
     cand = [(k, v) for k, v in gpu if k[2] and k in warms and JACOBI_MAX_N < k[0]
-            <= WARM_ACCEPT_MAX_N and block_jacobi_enabled_for_sytrd()]
+            <= WARM_ACCEPT_MAX_N and not _use_sytrd(k[0])
+            and block_jacobi_enabled_for_sytrd()]
     if not cand:
         return gpu
     flags, stats = [], []
@@ -467,9 +470,11 @@ def _tail_job(stream: torch.cuda.Stream, ev: torch.cuda.Event, red: torch.Tensor
         for t in (red, d, e, tau):  # produced on the chain lane
             t.record_stream(stream)
         if _q_back_transform() == 'rocsolver':
-            return native().tridiag_eigvecs(red, d, e, tau)
+            w, x = native().tridiag_eigvecs(red, d, e, tau)
+            return w.clone(), x
         w, z = native().tridiag_stedc(d, e)
-        return w, apply_q_blocked(red, tau, z)
+        # d is the chain's persistent buffer when replayed from graphs
+        return w.clone(), apply_q_blocked(red, tau, z)
 
 
 def _chain_groups(keys: list) -> list[list]:
@@ -488,31 +493,103 @@ def _chain_groups(keys: list) -> list[list]:
     return [g for g in groups if g]
 
 
+_chain_cache: dict[tuple, dict] = {}
+_hi: list[torch.cuda.Stream] = []
+
+
+def _hi_streams(device: torch.device) -> list[torch.cuda.Stream]:
+    """High-priority lanes for the largest chain and its tail
+    (``KFAC_SYTRD_PRIORITY=0``: none)."""
+    global _hi
+    if os.environ.get('KFAC_SYTRD_PRIORITY', '1') == '0':
+        return []
+    if not _hi or _hi[0].device != device:
+        lo, hi_prio = torch.cuda.Stream.priority_range()
+        _hi = [torch.cuda.Stream(device=device, priority=hi_prio) for _ in range(2)]
+    return _hi
+
+
+def _chain_graphs_enabled() -> bool:
+    return os.environ.get('KFAC_SYTRD_GRAPHS', '1') != '0'
+
+
+def _chain_entry(sig: tuple, keys: list, stacks: dict) -> dict:
+    """Persistent operands + one captured HIP graph per segment for a chain
+    signature (the sizes and counts of its buckets), built on first use.
+
+    A refresh is bound by the HOST's launch rate, not the GPU: ~45k kernel
+    launches (the 4608 chain alone issues ~9.3k) complete only ~5 ms after
+    the last one is enqueued (profiles/refresh_variance_r2.jsonl).  A
+    replayed segment is one host call; the matrices are copied into the
+    persistent operands first (a D2D copy)."""
+    ent = _chain_cache.get(sig)
+    if ent is not None:
+        return ent
+    lib = native()
+    nb = int(lib.sytrd_nb())
+    bufs = [torch.empty_like(stacks[k]) for k in keys]
+    state = lib.sytrd_begin(bufs)
+    sizes = [k[0] for k in keys for _ in range(stacks[k].shape[0])]
+    graphs: list = []
+    k0 = 0
+    for key in keys:
+        k1 = -(-key[0] // nb) * nb
+        g = None
+        if k1 > k0:
+            g = torch.cuda.CUDAGraph()
+            # no torch.cuda.graph(): its entry synchronises the device and
+            # empties the cache while the other lanes are running
+            g.capture_begin(capture_error_mode='thread_local')
+            lib.sytrd_advance(state[0], sizes, k0, k1)
+            g.capture_end()
+            k0 = k1
+        graphs.append(g)
+    ent = {'bufs': bufs, 'state': state, 'graphs': graphs}
+    _chain_cache[sig] = ent
+    return ent
+
+
 def _run_chain(stream: torch.cuda.Stream, keys: list, stacks: dict,
                tail_lane: dict, pool: Any) -> list:
     """Issue one chain (ascending n) in segments; after each bucket's last
-    panel, hand that bucket's tail to its lane behind an event."""
+    panel, hand that bucket's tail to its lane behind an event.  Segments
+    replay from captured HIP graphs (``_chain_entry``; ``KFAC_SYTRD_GRAPHS=0``
+    launches them eagerly)."""
     lib = native()
     nb = int(lib.sytrd_nb())
     keys = sorted(keys, key=lambda k: k[0])
     out = []
     with torch.cuda.stream(stream):
-        state = lib.sytrd_begin([stacks[k] for k in keys])
+        if _chain_graphs_enabled():
+            sig = (str(stream.device), tuple((k[0], stacks[k].shape[0]) for k in keys))
+            ent = _chain_entry(sig, keys, stacks)
+            for buf, k in zip(ent['bufs'], keys):
+                buf.copy_(stacks[k])
+            state, reds, graphs = ent['state'], ent['bufs'], ent['graphs']
+        else:
+            reds = [stacks[k] for k in keys]
+            state = lib.sytrd_begin(reds)
+            graphs = None
         descs = state[0]
         sizes = [k[0] for k in keys for _ in range(stacks[k].shape[0])]
         k0 = 0
         for j, key in enumerate(keys):
-            k1 = -(-key[0] // nb) * nb
-            if k1 > k0:
-                lib.sytrd_advance(descs, sizes, k0, k1)
-                k0 = k1
+            if graphs is not None:
+                if graphs[j] is not None:
+                    graphs[j].replay()
+            else:
+                k1 = -(-key[0] // nb) * nb
+                if k1 > k0:
+                    lib.sytrd_advance(descs, sizes, k0, k1)
+                    k0 = k1
             ev = torch.cuda.Event()
             ev.record(stream)
             d, e, tau = state[2 + 3 * j:5 + 3 * j]
-            args = (tail_lane[key], ev, stacks[key], d, e, tau)
+            args = (tail_lane[key], ev, reds[j], d, e, tau)
             out.append((key, pool.submit(_tail_job, *args) if pool else _tail_job(*args)))
-        for t in state[:2]:
-            t.record_stream(stream)
+        if graphs is None:
+            for t in state[:2]:
+                t.record_stream(stream)
         for k in keys:
             stacks[k].record_stream(stream)
     return out
@@ -547,6 +624,17 @@ def _launch_sytrd(
         nchain = 1
     chains = streams[:nchain]
     others = streams[nchain:]
+    hi = _hi_streams(streams[0].device)
+    if hi:
+        # the largest chain and its tail are the critical path: high-priority
+        # queues get the CUs first, the other lanes fill in around them
+        # (276 vs 301 ms on the step-100 ResNet-50 mix).  Giving the second
+        # chain a high-priority lane as well measured worse (334 ms): the two
+        # chains are both bandwidth-bound and slow each other down
+        # (profiles/refresh_trace_r2.txt)
+        for h in hi:
+            h.wait_event(ready)
+        chains = [hi[0]] + chains[1:]
     small_jobs = sorted(_jobs(rest), key=lambda j: -_bucket_cost(j[0][0], j[3] - j[2]))
     lanes: list[list] = [[] for _ in others]
     loads = [0.0] * len(others)
@@ -560,6 +648,8 @@ def _launch_sytrd(
         k = loads.index(min(loads))
         loads[k] += _bucket_cost(key[0], stacks[key].shape[0]) / 4  # tail only
         tail_lane[key] = others[k]
+    if hi:
+        tail_lane[max(groups[0], key=lambda k: k[0])] = hi[1]
     threads = _threads_enabled()
     pool = _executor(len(others) + nchain + len(big)) if threads else None
     active = [(s, ln) for s, ln in zip(others, lanes) if ln]
@@ -571,7 +661,7 @@ def _launch_sytrd(
     tails = [(key, f.result() if pool else f)
              for key, f in sum((c.result() if pool else c for c in cf), [])]
     out: dict[int, tuple[torch.Tensor, torch.Tensor]] = {}
-    for s in streams:  # every lane's work is enqueued by now
+    for s in streams + hi:  # every lane's work is enqueued by now
         main.wait_stream(s)
     for (s, ln), res in zip(active, results):
         for (key, idxs, lo, hi), (evals, evecs) in zip(ln, res):

@@ -269,24 +269,28 @@ def test_eigh_many_sytrd_tier(cuda, monkeypatch, sizes, back):
     monkeypatch.setenv('KFAC_SYTRD_MIN_N', '65')
     monkeypatch.setenv('KFAC_EIGH_ORMTR', back)
     torch.manual_seed(7)
-    mats = []
-    for j, n in enumerate(sizes):
-        rows = n // 3 if j % 2 else 2 * n  # odd: rank-deficient PSD
-        x = torch.randn(n, rows, device=cuda)
-        mats.append(x @ x.t() / rows + 1e-3 * torch.eye(n, device=cuda))
-    mats.append(mats[0].clone())  # duplicate size -> a bucket of 2
-    res = linalg.eigh_many(mats)
-    for m, (d, q) in zip(mats, res):
-        assert d.shape == (m.shape[0],) and q.shape == m.shape
-        _check_eigpairs(m, d, q)
+    # twice with the same sizes: the second refresh replays the chain's
+    # captured HIP graphs on new matrices
+    for rep in range(2):
+        mats = []
+        for j, n in enumerate(sizes):
+            rows = n // 3 if (j + rep) % 2 else 2 * n  # rank-deficient PSD
+            x = torch.randn(n, rows, device=cuda)
+            mats.append(x @ x.t() / rows + 1e-3 * torch.eye(n, device=cuda))
+        mats.append(mats[0].clone())  # duplicate size -> a bucket of 2
+        res = linalg.eigh_many(mats)
+        for m, (d, q) in zip(mats, res):
+            assert d.shape == (m.shape[0],) and q.shape == m.shape
+            _check_eigpairs(m, d, q)
 
 
 def test_eigh_many_sytrd_warm_acceptance(cuda, monkeypatch):
     """Default large tier with warm bases: a factor its previous basis still
-    diagonalises is settled by the acceptance test (no reduction), the
-    others go through the chain; every result matches float64."""
+    diagonalises is settled by the acceptance test (no solve); chain
+    members are never candidates (fixed chain signature); every result
+    matches float64."""
     monkeypatch.setenv('KFAC_EIGH_LARGE', 'sytrd')
-    monkeypatch.setenv('KFAC_SYTRD_MIN_N', '129')
+    monkeypatch.setenv('KFAC_SYTRD_MIN_N', '250')  # 300: chain; 130, 200: syevd
     torch.manual_seed(11)
     mats, warm = [], []
     for j, n in enumerate((200, 200, 300, 130)):
