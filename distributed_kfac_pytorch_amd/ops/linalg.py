@@ -290,7 +290,7 @@ def _settle_warm(gpu: list, stacks: dict, warms: dict, out: dict) -> list:
     # chain members are not candidates: a fixed chain membership keeps its
     # captured graphs (one per signature) valid from refresh to refresh
     cand = [(k, v) for k, v in gpu if k[2] and k in warms and JACOBI_MAX_N < k[0]
-            <= WARM_ACCEPT_MAX_N and not _use_sytrd(k[0])
+            <= WARM_ACCEPT_MAX_N and not _use_sytrd(k[0], len(v))
             and block_jacobi_enabled_for_sytrd()]
     if not cand:
         return gpu
@@ -339,10 +339,21 @@ def block_jacobi_enabled_for_sytrd() -> bool:
     return os.environ.get('KFAC_EIGH_BLOCK', '1') != '0'
 
 
-def _use_sytrd(n: int) -> bool:
+def _use_sytrd(n: int, count: int = 1) -> bool:
+    """Native tier for a bucket of ``count`` factors of size n.
+
+    Buckets of more than ``KFAC_SYTRD_MAX_BATCH`` (8) factors stay on syevd:
+    the chain's symv streams the FULL square of every member per column
+    (rocSOLVER's reads one triangle), so it wins where the refresh is
+    latency-bound -- a few large factors, ResNet-50: 3 x 4608, 6 x 2304,
+    7 x 2048 -- and loses where it is bandwidth-bound: GPT-NeoX-125M's
+    12 x 3073 + 12 x 3072 + 12 x 2304 refresh took 947 ms in one chain vs
+    737 ms on syevd (profiles/neox_sytrd_vs_syevd_r2.txt)."""
     mode = os.environ.get('KFAC_EIGH', 'auto')
     on = mode == 'sytrd' or (mode == 'auto' and large_algo() == 'sytrd')
     if not on or n < sytrd_min_n():
+        return False
+    if mode == 'auto' and count > int(os.environ.get('KFAC_SYTRD_MAX_BATCH', '8')):
         return False
     lib = native()
     return lib is not None and n <= int(lib.sytrd_max_n())
@@ -406,13 +417,15 @@ def _launch_jobs(
     """
     main = torch.cuda.current_stream(dev)
     out: dict[int, tuple[torch.Tensor, torch.Tensor]] = {}
-    if warms and any(_use_sytrd(k[0]) for k, _ in gpu):
+    # chain membership is decided on the full buckets (before acceptance)
+    chain_keys = {k for k, v in gpu if _use_sytrd(k[0], len(v))}
+    if warms and chain_keys:
         gpu = _settle_warm(gpu, stacks, warms, out)
     ready = torch.cuda.Event()
     ready.record(main)
     streams = _side_streams(dev)
-    big = [(k, v) for k, v in gpu if _use_sytrd(k[0])]
-    rest = [(k, v) for k, v in gpu if not _use_sytrd(k[0])]
+    big = [(k, v) for k, v in gpu if k in chain_keys]
+    rest = [(k, v) for k, v in gpu if k not in chain_keys]
     if big:
         out.update(_launch_sytrd(big, rest, stacks, main, ready, streams))
         return out
