@@ -522,8 +522,18 @@ def _hi_streams(device: torch.device) -> list[torch.cuda.Stream]:
     return _hi
 
 
-def _chain_graphs_enabled() -> bool:
-    return os.environ.get('KFAC_SYTRD_GRAPHS', '1') != '0'
+def _chain_graphs_enabled(group: int = 0) -> bool:
+    """``KFAC_SYTRD_GRAPHS``: 0 (default: chains launched eagerly), 1 (every
+    chain replays captured graphs) or first (only the largest chain).
+
+    Replay enqueues a whole chain at once, so a lane that HIP maps onto the
+    same hardware queue waits behind all of it; eager launches interleave.
+    In the bench process (alternating runs, one box) replay gave 470 / 351 ms
+    refresh steps, first 364 / 368, eager 353 / 360
+    (profiles/sytrd_graphs_ab_r2.txt): the replay's host saving does not
+    pay for the outlier risk."""
+    mode = os.environ.get('KFAC_SYTRD_GRAPHS', '0')
+    return mode == '1' or (mode == 'first' and group == 0)
 
 
 def _chain_entry(sig: tuple, keys: list, stacks: dict) -> dict:
@@ -563,7 +573,7 @@ def _chain_entry(sig: tuple, keys: list, stacks: dict) -> dict:
 
 
 def _run_chain(stream: torch.cuda.Stream, keys: list, stacks: dict,
-               tail_lane: dict, pool: Any) -> list:
+               tail_lane: dict, pool: Any, group: int = 0) -> list:
     """Issue one chain (ascending n) in segments; after each bucket's last
     panel, hand that bucket's tail to its lane behind an event.  Segments
     replay from captured HIP graphs (``_chain_entry``; ``KFAC_SYTRD_GRAPHS=0``
@@ -573,7 +583,7 @@ def _run_chain(stream: torch.cuda.Stream, keys: list, stacks: dict,
     keys = sorted(keys, key=lambda k: k[0])
     out = []
     with torch.cuda.stream(stream):
-        if _chain_graphs_enabled():
+        if _chain_graphs_enabled(group):
             sig = (str(stream.device), tuple((k[0], stacks[k].shape[0]) for k in keys))
             ent = _chain_entry(sig, keys, stacks)
             for buf, k in zip(ent['bufs'], keys):
@@ -667,8 +677,9 @@ def _launch_sytrd(
     pool = _executor(len(others) + nchain + len(big)) if threads else None
     active = [(s, ln) for s, ln in zip(others, lanes) if ln]
     futs = [pool.submit(_run_lane, s, ln, stacks) for s, ln in active] if pool else []
-    cf = [pool.submit(_run_chain, c, g, stacks, tail_lane, pool) if pool else
-          _run_chain(c, g, stacks, tail_lane, None) for c, g in zip(chains, groups)]
+    cf = [pool.submit(_run_chain, c, g, stacks, tail_lane, pool, gi) if pool else
+          _run_chain(c, g, stacks, tail_lane, None, gi)
+          for gi, (c, g) in enumerate(zip(chains, groups))]
     results = [f.result() for f in futs] if pool else [
         _run_lane(s, ln, stacks) for s, ln in active]
     tails = [(key, f.result() if pool else f)
