@@ -12,7 +12,7 @@ sizes (all K-FAC factors a rank owns) with as little latency as possible:
   the rest), each chain on its own lane advancing every member one column
   per launch pair; a chain is issued in segments ending where each bucket
   ends, so the bucket's tail -- rocSOLVER ``stedc`` on T, then the blocked
-  UT back-transform ``apply_q_blocked`` (3 batched fp32 GEMMs per 256
+  UT back-transform ``apply_q_blocked`` (3 batched fp32 GEMMs per 512
   reflectors; 4-8x faster than rocSOLVER ``ormtr``: 3 x 4608 in 11 vs
   39 ms, profiles/tail_probe_r2.jsonl) -- runs on another lane while the
   chain continues.  Real step-100 ResNet-50 refresh: 290 ms vs 355 ms for
@@ -703,7 +703,7 @@ def _launch_sytrd(
 
 
 def apply_q_blocked(red: torch.Tensor, tau: torch.Tensor, z: torch.Tensor,
-                    nb: int = 256) -> torch.Tensor:
+                    nb: int = 512) -> torch.Tensor:
     """``Q Z`` for the reflectors the native tridiagonalisation left in
     ``red`` (reflector k in ROW k: v[k+1] = 1 implicit, v[k+2:] stored;
     Q = H_0 H_1 ... H_{n-2}, H_k = I - tau_k v_k v_k^T) -- the back-transform
