@@ -277,9 +277,44 @@ def eigh_many(
                 key: torch.stack([warm[i] for i in idxs])  # type: ignore[index]
                 for key, idxs in gpu if key[2]
             }
-            for i, r in _launch_jobs(gpu, stacks, dev, warms).items():
+            res = _launch_jobs(gpu, stacks, dev, warms)
+            for i, r in res.items():
                 out[i] = r
+            _repair_nonfinite(mats, out, list(res))
     return [o for o in out if o is not None]
+
+
+def _repair_nonfinite(mats: list[torch.Tensor], out: list, idxs: list[int]) -> None:
+    """A failed solve must never be installed silently: rocSOLVER reports
+    divide-and-conquer failures only in a device ``info`` flag, which the
+    host never reads.  One fused finiteness check over every result (one
+    host read-back per refresh, which is already synchronised by the warm
+    acceptance test); a non-finite factor is re-solved by torch's float64
+    eigh (the reference's routine, kfac/layers/eigen.py:294-347) and logged.
+    ``KFAC_EIGH_CHECK=0`` skips the check."""
+    if not idxs or os.environ.get('KFAC_EIGH_CHECK', '1') == '0':
+        return
+    # results are views of a few per-bucket stacks: check each stack once
+    bases: dict[int, torch.Tensor] = {}
+    for i in idxs:
+        for t in out[i]:
+            b = t._base if t._base is not None else t
+            bases.setdefault(id(b), b)
+    ok = torch.stack([torch.isfinite(b).all() for b in bases.values()]).all()
+    if bool(ok):
+        return
+    flags = torch.stack([
+        torch.isfinite(out[i][0]).all() & torch.isfinite(out[i][1]).all() for i in idxs
+    ])
+    bad = [i for i, good in zip(idxs, flags.tolist()) if not good]
+    if not bad:
+        return
+    logger.warning('eigendecomposition: %d non-finite result(s) (sizes %s); '
+                   're-solving with torch float64 eigh', len(bad),
+                   sorted({int(mats[i].shape[0]) for i in bad}))
+    for i in bad:
+        d, q = torch.linalg.eigh(mats[i].double())
+        out[i] = (d.float(), q.float())
 
 
 def _settle_warm(gpu: list, stacks: dict, warms: dict, out: dict) -> list:

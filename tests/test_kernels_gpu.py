@@ -553,3 +553,26 @@ def test_syrk_fp32_input_modes(cuda, exact):
     rel = (out.double() - ref).abs().max().item() / ref.abs().max().item()
     assert rel < (2e-6 if exact else 1e-5), rel
     assert torch.equal(out, out.t())
+
+
+def test_eigh_many_repairs_nonfinite_results(cuda, monkeypatch):
+    """A solver result with NaN (e.g. a divide-and-conquer failure that
+    rocSOLVER reports only on the device) is detected and re-solved."""
+    torch.manual_seed(13)
+    mats = []
+    for n in (200, 300):
+        x = torch.randn(n, 2 * n, device=cuda)
+        mats.append(x @ x.t() / (2 * n))
+    real = linalg._launch_jobs
+
+    def broken(gpu, stacks, dev, warms=None):
+        res = real(gpu, stacks, dev, warms)
+        k = sorted(res)[0]
+        d, q = res[k]
+        res[k] = (d, torch.full_like(q, float('nan')))
+        return res
+
+    monkeypatch.setattr(linalg, '_launch_jobs', broken)
+    for m, (d, q) in zip(mats, linalg.eigh_many(mats)):
+        assert torch.isfinite(q).all()
+        _check_eigpairs(m, d, q)
