@@ -4,10 +4,15 @@
 sizes (all K-FAC factors a rank owns) with as little latency as possible:
 
 * matrices are bucketed by size; each bucket is ONE batched call;
-* n <= 64: the LDS-resident parallel Jacobi kernel (csrc/eigh_jacobi.hip),
+* n <= 128: the LDS-resident parallel Jacobi kernel (csrc/eigh_jacobi.hip),
   one matrix per workgroup;
-* n >= ``KFAC_SYTRD_MIN_N`` (default tier, ``KFAC_EIGH_LARGE=sytrd``):
-  the native batched tridiagonalisation (csrc/sytrd.hip).  The factors are
+* a warm bucket (previous eigenbasis available, 128 < n <= 2048, not a
+  chain member) first takes the acceptance test: factors the old basis
+  still diagonalises to 1e-6 keep it with fresh eigenvalues;
+* n >= ``KFAC_SYTRD_MIN_N`` (2000) in buckets of at most
+  ``KFAC_SYTRD_MAX_BATCH`` (8) factors (default tier,
+  ``KFAC_EIGH_LARGE=sytrd``): the native batched tridiagonalisation
+  (csrc/sytrd.hip).  The factors are
   grouped into chains by size (``KFAC_SYTRD_SPLIT``, default: n >= 4000 and
   the rest), each chain on its own lane advancing every member one column
   per launch pair; a chain is issued in segments ending where each bucket
@@ -15,8 +20,13 @@ sizes (all K-FAC factors a rank owns) with as little latency as possible:
   UT back-transform ``apply_q_blocked`` (3 batched fp32 GEMMs per 512
   reflectors; 4-8x faster than rocSOLVER ``ormtr``: 3 x 4608 in 11 vs
   39 ms, profiles/tail_probe_r2.jsonl) -- runs on another lane while the
-  chain continues.  Real step-100 ResNet-50 refresh: 290 ms vs 355 ms for
-  syevd (profiles/refresh_probe_r2_chains.jsonl);
+  chain continues.  The largest chain and its tail run on high-priority
+  lanes.  Real step-100 ResNet-50 refresh: 276 ms vs 329-361 ms for syevd
+  (profiles/refresh_probe_r2_chains.jsonl, profiles/refresh_trace_r2.txt);
+  every result is checked for finiteness once per refresh
+  (``_repair_nonfinite``); splitting the largest bucket's tail into one
+  factor per high-priority lane measured slower (336 ms: the tails are host-
+  and GIL-bound, profiles/tail_split_negative_r2.txt);
 * other n: direct batched rocSOLVER ``syevd`` calls from C++
   (csrc/solver.cpp) which, unlike ``torch.linalg.eigh``, never synchronise
   the host;
