@@ -328,6 +328,9 @@ def run(args: argparse.Namespace, use_kfac: bool, rank: int, world: int,
             out['graph_captures'] = g.captures
         mem = precond.memory_usage()
         out['kfac_memory_mb'] = round(mem['total'] / 1e6, 1)
+    # numerical health of the timed run (one read-back, after the timing)
+    out['params_finite'] = bool(torch.stack(
+        [torch.isfinite(p_).all() for p_ in model.parameters()]).all())
     del model, opt, precond
     torch.cuda.empty_cache()
     return out
@@ -408,7 +411,8 @@ def main() -> None:
     if base is not None and 'step_graphs' in base:
         line['sgd_step_graphs'] = base['step_graphs']
     for k in ('phase_ms_per_step', 'phase_counts', 'kfac_layers', 'step_graphs',
-              'kfac_memory_mb', 'kfac_steps_end', 'align_steps', 'inverse_ms_each'):
+              'kfac_memory_mb', 'kfac_steps_end', 'align_steps', 'inverse_ms_each',
+              'params_finite'):
         if k in res:
             line[k] = res[k]
     if rank == 0:

@@ -319,10 +319,15 @@ def _repair_nonfinite(mats: list[torch.Tensor], out: list, idxs: list[int]) -> N
     bad = [i for i, good in zip(idxs, flags.tolist()) if not good]
     if not bad:
         return
-    logger.warning('eigendecomposition: %d non-finite result(s) (sizes %s); '
-                   're-solving with torch float64 eigh', len(bad),
-                   sorted({int(mats[i].shape[0]) for i in bad}))
-    for i in bad:
+    # a non-finite FACTOR (NaN / Inf gradients upstream) cannot be repaired
+    # here: its results stay non-finite, as torch's eigh would fail on it
+    fin = torch.stack([torch.isfinite(mats[i]).all() for i in bad]).tolist()
+    fixable = [i for i, f in zip(bad, fin) if f]
+    logger.warning('eigendecomposition: %d non-finite result(s) (sizes %s), %d of them '
+                   'from non-finite factors; re-solving the others with torch float64 '
+                   'eigh', len(bad), sorted({int(mats[i].shape[0]) for i in bad}),
+                   len(bad) - len(fixable))
+    for i in fixable:
         d, q = torch.linalg.eigh(mats[i].double())
         out[i] = (d.float(), q.float())
 
