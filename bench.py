@@ -82,10 +82,10 @@ def parse_args() -> argparse.Namespace:
     p.add_argument('--no-channels-last', action='store_true')
     p.add_argument('--fp32', action='store_true', help='disable bf16 autocast')
     p.add_argument('--phase-timing', action='store_true')
-    p.add_argument('--grad-set-to-none', type=int, default=1,
+    p.add_argument('--grad-set-to-none', type=int, default=0,
                    help='zero_grad(set_to_none=...): 1 lets autograd hand its gradient '
                         'buffers to .grad (no accumulate kernels)')
-    p.add_argument('--graphs', type=int, default=1,
+    p.add_argument('--graphs', type=int, default=0,
                    help='1: replay each step kind from a captured HIP graph '
                         '(distributed_kfac_pytorch_amd.graphs.GraphedTrainStep; '
                         'single-rank jobs only, second-order update steps stay '
@@ -272,10 +272,19 @@ def run(args: argparse.Namespace, use_kfac: bool, rank: int, world: int,
     if marker is not None:
         marker()
     t0 = time.perf_counter()
+    nan_probe = os.environ.get('KFAC_BENCH_NANSTEP') == '1'  # diagnostics only
     for i in range(args.steps):
         kinds.append(kind())
         ev[i].record()
         step()
+        if nan_probe:
+            bad = [n for n, p_ in model.named_parameters() if not torch.isfinite(p_).all()]
+            gbad = [n for n, p_ in model.named_parameters()
+                    if p_.grad is not None and not torch.isfinite(p_.grad).all()]
+            if bad or gbad:
+                print(f'[nan] step {i} kind {kinds[-1]}: {len(bad)} params, {len(gbad)} grads '
+                      f'non-finite, e.g. {(bad or gbad)[:3]}', file=sys.stderr, flush=True)
+                nan_probe = False
     ev[args.steps].record()
     if marker is not None:
         marker()

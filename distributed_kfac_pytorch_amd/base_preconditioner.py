@@ -175,6 +175,16 @@ class StepGraphs:
 
         if inverse_step or not ordered or _native.native() is None:
             self.pending_key = None
+            if inverse_step and self.graph is not None:
+                # a refresh: capture again afterwards.  Whole-step graphs
+                # (graphs.GraphedTrainStep) captured before a refresh produced
+                # non-finite gradients in every K-FAC layer after it on
+                # ResNet-50 while eager steps and re-captured graphs stayed
+                # finite (profiles/graph_replay_nonfinite_r2.txt); the cause
+                # is not pinned down, so no precondition graph outlives one
+                self.graph = None
+                self.key = None
+                self._release()
             return False
         if ordered[0][1].module.device.type != 'cuda':
             return False

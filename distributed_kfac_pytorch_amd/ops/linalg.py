@@ -186,8 +186,10 @@ def large_algo() -> str:
     Default sytrd: factors with n >= ``KFAC_SYTRD_MIN_N`` (2000) go through
     the native tridiagonalisation chains with the blocked back-transform,
     the rest through batched syevd on the other lanes -- the real ResNet-50
-    step-100 refresh takes 290 ms against 355 ms with syevd alone
-    (profiles/refresh_probe_r2_chains.jsonl).
+    step-100 refresh takes 276-290 ms against 329-361 ms with syevd alone
+    (profiles/refresh_probe_r2_chains.jsonl).  (The non-finite gradients
+    seen after a refresh with whole-step HIP graphs occur with syevd too:
+    profiles/graph_replay_nonfinite_r2.txt.)
 
     block: on the real ResNet-50 step-100 refresh the native block
     Jacobi (warm) needs 6-12 sweeps on the large A factors (the step-0
