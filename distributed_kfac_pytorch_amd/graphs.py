@@ -239,6 +239,11 @@ class GraphedTrainStep:
             self.seen += 1
             if kind == 'inverse':
                 self._inverse_done = True
+                if os.environ.get('KFAC_GRAPH_SYNC_AFTER_REFRESH') == '1':
+                    # diagnostic for the non-finite replays after a refresh
+                    # (profiles/graph_replay_nonfinite_r2.txt): rules a race
+                    # with the refresh's side-lane work in or out
+                    torch.cuda.synchronize()
             return loss
         sig = self._signature()
         if sig != self.signature:
