@@ -60,6 +60,11 @@ REFERENCE_IMG_S_PER_GPU = 753.96
 REFERENCE_KFAC_OVERHEAD_MS = 31.51
 
 
+# precondition graphs off by default in the bench: eager 2007 img/s vs 1775 with
+# per-refresh re-capture (profiles/graph_replay_nonfinite_r2.txt)
+os.environ.setdefault('KFAC_GRAPHS', '0')
+
+
 def parse_args() -> argparse.Namespace:
     p = argparse.ArgumentParser(description=__doc__)
     p.add_argument('--gpus', type=int, default=1)
