@@ -54,15 +54,13 @@ from distributed_kfac_pytorch_amd.ops.cast import enable_fused_weight_cast  # no
 # (profiles/bench_reference_impl_mi355x_1gpu_r1c.json; 728.91 and 729.89
 # under the earlier harness settings).  For N GPUs the comparison point is
 # the reference's linear-scaling upper bound N * 753.96.
-REFERENCE_IMG_S_PER_GPU = 753.96
+# bf16 (autocast) row; the fp32 row (the reference's ImageNet default, no
+# --fp16) is measured the same way with --dtype fp32.  None = not measured.
+REFERENCE_IMG_S_PER_GPU = {'bf16': 753.96, 'fp32': None}
 # the reference's K-FAC-only cost on the same box and harness: 42.44 ms/step
-# with K-FAC minus 10.93 ms/step for its own SGD step
-REFERENCE_KFAC_OVERHEAD_MS = 31.51
+# with K-FAC minus 10.93 ms/step for its own SGD step (bf16)
+REFERENCE_KFAC_OVERHEAD_MS = {'bf16': 31.51, 'fp32': None}
 
-
-# precondition graphs off by default in the bench: eager 2007 img/s vs 1775 with
-# per-refresh re-capture (profiles/graph_replay_nonfinite_r2.txt)
-os.environ.setdefault('KFAC_GRAPHS', '0')
 
 
 def parse_args() -> argparse.Namespace:
@@ -85,12 +83,20 @@ def parse_args() -> argparse.Namespace:
     p.add_argument('--baseline', type=int, default=1,
                    help='also time plain SGD and report the K-FAC overhead')
     p.add_argument('--no-channels-last', action='store_true')
-    p.add_argument('--fp32', action='store_true', help='disable bf16 autocast')
+    p.add_argument('--dtype', default='fp32', choices=['fp32', 'bf16'],
+                   help='model compute dtype of the headline run: fp32 (the reference '
+                        'ImageNet default, examples/torch_imagenet_resnet.py:73-76 --fp16 '
+                        'off) or bf16 autocast')
+    p.add_argument('--fp32', action='store_true', help='alias of --dtype fp32')
+    p.add_argument('--bf16', action='store_true', help='alias of --dtype bf16')
+    p.add_argument('--secondary-bf16', type=int, default=1,
+                   help='with an fp32 headline, also time the same K-FAC config '
+                        'under bf16 autocast and report it as bf16_* fields')
     p.add_argument('--phase-timing', action='store_true')
     p.add_argument('--grad-set-to-none', type=int, default=0,
                    help='zero_grad(set_to_none=...): 1 lets autograd hand its gradient '
                         'buffers to .grad (no accumulate kernels)')
-    p.add_argument('--graphs', type=int, default=0,
+    p.add_argument('--graphs', type=int, default=1,
                    help='1: replay each step kind from a captured HIP graph '
                         '(distributed_kfac_pytorch_amd.graphs.GraphedTrainStep; '
                         'single-rank jobs only, second-order update steps stay '
@@ -158,13 +164,13 @@ def _profile_marker(dev: torch.device):  # type: ignore[no-untyped-def]
 
 
 def run(args: argparse.Namespace, use_kfac: bool, rank: int, world: int,
-        dev: torch.device) -> dict:
+        dev: torch.device, amp: bool) -> dict:
     torch.manual_seed(1234 + rank)
     model = get_model(args.model).to(dev)
     cl = not args.no_channels_last
     if cl:
         model = model.to(memory_format=torch.channels_last)
-    if args.fused_weight_cast and args.impl == 'native' and not args.fp32:
+    if args.fused_weight_cast and args.impl == 'native' and amp:
         # bf16 weight copies / fp32 weight gradients by multi-tensor launches
         # instead of autocast's per-weight casts (ops/cast.py)
         enable_fused_weight_cast(model)
@@ -219,7 +225,6 @@ def run(args: argparse.Namespace, use_kfac: bool, rank: int, world: int,
         x.copy_(pool_x[i])
         y.copy_(pool_y[i])
     crit = torch.nn.CrossEntropyLoss(label_smoothing=0.1)
-    amp = not args.fp32
 
     use_graphs = bool(args.graphs) and args.impl == 'native' and world == 1
 
@@ -301,6 +306,7 @@ def run(args: argparse.Namespace, use_kfac: bool, rank: int, world: int,
     for k in ('plain', 'factor', 'inverse'):
         v = [t for t, kk in zip(per_step, kinds) if kk == k]
         by_kind[k] = (sum(v) / len(v)) if v else 0.0
+    by_kind_local = dict(by_kind)
     t = torch.tensor([elapsed, by_kind['plain'], by_kind['factor'], by_kind['inverse']],
                      device=dev, dtype=torch.float64)
     if world > 1:
@@ -342,9 +348,20 @@ def run(args: argparse.Namespace, use_kfac: bool, rank: int, world: int,
             out['graph_captures'] = g.captures
         mem = precond.memory_usage()
         out['kfac_memory_mb'] = round(mem['total'] / 1e6, 1)
-    # numerical health of the timed run (one read-back, after the timing)
-    out['params_finite'] = bool(torch.stack(
-        [torch.isfinite(p_).all() for p_ in model.parameters()]).all())
+    # numerical health of the timed run (one read-back, after the timing),
+    # over every rank
+    fin = torch.stack([torch.isfinite(p_).all() for p_ in model.parameters()]).all()
+    fin = fin.to(torch.int32).reshape(1)
+    if world > 1:
+        dist.all_reduce(fin, op=dist.ReduceOp.MIN)
+    out['params_finite'] = bool(fin.item())
+    if precond is not None and world > 1:
+        # per-rank refresh cost: KAISA places each factor's decomposition on
+        # one rank, so the slowest rank sets the refresh step
+        mine = torch.tensor([by_kind_local.get('inverse', 0.0)], device=dev, dtype=torch.float64)
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        out['refresh_ms_per_rank'] = [round(float(t.item()), 1) for t in allr]
     del model, opt, precond
     torch.cuda.empty_cache()
     return out
@@ -352,33 +369,44 @@ def run(args: argparse.Namespace, use_kfac: bool, rank: int, world: int,
 
 def main() -> None:
     args = parse_args()
+    if args.bf16:
+        args.dtype = 'bf16'
+    if args.fp32:
+        args.dtype = 'fp32'
+    amp = args.dtype == 'bf16'
     rank, world, dev = setup(args)
     if world != args.gpus and rank == 0:
         print(f'[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}',
               file=sys.stderr)
-    res = run(args, not args.no_kfac, rank, world, dev)
+    res = run(args, not args.no_kfac, rank, world, dev, amp)
     base = None
     if args.baseline and not args.no_kfac:
-        base = run(args, False, rank, world, dev)
+        base = run(args, False, rank, world, dev, amp)
+    sec = None
+    if args.secondary_bf16 and not amp and not args.no_kfac:
+        sec = run(args, True, rank, world, dev, True)
     gb = args.batch_size * world
     window_value = gb * args.steps / res['seconds']
     # headline: period-averaged throughput (the reference baseline was timed
     # over whole 100-step periods); without K-FAC the window value
     ms = res.get('period_ms_per_step', res['ms_per_step'])
     value = gb * 1e3 / ms
+    ref_per_gpu = REFERENCE_IMG_S_PER_GPU[args.dtype]
     line = {
         'impl': args.impl,
         'metric': 'images/sec (whole node), ResNet-50 ImageNet K-FAC training',
         'value': round(value, 2),
         'unit': 'images/s',
         'n_gpus': world,
+        'world_size': dist.get_world_size() if dist.is_initialized() else 1,
         'steps': args.steps,
         'warmup': args.warmup,
         'ms_per_step': round(ms, 3),
         'higher_is_better': True,
         'scaling': 'weak',
-        'vs_baseline': round(value / (REFERENCE_IMG_S_PER_GPU * world), 4),
-        'dtype': 'fp32' if args.fp32 else 'bf16',
+        'vs_baseline': round(value / (ref_per_gpu * world), 4) if ref_per_gpu else None,
+        'baseline_img_s_per_gpu': ref_per_gpu,
+        'dtype': args.dtype,
         'data': 'synthetic (random 224x224 images / labels, random-init '
                 'weights)',
         'config': {
@@ -397,8 +425,9 @@ def main() -> None:
                 'kl_clip': args.kfac_kl_clip,
             },
             'channels_last': not args.no_channels_last,
-            'fused_weight_cast': bool(args.fused_weight_cast) and not args.fp32,
+            'fused_weight_cast': bool(args.fused_weight_cast) and amp,
             'sgd_impl': args.sgd_impl,
+            'graphs': bool(args.graphs) and world == 1,
         },
         'timing': (
             'period-averaged: the timed window of exactly `steps` steps starts on '
@@ -420,13 +449,23 @@ def main() -> None:
         line['sgd_images_per_sec'] = round(gb * args.steps / base['seconds'], 2)
         line['kfac_overhead_ms'] = round(ms - base['ms_per_step'], 3)
         # the reference kfac_pytorch on the same MI355X and harness
-        # (profiles/bench_reference_impl_mi355x_1gpu_r1c.json)
-        line['reference_kfac_overhead_ms'] = REFERENCE_KFAC_OVERHEAD_MS
+        # 
+        line['reference_kfac_overhead_ms'] = REFERENCE_KFAC_OVERHEAD_MS[args.dtype]
+        line['sgd_params_finite'] = base['params_finite']
     if base is not None and 'step_graphs' in base:
         line['sgd_step_graphs'] = base['step_graphs']
+    if sec is not None:
+        ms2 = sec.get('period_ms_per_step', sec['ms_per_step'])
+        v2 = gb * 1e3 / ms2
+        line['bf16'] = {
+            'value': round(v2, 2), 'ms_per_step': round(ms2, 3),
+            'vs_baseline': round(v2 / (REFERENCE_IMG_S_PER_GPU['bf16'] * world), 4),
+            'kind_ms': sec['kind_ms'], 'params_finite': sec['params_finite'],
+            'eigen_refresh_ms': round(sec.get('refresh_ms', 0.0), 3),
+        }
     for k in ('phase_ms_per_step', 'phase_counts', 'kfac_layers', 'step_graphs',
               'kfac_memory_mb', 'kfac_steps_end', 'align_steps', 'inverse_ms_each',
-              'params_finite'):
+              'refresh_ms_per_rank', 'params_finite'):
         if k in res:
             line[k] = res[k]
     if rank == 0:

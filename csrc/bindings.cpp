@@ -1022,6 +1022,10 @@ at::Tensor bn_act(const at::Tensor& x, const at::Tensor& weight, const at::Tenso
                         num_batches, momentum, eps, relu, has_res);
 }
 
+// tridiag_host.cpp
+std::vector<at::Tensor> tridiag_eigh_dc(const at::Tensor& d, const at::Tensor& e);
+std::vector<int64_t> tridiag_dc_plan(int64_t n);
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "MI355X (gfx950) HIP kernels for distributed K-FAC";
   m.def("triu_pack", &triu_pack);
@@ -1089,5 +1093,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("A"), py::arg("Q0") = py::none(), py::arg("max_sweeps") = 12,
         py::arg("tol") = 1e-6, py::arg("inner_sweeps") = 2, py::arg("noise") = 4e-6,
         py::arg("refine") = true);
+  m.def("tridiag_eigh_dc", &tridiag_eigh_dc, py::call_guard<py::gil_scoped_release>());
+  m.def("tridiag_dc_plan", &tridiag_dc_plan);
   m.attr("arch") = "gfx950";
 }

@@ -188,6 +188,11 @@ class StepGraphs:
             return False
         if ordered[0][1].module.device.type != 'cuda':
             return False
+        if type(pre)._precondition_all is not BaseKFACPreconditioner._precondition_all:
+            # a subclass with its own precondition phase (NeoX: gather to the
+            # primary, GEMMs, scatter back) -- replaying only the GEMMs would
+            # skip the collectives its model-parallel peers enter
+            return False
         if torch.cuda.is_current_stream_capturing():
             # inside a whole-step capture (graphs.GraphedTrainStep): the
             # eager launches are recorded into the outer graph
@@ -695,6 +700,8 @@ class BaseKFACPreconditioner:
             return
         if self._accumulation_steps != 1 or get_world_size() > 1:
             return
+        if any(getattr(l, '_scaler', None) is not None for _, l in ordered):
+            return  # a GradScaler unscales the gradients after backward
         if type(self)._precondition_all is not BaseKFACPreconditioner._precondition_all:
             return  # a subclass with its own precondition phase (NeoX)
         if self._assignment.broadcast_gradients() or not pops.grouped_gemm_enabled():
@@ -726,7 +733,7 @@ class BaseKFACPreconditioner:
         for p in params:
             self._hook_handles.append(p.register_post_accumulate_grad_hook(self._early_ready))
         self._early.update(
-            names=names, total=len(params), grouped=pops.make_grouped(),
+            names=names, total=len(params), grouped=pops.make_grouped(), params=params,
             layers=[l for n, l in workers if n in names],
             stream=torch.cuda.Stream(device=workers[0][1].module.device),
         )
@@ -740,6 +747,10 @@ class BaseKFACPreconditioner:
             return
         side = st['stream']
         side.wait_stream(torch.cuda.current_stream(side.device))
+        # the side stream reads the gradients now: anything that changes them
+        # before step() (GradScaler.unscale_, clip_grad_norm_) bumps their
+        # version, and _join_early then redoes those layers eagerly
+        st['versions'] = [g._version for g in (p.grad for p in st['params']) if g is not None]
         with torch.cuda.stream(side):
             st['pending'] = bool(st['grouped'].run(st['layers'], self.damping))
 
@@ -752,6 +763,11 @@ class BaseKFACPreconditioner:
         done = set(st['names']) if st['pending'] else set()
         if st['pending']:
             torch.cuda.current_stream(st['stream'].device).wait_stream(st['stream'])
+            now = [g._version for g in (p.grad for p in st['params']) if g is not None]
+            if now != st.get('versions'):
+                # a gradient changed after the early launch (unscale / clip):
+                # the early P is stale, precondition those layers again
+                done = set()
         st['pending'] = False
         st['count'] = 0
         return done

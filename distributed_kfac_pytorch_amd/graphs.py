@@ -214,8 +214,13 @@ class GraphedTrainStep:
         # no Python GC while capturing: collecting an unreachable cycle that
         # holds an old CUDAGraph would destroy that graph mid-capture, which
         # HIP forbids (hipErrorStreamCaptureUnsupported -> abort)
+        pool = None
+        if os.environ.get('KFAC_GRAPH_SHARED_POOL') == '1':  # diagnostics
+            if getattr(self, '_pool', None) is None:
+                self._pool = torch.cuda.graph_pool_handle()
+            pool = self._pool
         with _no_gc(), torch.cuda.stream(side):
-            with torch.cuda.graph(g, stream=side):
+            with torch.cuda.graph(g, pool=pool, stream=side):
                 loss = self.forward_backward()
                 if p is not None:
                     p.step()
@@ -227,7 +232,21 @@ class GraphedTrainStep:
             p._mini_steps = defaultdict(int)
             p._mini_steps_g = defaultdict(int)
         self.graphs[kind] = g
-        self.outputs[kind] = loss
+        # Keep only the loss VALUE (replays rewrite its storage).  Holding the
+        # captured loss itself keeps its autograd graph alive, and with it
+        # every parameter's AccumulateGrad node -- created during the capture
+        # and bound to the capture's side stream.  The next EAGER step (the
+        # second-order refresh) then reuses those nodes: each gradient is
+        # accumulated on that foreign stream while the producing stream has
+        # already recycled the incoming gradient's memory, so the refresh
+        # step folds garbage into the gradients / factors and the replays
+        # after it diverge (profiles/graph_replay_nonfinite_r2.txt; torch
+        # warns "The AccumulateGrad node's stream does not match ...").
+        if os.environ.get('KFAC_GRAPH_KEEP_AUTOGRAD') == '1':  # A/B diagnostic only
+            self.outputs[kind] = loss
+        else:
+            self.outputs[kind] = loss.detach()
+        del loss
         self.grads[kind] = [q.grad for q in self._params()]
         self.captures += 1
 
@@ -258,7 +277,11 @@ class GraphedTrainStep:
             if self.seen < self.warmup or not self._capturable():
                 self.seen += 1
                 return self._eager()
-            for k in ('plain', 'factor') if self.preconditioner is not None else ('plain',):
+            kinds = ('plain', 'factor') if self.preconditioner is not None else ('plain',)
+            only = os.environ.get('KFAC_GRAPH_KINDS')  # diagnostics: capture a subset
+            if only:
+                kinds = tuple(k for k in kinds if k in only.split(','))
+            for k in kinds:
                 if k not in self.graphs:
                     try:
                         self._capture(k)
@@ -274,6 +297,8 @@ class GraphedTrainStep:
                 return self._eager()
         with tracing.phase(f'step(graph:{kind})'):
             self.graphs[kind].replay()
+        if os.environ.get('KFAC_GRAPH_SYNC') == '1':  # diagnostics
+            torch.cuda.synchronize()
         # expose this graph's gradients as .grad (each kind has its own)
         for q, gr in zip(self._params(), self.grads[kind]):
             q.grad = gr

@@ -117,15 +117,27 @@ class _FusedCast(torch.autograd.Function):
         return (None, *out)
 
 
-def _conv_forward(self: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
+def _copies(self: nn.Module) -> dict | None:
+    """This forward's fused bf16 copies, only inside the autocast region
+    they were made for (a call outside it runs the plain forward)."""
     c = self.__dict__.get('_fused_cast')
+    if c is None or 'weight' not in c:
+        return None
+    dt = c['device_type']
+    if not torch.is_autocast_enabled(dt) or torch.get_autocast_dtype(dt) != c['dtype']:
+        return None
+    return c
+
+
+def _conv_forward(self: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
+    c = _copies(self)
     if c is None:
         return nn.Conv2d.forward(self, x)
     return self._conv_forward(x, c['weight'], c.get('bias'))
 
 
 def _linear_forward(self: nn.Linear, x: torch.Tensor) -> torch.Tensor:
-    c = self.__dict__.get('_fused_cast')
+    c = _copies(self)
     if c is None:
         return nn.Linear.forward(self, x)
     return torch.nn.functional.linear(x, c['weight'], c.get('bias'))
@@ -175,6 +187,10 @@ class FusedWeightCast:
                 and torch.get_autocast_dtype(self.device_type) == self.dtype)
 
     def _before(self, module: nn.Module, args: Any) -> None:
+        # copies left behind by a forward that raised (e.g. OOM) must never
+        # be used by a later forward
+        for m in self.mods:
+            m.__dict__.pop('_fused_cast', None)
         if not self._active():
             return
         for group in self.groups:
@@ -183,7 +199,9 @@ class FusedWeightCast:
                 continue
             outs = _FusedCast.apply(self.dtype, *ps)
             for (m, n), o in zip(group, outs):
-                m.__dict__.setdefault('_fused_cast', {})[n] = o
+                c = m.__dict__.setdefault('_fused_cast', {'device_type': self.device_type,
+                                                          'dtype': self.dtype})
+                c[n] = o
 
     def _after(self, module: nn.Module, args: Any, output: Any) -> None:
         for m in self.mods:

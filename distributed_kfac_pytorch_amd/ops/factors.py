@@ -53,6 +53,12 @@ def fp32_exact() -> bool:
     return os.environ.get('KFAC_SYRK_FP32', 'bf16x3').lower() == 'exact'
 
 
+def _splits() -> int:
+    """Split-K slab count of the SYRK (``KFAC_SYRK_SPLITS``; 0 = the
+    kernel's own choice, 1 = no split-K workspace)."""
+    return int(os.environ.get('KFAC_SYRK_SPLITS', '0'))
+
+
 def packed_dim(out: torch.Tensor) -> int:
     """D of a packed D x D upper triangle held in the 1-D ``out``."""
     n = out.numel()
@@ -101,7 +107,8 @@ def cov_accumulate_(
             xin = xin.float()
         if xin.stride(1) != 1 or (xin.shape[0] > 1 and xin.stride(0) < xin.shape[1]):
             xin = xin.contiguous()
-        native().syrk(xin, out, bias, float(alpha), float(beta), 0, alpha_scale, fp32_exact())
+        native().syrk(xin, out, bias, float(alpha), float(beta), _splits(), alpha_scale,
+                      fp32_exact())
         return out
     if out.dim() == 1:
         _packed_emulate_(out, lambda dense: _torch_cov_accumulate_(
@@ -142,8 +149,8 @@ def conv_cov_accumulate_(
     ):
         return False
     native().syrk_conv(x, out, kernel[0], kernel[1], stride[0], stride[1],
-                       padding[0], padding[1], bias, float(alpha), float(beta), 0, None,
-                       fp32_exact())
+                       padding[0], padding[1], bias, float(alpha), float(beta), _splits(),
+                       None, fp32_exact())
     return True
 
 

@@ -537,9 +537,20 @@ def _tail_job(stream: torch.cuda.Stream, ev: torch.cuda.Event, red: torch.Tensor
         if _q_back_transform() == 'rocsolver':
             w, x = native().tridiag_eigvecs(red, d, e, tau)
             return w.clone(), x
+        if tridiag_solver() == 'dc':
+            n = d.shape[-1]
+            w, z = native().tridiag_eigh_dc(d, e[:, :max(n - 1, 0)])
+            return w, apply_q_blocked(red, tau, z)
         w, z = native().tridiag_stedc(d, e)
         # d is the chain's persistent buffer when replayed from graphs
         return w.clone(), apply_q_blocked(red, tau, z)
+
+
+def tridiag_solver() -> str:
+    """Eigensolver of the reduced tridiagonal: ``KFAC_EIGH_TRIDIAG`` = dc
+    (native divide and conquer, csrc/tridiag.hip; default) | stedc
+    (rocSOLVER)."""
+    return os.environ.get('KFAC_EIGH_TRIDIAG', 'dc')
 
 
 def _chain_groups(keys: list) -> list[list]:

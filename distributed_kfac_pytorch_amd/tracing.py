@@ -18,6 +18,7 @@ from __future__ import annotations
 import contextlib
 import logging
 import os
+import sys
 import time
 from collections import defaultdict
 from typing import Any
@@ -166,6 +167,9 @@ def enable_phase_timing(enable: bool = True) -> PhaseTimer | None:
     return _PHASE_TIMER
 
 
+_DEBUG_SYNC = os.environ.get('KFAC_DEBUG_SYNC') == '1'
+
+
 def phase_timer() -> PhaseTimer | None:
     """The global phase timer, or None when phase timing is off."""
     return _PHASE_TIMER
@@ -176,6 +180,13 @@ def phase(name: str) -> Iterator[None]:
     """Record a K-FAC phase on the global timer (no-op when disabled, and
     while a HIP graph is being captured: event timing is not capturable)."""
     timer = _PHASE_TIMER
+    if _DEBUG_SYNC and torch.cuda.is_available() and not torch.cuda.is_current_stream_capturing():
+        # KFAC_DEBUG_SYNC=1: synchronise after every phase so an asynchronous
+        # device fault is reported by the phase that caused it
+        yield
+        torch.cuda.synchronize()
+        print(f'[kfac-sync] {name} ok', file=sys.stderr, flush=True)
+        return
     if timer is None or (
         torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
     ):

@@ -63,6 +63,30 @@ def test_fused_cast_groups_follow_backward_order() -> None:
     h.remove()
 
 
+def test_fused_cast_stale_copies_never_used() -> None:
+    """A forward that raises leaves its bf16 copies behind; later forwards
+    (inside or outside autocast) must not use them."""
+    net = _net()
+    h = cast_ops.enable_fused_weight_cast(net, device_type='cpu')
+    x = torch.randn(2, 3, 8, 8)
+    with pytest.raises(RuntimeError):
+        with torch.autocast('cpu', dtype=torch.bfloat16):
+            net(x[:, :2])  # wrong channel count: the first conv raises
+    assert '_fused_cast' in net[0].__dict__  # left behind by the failed forward
+    with torch.no_grad():
+        net[0].weight.add_(1.0)  # an optimizer update after the failure
+    out = net(x)  # outside autocast: plain fp32 forward
+    assert out.dtype == torch.float32
+    ref = nn.Sequential(*[m for m in _net()])
+    ref.load_state_dict(net.state_dict())
+    torch.testing.assert_close(out, ref(x))
+    with torch.autocast('cpu', dtype=torch.bfloat16):
+        o2 = net(x)
+        o3 = ref(x)
+    assert torch.equal(o2.float(), o3.float())
+    h.remove()
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize('channels_last', [False, True])
 @pytest.mark.parametrize('group_mb', [25.0, 0.001])

@@ -1,0 +1,141 @@
+"""Locate where whole-step graph replay departs from eager execution.
+
+Runs the configuration of tests/test_graphs_refresh_gpu.py (ResNet-50 at
+64x64, fused BN / weight casts, bf16 autocast, channels_last, factor side
+stream) through ``GraphedTrainStep`` in lockstep with an eager twin, and after
+every step prints one JSON line: per state category, the number of non-finite
+tensors and the largest relative difference to the eager twin.
+
+    python tools/graph_nan_probe.py [--steps 6] [--fp32]
+"""
+from __future__ import annotations
+
+import argparse
+import copy
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import distributed_kfac_pytorch_amd as kfac  # noqa: E402
+from distributed_kfac_pytorch_amd.graphs import GraphedTrainStep  # noqa: E402
+from distributed_kfac_pytorch_amd.models.resnet import resnet50  # noqa: E402
+from distributed_kfac_pytorch_amd.ops.cast import enable_fused_weight_cast  # noqa: E402
+
+
+def build(base, dev, graphs: bool, amp: bool, fused_cast: bool):  # type: ignore[no-untyped-def]
+    model = copy.deepcopy(base).to(dev).to(memory_format=torch.channels_last)
+    if fused_cast and amp:
+        enable_fused_weight_cast(model)
+    opt = torch.optim.SGD(model.parameters(), lr=0.01, momentum=0.9, weight_decay=5e-5)
+    pre = kfac.KFACPreconditioner(
+        model, factor_update_steps=2, inv_update_steps=8, damping=0.001, kl_clip=0.001,
+        lr=lambda s: opt.param_groups[0]['lr'], grad_worker_fraction=0.5)
+    x = torch.empty(8, 3, 64, 64, device=dev).contiguous(memory_format=torch.channels_last)
+    y = torch.empty(8, dtype=torch.long, device=dev)
+    crit = torch.nn.CrossEntropyLoss(label_smoothing=0.1)
+
+    def fb() -> torch.Tensor:
+        with torch.autocast('cuda', dtype=torch.bfloat16, enabled=amp, cache_enabled=not graphs):
+            loss = crit(model(x), y)
+        loss.backward()
+        return loss
+
+    if graphs:
+        runner = GraphedTrainStep(fb, opt, pre, warmup=1, enabled=True)
+    else:
+        def runner() -> torch.Tensor:
+            opt.zero_grad(set_to_none=False)
+            loss = fb()
+            pre.step()
+            opt.step()
+            return loss.detach()
+    return model, opt, pre, x, y, runner
+
+
+def state(model, opt, pre) -> dict:  # type: ignore[no-untyped-def]
+    cats: dict[str, list] = {k: [] for k in (
+        'param', 'grad', 'momentum', 'buffer', 'factor', 'basis', 'dgda', 'pbuf', 'img')}
+    for p in model.parameters():
+        cats['param'].append(p)
+        if p.grad is not None:
+            cats['grad'].append(p.grad)
+        st = opt.state.get(p, {})
+        if 'momentum_buffer' in st and st['momentum_buffer'] is not None:
+            cats['momentum'].append(st['momentum_buffer'])
+    for b in model.buffers():
+        if b.is_floating_point():
+            cats['buffer'].append(b)
+    for _, layer in pre._layers.values():
+        for t in (layer.a_factor, layer.g_factor):
+            if t is not None:
+                cats['factor'].append(t)
+        for t in (getattr(layer, 'qa', None), getattr(layer, 'qg', None)):
+            if t is not None:
+                cats['basis'].append(t)
+        if getattr(layer, 'dgda', None) is not None:
+            cats['dgda'].append(layer.dgda)
+        if layer._grad_buf is not None:
+            cats['pbuf'].append(layer._grad_buf)
+        st = getattr(layer, '_g3s', None)
+        if st:
+            for k in ('fa', 'fg'):
+                cats['img'].append(st[k])
+    return cats
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--steps', type=int, default=6)
+    ap.add_argument('--fp32', action='store_true')
+    ap.add_argument('--fused-cast', type=int, default=1)
+    ap.add_argument('--deterministic', type=int, default=1)
+    args = ap.parse_args()
+    torch.backends.cudnn.deterministic = bool(args.deterministic)
+    dev = torch.device('cuda')
+    torch.manual_seed(0)
+    base = resnet50(num_classes=10)
+    A = build(base, dev, True, not args.fp32, bool(args.fused_cast))
+    B = build(base, dev, False, not args.fp32, bool(args.fused_cast))
+    gen = torch.Generator(device='cpu').manual_seed(1)
+    pool = [(torch.randn(8, 3, 64, 64, generator=gen), torch.randint(0, 10, (8,), generator=gen))
+            for _ in range(4)]
+    env = {k: v for k, v in os.environ.items() if k.startswith('KFAC_')}
+    for i in range(args.steps):
+        kind = A[5].kind()
+        x, y = pool[i % len(pool)]
+        for m in (A, B):
+            m[3].copy_(x)
+            m[4].copy_(y)
+        la = A[5]()
+        lb = B[5]()
+        torch.cuda.synchronize()
+        sa, sb = state(*A[:3]), state(*B[:3])
+        rec: dict = {'step': i, 'kind': kind, 'env': env,
+                     'loss': [float(la), float(lb)]}
+        # per layer: factor and P differences (first 3 worst)
+        per = []
+        for (name, la_), (_, lb_) in zip(A[2]._layers.values(), B[2]._layers.values()):
+            fa = float((la_.a_factor - lb_.a_factor).abs().max() / lb_.a_factor.abs().max())
+            fg = float((la_.g_factor - lb_.g_factor).abs().max() / lb_.g_factor.abs().max())
+            pa, pb_ = la_._grad_buf, lb_._grad_buf
+            pd = float((pa - pb_).abs().max() / pb_.abs().max().clamp_min(1e-30)) \
+                if pa is not None and pb_ is not None else -1.0
+            per.append((max(fa, fg, pd), name, round(fa, 6), round(fg, 6), round(pd, 6)))
+        per.sort(reverse=True)
+        rec['worst_layers'] = per[:3]
+        for k in sa:
+            bad = sum(int(not bool(torch.isfinite(t.float()).all())) for t in sa[k])
+            diffs = [float((a.float() - b.float()).abs().max() / b.float().abs().max().clamp_min(1e-30))
+                     for a, b in zip(sa[k], sb[k]) if a.shape == b.shape]
+            rec[k] = {'nonfinite': bad, 'n': len(sa[k]), 'maxrel': max(diffs) if diffs else None}
+        print(json.dumps(rec), flush=True)
+        if any(rec[k]['nonfinite'] for k in sa):
+            break
+
+
+if __name__ == '__main__':
+    main()
