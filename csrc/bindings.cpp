@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <cstring>
+#include <mutex>
+#include <unordered_map>
 #include <tuple>
 #include <vector>
 
@@ -431,10 +433,39 @@ std::vector<at::Tensor> jacobi_eigh(const at::Tensor& A, int64_t max_sweeps,
 // while the tensors' storages are unchanged.
 // Upload a host-built descriptor table.  `host` is an optional pinned byte
 // buffer owned by the caller (preallocated outside any HIP-graph capture);
-// the copy is a plain hipMemcpyAsync on the current stream, so when the
-// table is built inside a capture it becomes a graph node that re-reads
-// `host` on every replay.  Without `host` a pinned staging tensor is
-// allocated here (not possible while capturing).
+// without it a pinned staging tensor is allocated here.
+//
+// Outside a capture the copy is a plain hipMemcpyAsync on the current stream.
+// INSIDE a capture the table is allocated outside the graph's memory pool and
+// no copy is recorded: the (device table, staging) pair is queued and
+// flush_table_uploads() -- called by every capturing site right after its
+// capture ends -- uploads it once, eagerly, before the graph's first replay.
+// Round 2 allocated the table in the private pool and captured its copy: the
+// pool hands a table's block to other tensors of the same graph, so the table
+// was valid only from its copy node to its last reader within one replay --
+// garbage when used eagerly (an illegal address for an eager step after a
+// capture) and whenever graph work touching the recycled block ran between
+// the copy and the readers (the post-refresh NaN of
+// profiles/graph_replay_nonfinite_r2.txt; tools/graph_nan_probe.py,
+// tools/graph_ptr_audit.py).
+namespace {
+std::mutex g_pending_mu;
+std::vector<std::pair<at::Tensor, at::Tensor>> g_pending_uploads;
+
+// Device twins of the caller's pinned staging slots (ops/precondition.py
+// _TableCache): a table built inside a capture is written into the slot's
+// persistent device buffer -- allocated eagerly, outside every graph pool --
+// so a capture never allocates table memory.
+std::mutex g_slot_mu;
+std::unordered_map<const void*, at::Tensor> g_slot_dev;
+
+bool current_stream_capturing() {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(cur_stream(), &st) != hipSuccess) return false;
+  return st == hipStreamCaptureStatusActive;
+}
+}  // namespace
+
 std::tuple<at::Tensor, at::Tensor> upload_table(
     const void* data, int64_t nbytes, const at::Device& device,
     const c10::optional<at::Tensor>& host) {
@@ -448,11 +479,58 @@ std::tuple<at::Tensor, at::Tensor> upload_table(
                     at::TensorOptions().dtype(at::kByte).pinned_memory(true));
   }
   std::memcpy(cpu.data_ptr(), data, nbytes);
-  auto dev_t = at::empty({std::max<int64_t>(nbytes, 1)},
-                         at::TensorOptions().dtype(at::kByte).device(device));
-  C10_HIP_CHECK(hipMemcpyAsync(dev_t.data_ptr(), cpu.data_ptr(), nbytes,
-                               hipMemcpyHostToDevice, cur_stream()));
+  const bool capturing = current_stream_capturing();
+  at::Tensor dev_t;
+  if (host.has_value()) {
+    std::lock_guard<std::mutex> lk(g_slot_mu);
+    auto it = g_slot_dev.find(host->data_ptr());
+    if (it != g_slot_dev.end() && it->second.numel() >= std::max<int64_t>(nbytes, 1) &&
+        it->second.device() == device)
+      dev_t = it->second.narrow(0, 0, std::max<int64_t>(nbytes, 1));
+  }
+  if (!dev_t.defined()) {
+    // NOT from a graph's private pool: the pool hands a block to other
+    // tensors of the same graph, so a table there would be valid only from
+    // its copy node to its last reader within one replay
+    TORCH_CHECK(!capturing,
+                "descriptor table built during a HIP-graph capture without a "
+                "registered device slot (register_table_slot)");
+    dev_t = at::empty({std::max<int64_t>(nbytes, 1)},
+                      at::TensorOptions().dtype(at::kByte).device(device));
+  }
+  if (capturing) {
+    std::lock_guard<std::mutex> lk(g_pending_mu);
+    g_pending_uploads.emplace_back(dev_t.narrow(0, 0, std::max<int64_t>(nbytes, 1)),
+                                   cpu.narrow(0, 0, std::max<int64_t>(nbytes, 1)));
+  } else {
+    C10_HIP_CHECK(hipMemcpyAsync(dev_t.data_ptr(), cpu.data_ptr(), nbytes,
+                                 hipMemcpyHostToDevice, cur_stream()));
+  }
   return {dev_t, cpu};
+}
+
+// Upload every table built inside the capture that just ended (on the
+// current stream; the pinned-source copies record their stream events, so
+// the staging is never recycled before they ran).  Returns the count.
+void register_table_slot(const at::Tensor& host, const at::Tensor& dev) {
+  TORCH_CHECK(host.is_pinned() && host.scalar_type() == at::kByte && dev.is_cuda() &&
+                  dev.scalar_type() == at::kByte && dev.is_contiguous() &&
+                  dev.numel() >= host.numel(),
+              "register_table_slot: pinned byte host slot and a device byte buffer as large");
+  std::lock_guard<std::mutex> lk(g_slot_mu);
+  g_slot_dev[host.data_ptr()] = dev;
+}
+
+int64_t flush_table_uploads() {
+  std::vector<std::pair<at::Tensor, at::Tensor>> todo;
+  {
+    std::lock_guard<std::mutex> lk(g_pending_mu);
+    todo.swap(g_pending_uploads);
+  }
+  TORCH_CHECK(todo.empty() || !current_stream_capturing(),
+              "flush_table_uploads must run after the capture has ended");
+  for (auto& p : todo) p.first.copy_(p.second, /*non_blocking=*/true);
+  return (int64_t)todo.size();
 }
 
 // Returns (device table, block count, pinned host staging).  The host copy
@@ -1095,5 +1173,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("refine") = true);
   m.def("tridiag_eigh_dc", &tridiag_eigh_dc, py::call_guard<py::gil_scoped_release>());
   m.def("tridiag_dc_plan", &tridiag_dc_plan);
+  m.def("flush_table_uploads", &flush_table_uploads);
+  m.def("register_table_slot", &register_table_slot);
   m.attr("arch") = "gfx950";
 }

@@ -37,7 +37,8 @@ constexpr int SY_NB = 32;                 // panel width
 constexpr int SY_T = 256;                 // threads per block
 constexpr int SY_P1 = 2 * SY_NB + 4;      // partial stride: xn2, dW[NB], dV[NB]
 constexpr int SY_ROWS = 16;               // symv rows per workgroup
-constexpr int SY_RPW = SY_ROWS / (SY_T / 64);  // symv rows per wave (8)
+constexpr int SY_RPW = SY_ROWS / (SY_T / 64);  // symv rows per wave (4)
+constexpr int SY_SU = 4;                  // symv column blocks in flight per row
 constexpr int SY_MAXN = 8192;             // v staged in LDS (32 KiB)
 constexpr int SY_MAXCH = SY_MAXN / SY_T;  // col-step chunks
 constexpr int SY_MAXROWBLK = SY_MAXN / SY_ROWS;
@@ -301,14 +302,38 @@ __global__ void __launch_bounds__(SY_T) sytrd_symv_kernel(
   if ((n & 3) == 0) {
     typedef float f4 __attribute__((ext_vector_type(4)));
     const int nq = span >> 2;
-    for (int q = l; q < nq; q += 64) {
+    // rows past the end read row n-1 (valid memory) and are dropped below,
+    // so the streaming loop has no per-row branch
+    const GLOBAL float* rp[SY_RPW];
+#pragma unroll
+    for (int h = 0; h < SY_RPW; ++h)
+      rp[h] = D.A + (int64_t)(rw + h < n ? rw + h : n - 1) * n + base;
+    // SY_SU column blocks per row in flight together: SY_RPW * SY_SU 16-B
+    // loads per lane before the first FMA (the 1-deep loop kept 4 loads in
+    // flight and streamed the trailing matrix at ~2.5 TB/s)
+    int q = l;
+    for (; q + (SY_SU - 1) * 64 < nq; q += SY_SU * 64) {
+      f4 a4[SY_SU][SY_RPW];
+#pragma unroll
+      for (int u = 0; u < SY_SU; ++u)
+#pragma unroll
+        for (int h = 0; h < SY_RPW; ++h)
+          a4[u][h] = *(const GLOBAL f4*)(rp[h] + 4 * (q + 64 * u));
+#pragma unroll
+      for (int u = 0; u < SY_SU; ++u) {
+        const f4 vv = *reinterpret_cast<const f4*>(sv + 4 * (q + 64 * u));
+#pragma unroll
+        for (int h = 0; h < SY_RPW; ++h)
+          acc[h] += (a4[u][h].x * vv.x + a4[u][h].y * vv.y) +
+                    (a4[u][h].z * vv.z + a4[u][h].w * vv.w);
+      }
+    }
+    for (; q < nq; q += 64) {
       const f4 vv = *reinterpret_cast<const f4*>(sv + 4 * q);
 #pragma unroll
       for (int h = 0; h < SY_RPW; ++h) {
-        if (rw + h < n) {
-          const f4 a4 = *(const GLOBAL f4*)(D.A + (int64_t)(rw + h) * n + base + 4 * q);
-          acc[h] += (a4.x * vv.x + a4.y * vv.y) + (a4.z * vv.z + a4.w * vv.w);
-        }
+        const f4 a = *(const GLOBAL f4*)(rp[h] + 4 * q);
+        acc[h] += (a.x * vv.x + a.y * vv.y) + (a.z * vv.z + a.w * vv.w);
       }
     }
   } else {

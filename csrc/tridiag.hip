@@ -101,7 +101,10 @@ __global__ void __launch_bounds__(DC_T) dc_sort_kernel(
   const int g = blockIdx.x, m = 2 * h;
   const int b = g / S, s = g % S;
   const double* D = Dprev + (int64_t)g * m;
-  for (int i = threadIdx.x; i < m; i += DC_T) sh[i] = D[i];
+  for (int i = threadIdx.x; i < m; i += DC_T) {
+    const double v = D[i];
+    sh[i] = v == v ? v : __builtin_huge_val();
+  }
   const float beta = e_pad[(int64_t)b * (n_pad - 1) + (int64_t)s * m + h - 1];
   const double sgn = beta >= 0.f ? 1.0 : -1.0;
   const double rho = 2.0 * fabs((double)beta);
@@ -387,7 +390,9 @@ __global__ void __launch_bounds__(DC_T) dc_zhat_kernel(
   if (act) {
     di = sd[base + ndidx[base + i]];
     const double ti = tau[base + i];
-    const double doi = ti > 0.0 ? di : sd[base + ndidx[base + i + 1]];
+    // origin j+1 only when tau < 0 AND a next pole exists (NaN-safe: a
+    // non-finite factor must give non-finite results, never a stray index)
+    const double doi = (ti > 0.0 || i == K - 1) ? di : sd[base + ndidx[base + i + 1]];
     prod = ((doi - di) + ti) / rho;
   }
   for (int c0 = 0; c0 < K; c0 += DC_CH) {
@@ -404,7 +409,7 @@ __global__ void __launch_bounds__(DC_T) dc_zhat_kernel(
         const int jj = c0 + q;
         if (jj == i) continue;
         const double tj = ct[q];
-        const double dorg = tj > 0.0 ? cd[q] : cd[q + 1];
+        const double dorg = (tj > 0.0 || jj == K - 1) ? cd[q] : cd[q + 1];
         prod *= ((dorg - di) + tj) / (cd[q] - di);
       }
     }
@@ -431,7 +436,8 @@ __global__ void __launch_bounds__(DC_T) dc_vectors_kernel(
   float* Wg = W + (int64_t)g * m * m;
   if (blockIdx.y == 0) {
     for (int r = threadIdx.x; r < m; r += DC_T)
-      if (isnd[base + r] < 0) Wg[(int64_t)perm[base + r] * m + outpos[base + r]] = 1.f;
+      if (isnd[base + r] < 0)
+        Wg[(int64_t)min(max(perm[base + r], 0), m - 1) * m + outpos[base + r]] = 1.f;
   }
   if ((int)(blockIdx.y * DC_T) >= K) return;
   const int j = blockIdx.y * DC_T + threadIdx.x;
@@ -440,7 +446,7 @@ __global__ void __launch_bounds__(DC_T) dc_vectors_kernel(
   int64_t col = 0;
   if (act) {
     tj = tau[base + j];
-    dorg = sd[base + ndidx[base + (tj > 0.0 ? j : j + 1)]];
+    dorg = sd[base + ndidx[base + ((tj > 0.0 || j == K - 1) ? j : j + 1)]];
     col = outpos[base + ndidx[base + j]];
   }
   double ss = 0.0;
@@ -453,7 +459,7 @@ __global__ void __launch_bounds__(DC_T) dc_vectors_kernel(
         const int idx = ndidx[base + c0 + q];
         cd[q] = sd[base + idx];
         cz[q] = zh[base + c0 + q];
-        crow[q] = perm[base + idx];
+        crow[q] = min(max(perm[base + idx], 0), m - 1);
       }
       __syncthreads();
       if (!act) continue;
@@ -486,8 +492,8 @@ __global__ void __launch_bounds__(DC_T) dc_rotate_kernel(
   const int64_t base = (int64_t)g * m;
   float* Wg = W + (int64_t)g * m * m;
   for (int r = nrot - 1; r >= 0; --r) {
-    const int a = perm[base + rot_idx[(base + r) * 2 + 0]];
-    const int b = perm[base + rot_idx[(base + r) * 2 + 1]];
+    const int a = min(max(perm[base + rot_idx[(base + r) * 2 + 0]], 0), m - 1);
+    const int b = min(max(perm[base + rot_idx[(base + r) * 2 + 1]], 0), m - 1);
     const double cc = rot_cs[(base + r) * 2 + 0], s = rot_cs[(base + r) * 2 + 1];
     const double wa = Wg[(int64_t)a * m + c], wb = Wg[(int64_t)b * m + c];
     Wg[(int64_t)a * m + c] = (float)(cc * wa - s * wb);

@@ -48,6 +48,8 @@ from distributed_kfac_pytorch_amd.parallel.comm import (
 )
 
 logger = logging.getLogger(__name__)
+# diagnostics only: compute P but leave the raw gradients in place
+_DEBUG_NO_APPLY = os.environ.get('KFAC_DEBUG_NO_APPLY') == '1'
 
 
 class StepGraphs:
@@ -256,6 +258,8 @@ class StepGraphs:
                     if not bcast:
                         pre._multi_apply.launch(kl is not None)
             torch.cuda.current_stream().wait_stream(side)
+            # descriptor tables built during the capture: one eager upload
+            _native.flush_table_uploads()
             self.graph, self.key, self.pending_key = g, key, None
             self.captures += 1
         elif not bcast and not pre._multi_apply.prepare(layers, kl, lr, use_buffers=True):
@@ -808,7 +812,7 @@ class BaseKFACPreconditioner:
         GPU fast path: three multi-tensor launches for the whole model
         (``ops.precondition.MultiLayerApply``); otherwise per layer.
         """
-        if not ordered:
+        if not ordered or _DEBUG_NO_APPLY:
             return
         if self._multi_apply is None:
             self._multi_apply = pops.MultiLayerApply()

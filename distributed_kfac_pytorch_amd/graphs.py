@@ -61,6 +61,7 @@ import torch
 import torch.distributed as dist
 
 from distributed_kfac_pytorch_amd import tracing
+from distributed_kfac_pytorch_amd.ops import _native
 
 logger = logging.getLogger(__name__)
 
@@ -226,6 +227,8 @@ class GraphedTrainStep:
                     p.step()
                 self.optimizer.step()
         torch.cuda.current_stream().wait_stream(side)
+        # descriptor tables built during the capture: one eager upload now
+        _native.flush_table_uploads()
         if p is not None:
             # capture ran the step's host code without executing it
             p._steps = saved
@@ -280,18 +283,28 @@ class GraphedTrainStep:
             kinds = ('plain', 'factor') if self.preconditioner is not None else ('plain',)
             only = os.environ.get('KFAC_GRAPH_KINDS')  # diagnostics: capture a subset
             if only:
-                kinds = tuple(k for k in kinds if k in only.split(','))
+                kinds = tuple(k for k in only.split(',') if k in kinds)
             for k in kinds:
                 if k not in self.graphs:
+                    failed = None
                     try:
                         self._capture(k)
                     except Exception as e:  # noqa: BLE001
-                        # something in the step is not capturable: run eagerly
-                        logger.warning('step graph capture failed (%s); running eagerly', e)
+                        failed = repr(e)
+                    if failed is not None:
+                        # something in the step is not capturable: run eagerly.
+                        # (Outside the except block: the exception's traceback
+                        # holds the failed capture's loss, and with it
+                        # AccumulateGrad nodes bound to the capture stream.)
+                        logger.warning('step graph capture failed (%s); running eagerly', failed)
                         if self.preconditioner is not None:
                             self.preconditioner._steps = self._steps_before_capture
                         self.enabled = False
                         self.graphs.clear()
+                        self.outputs.clear()
+                        self.grads.clear()
+                        _native.flush_table_uploads()
+                        gc.collect()
                         return self._eager()
             if kind not in self.graphs:
                 return self._eager()

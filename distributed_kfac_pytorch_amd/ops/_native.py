@@ -71,3 +71,12 @@ def use_native(*tensors: torch.Tensor) -> bool:
         f'({_err!r}); build it with `python tools/build_native.py` or set '
         'KFAC_ALLOW_TORCH_FALLBACK=1 to run the PyTorch reference math.',
     )
+
+
+def flush_table_uploads() -> int:
+    """Upload the descriptor tables built inside the HIP-graph capture that
+    just ended (csrc/bindings.cpp ``upload_table``: captures record no copy
+    node; the tables are uploaded once, eagerly, before the first replay).
+    Every site that captures a graph calls this right after the capture."""
+    lib = native()
+    return int(lib.flush_table_uploads()) if lib is not None else 0

@@ -69,8 +69,10 @@ JACOBI_MAX_N = int(os.environ.get('KFAC_JACOBI_MAX_N', '128'))
 
 
 def sytrd_min_n() -> int:
-    """Smallest factor dimension sent to the native tridiagonalisation."""
-    return int(os.environ.get('KFAC_SYTRD_MIN_N', '2000'))
+    """Smallest factor dimension sent to the native tridiagonalisation
+    (every factor above the LDS Jacobi tier by default: no rocSOLVER
+    eigensolver runs in a refresh)."""
+    return int(os.environ.get('KFAC_SYTRD_MIN_N', str(JACOBI_MAX_N + 1)))
 
 
 logger = logging.getLogger(__name__)
@@ -209,10 +211,16 @@ def _large_bucket(stack: torch.Tensor, warm: torch.Tensor | None
     algo = _algo_for(n)
     if algo in ('sytrd', 'auto'):
         algo = 'syevd'
+    _tier(algo, n, stack.shape[0])
     if algo == 'torch':
         return torch.linalg.eigh(stack)
     evals, evecs = native().rocsolver_eigh(stack.contiguous(), _ALGOS[algo], 100, 1e-7)
     return evals, evecs
+
+
+def _tier(name: str, n: int, count: int) -> None:
+    """Record which solver handled a bucket (``last_stats['tiers']``)."""
+    last_stats.setdefault('tiers', []).append((name, int(n), int(count)))
 
 
 def _gpu_bucket(stack: torch.Tensor, warm: torch.Tensor | None = None
@@ -220,6 +228,7 @@ def _gpu_bucket(stack: torch.Tensor, warm: torch.Tensor | None = None
     n = stack.shape[-1]
     lib = native()
     if n <= JACOBI_MAX_N:
+        _tier('jacobi', n, stack.shape[0])
         return lib.jacobi_eigh(stack.contiguous(), JACOBI_SWEEPS, JACOBI_TOL)
     if warm is not None and block_jacobi_enabled() and n <= WARM_ACCEPT_MAX_N:
         idx, r, q = _accept_warm(stack, warm)
@@ -342,7 +351,7 @@ def _settle_warm(gpu: list, stacks: dict, warms: dict, out: dict) -> list:
     # chain members are not candidates: a fixed chain membership keeps its
     # captured graphs (one per signature) valid from refresh to refresh
     cand = [(k, v) for k, v in gpu if k[2] and k in warms and JACOBI_MAX_N < k[0]
-            <= WARM_ACCEPT_MAX_N and not _use_sytrd(k[0], len(v))
+            <= WARM_ACCEPT_MAX_N and not (_use_sytrd(k[0], len(v)) and _chain_graphs_enabled())
             and block_jacobi_enabled_for_sytrd()]
     if not cand:
         return gpu
@@ -366,6 +375,8 @@ def _settle_warm(gpu: list, stacks: dict, warms: dict, out: dict) -> list:
         pos += len(idxs)
         acc = [i for i, v in enumerate(ok) if v]
         last_stats.setdefault('accepted', []).extend([key[0]] * len(acc))
+        if acc:
+            _tier('accepted', key[0], len(acc))
         if acc:
             sel = torch.tensor(acc, device=stacks[key].device)
             rs, order = stats[j].index_select(0, sel).sort(dim=1)
@@ -405,7 +416,7 @@ def _use_sytrd(n: int, count: int = 1) -> bool:
     on = mode == 'sytrd' or (mode == 'auto' and large_algo() == 'sytrd')
     if not on or n < sytrd_min_n():
         return False
-    if mode == 'auto' and count > int(os.environ.get('KFAC_SYTRD_MAX_BATCH', '8')):
+    if mode == 'auto' and count > int(os.environ.get('KFAC_SYTRD_MAX_BATCH', '1000000')):
         return False
     lib = native()
     return lib is not None and n <= int(lib.sytrd_max_n())
@@ -537,6 +548,7 @@ def _tail_job(stream: torch.cuda.Stream, ev: torch.cuda.Event, red: torch.Tensor
         if _q_back_transform() == 'rocsolver':
             w, x = native().tridiag_eigvecs(red, d, e, tau)
             return w.clone(), x
+        _tier('sytrd+' + tridiag_solver(), red.shape[-1], red.shape[0])
         if tridiag_solver() == 'dc':
             n = d.shape[-1]
             w, z = native().tridiag_eigh_dc(d, e[:, :max(n - 1, 0)])
@@ -559,7 +571,7 @@ def _chain_groups(keys: list) -> list[list]:
     of kernel-boundary latency per column of its largest matrix, so two
     chains on two hardware queues overlap each other's gaps, while the
     smaller matrices no longer add their symv traffic to the largest chain."""
-    cuts = sorted((int(c) for c in os.environ.get('KFAC_SYTRD_SPLIT', '4000').split(',')
+    cuts = sorted((int(c) for c in os.environ.get('KFAC_SYTRD_SPLIT', '4000,1000').split(',')
                    if c), reverse=True)
     groups, left = [], list(keys)
     for c in cuts:

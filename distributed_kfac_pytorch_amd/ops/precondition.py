@@ -139,12 +139,13 @@ class _TableCache:
     with the pinned host staging buffers they are uploaded from.
 
     A table built inside a HIP-graph capture (``graphs.GraphedTrainStep``:
-    the captured backward produces gradients at new addresses) is uploaded
-    by a captured H2D copy that re-reads its staging buffer on every replay,
-    so each entry owns its staging buffers until evicted.  Pinned memory
-    cannot be allocated while a capture is running, so the buffers are
-    allocated the first time they are needed outside a capture and recycled
-    after that.
+    the captured backward produces gradients at new addresses) is written to
+    the persistent device twin of its staging slot -- allocated eagerly,
+    outside every graph pool -- and uploaded once, eagerly, right after the
+    capture (``_native.flush_table_uploads``); no copy node is captured.
+    Pinned and device slots cannot be allocated while a capture is running,
+    so they are allocated the first time they are needed outside a capture
+    and recycled after that.
 
     Staging reuse is fenced: an eager upload records a HIP event on the
     stream that runs its H2D copy, and a buffer whose entry is evicted is
@@ -169,6 +170,8 @@ class _TableCache:
         self._parked: list[tuple[torch.Tensor, Any]] = []
         self._sticky: set = set()
         self._pins: dict = {}
+        # device twins of the staging slots (kept alive here)
+        self._dev_slots: list[torch.Tensor] = []
 
     @staticmethod
     def _capturing() -> bool:
@@ -224,9 +227,19 @@ class _TableCache:
         if not capturing and torch.cuda.is_available():
             # a parked buffer is reused only once its last copy has run
             self._unpark(wait=len(self._free) < self.per)
-            # top up so that a later capture never has to allocate
+            # top up so that a later capture never has to allocate: each
+            # pinned staging slot gets a persistent device twin (outside any
+            # graph pool) that a table built during a capture is written to
+            # (csrc/bindings.cpp upload_table / register_table_slot)
             while len(self._free) < self.per * self.size:
-                self._free.append(torch.empty(self.SLOT_BYTES, dtype=torch.uint8, pin_memory=True))
+                host = torch.empty(self.SLOT_BYTES, dtype=torch.uint8, pin_memory=True)
+                lib = native()
+                if lib is not None and hasattr(lib, 'register_table_slot'):
+                    dev = torch.empty(self.SLOT_BYTES, dtype=torch.uint8,
+                                      device=torch.device('cuda', torch.cuda.current_device()))
+                    lib.register_table_slot(host, dev)
+                    self._dev_slots.append(dev)
+                self._free.append(host)
         out: list[torch.Tensor | None] = []
         for _ in range(self.per):
             out.append(self._free.pop() if self._free else None)
@@ -632,6 +645,10 @@ class SplitGroupedPrecondition(GroupedPrecondition):
             layer._g3s = st
         return st
 
+    @staticmethod
+    def _capturing() -> bool:
+        return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+
     def _resplit(self, todo: list) -> None:
         """Split static operands whose content changed (one launch)."""
         if not todo:
@@ -688,6 +705,11 @@ class SplitGroupedPrecondition(GroupedPrecondition):
             else:
                 t['t1'].append((st['w'], st['fa'], st['t1'], none3, (g, a, a)))
                 t['t3i'].append((st['fg'], st['t1'], out, none3, (g, a, g)))
+        if todo and self._capturing():
+            # a basis changed since the last eager step: its split images are
+            # refreshed eagerly (never inside a capture); capture the
+            # per-layer path this time
+            return False
         self._resplit(todo)
         key_t = tuple(key)
         if key_t != self._key:

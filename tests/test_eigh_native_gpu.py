@@ -1,0 +1,64 @@
+"""The DEFAULT eigensolver tier selection at production factor sizes against
+float64 ``torch.linalg.eigh`` (reference: kfac/layers/eigen.py:294-347).
+
+Factors are K-FAC-like: an EMA of sample second moments over an identity
+start (decayed), i.e. PSD, with a cluster of eigenvalues near the decayed
+identity and a rank-deficient data part.
+"""
+from __future__ import annotations
+
+import pytest
+import torch
+
+from distributed_kfac_pytorch_amd.ops import linalg
+
+pytestmark = pytest.mark.gpu
+
+
+def _factor(n: int, seed: int) -> torch.Tensor:
+    g = torch.Generator().manual_seed(seed)
+    a = 0.95 ** 11 * torch.eye(n, dtype=torch.float64)
+    for _ in range(3):
+        x = torch.randn(max(8, n // 3), n, generator=g, dtype=torch.float64)
+        x *= torch.rand(n, generator=g, dtype=torch.float64) ** 2  # uneven columns
+        a = 0.95 * a + 0.05 * (x.T @ x) / x.shape[0]
+    return a
+
+
+def _check(a64: torch.Tensor, d: torch.Tensor, q: torch.Tensor) -> None:
+    d, q = d.double().cpu(), q.double().cpu()
+    n = a64.shape[0]
+    ref = torch.linalg.eigvalsh(a64)
+    nrm = float(torch.linalg.matrix_norm(a64, ord=2))
+    assert float((d - ref).abs().max()) <= 1e-5 * nrm
+    rec = q @ torch.diag(d) @ q.T
+    assert float((rec - a64).norm() / a64.norm()) <= 1e-5
+    assert float((q.T @ q - torch.eye(n, dtype=torch.float64)).abs().max()) <= 1e-5
+
+
+@pytest.mark.parametrize('n', [129, 577, 1152, 2304, 4608])
+def test_default_tier_matches_float64(cuda, n: int) -> None:
+    a64 = _factor(n, n)
+    linalg.last_stats.clear()
+    (d, q), = linalg.eigh_many([a64.float().to(cuda)])
+    torch.cuda.synchronize()
+    tiers = {t[0] for t in linalg.last_stats.get('tiers', [])}
+    assert tiers == {'sytrd+dc'}, tiers  # no rocSOLVER eigensolver
+    _check(a64, d, q)
+
+
+def test_mixed_refresh_two_rounds(cuda) -> None:
+    """A ResNet-50-like mix (every tier, several chains) twice, the second
+    round warm-started from the first round's bases (acceptance test)."""
+    sizes = [64, 147, 256, 512, 576, 1000, 1152, 2049, 2304, 4608]
+    mats64 = [_factor(n, 7 + i) for i, n in enumerate(sizes)]
+    mats = [m.float().to(cuda) for m in mats64]
+    res = linalg.eigh_many(mats)
+    torch.cuda.synchronize()
+    for a64, (d, q) in zip(mats64, res):
+        _check(a64, d, q)
+    warm = [q.contiguous() for _, q in res]
+    res2 = linalg.eigh_many(mats, warm)
+    torch.cuda.synchronize()
+    for a64, (d, q) in zip(mats64, res2):
+        _check(a64, d, q)

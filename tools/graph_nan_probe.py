@@ -26,14 +26,16 @@ from distributed_kfac_pytorch_amd.models.resnet import resnet50  # noqa: E402
 from distributed_kfac_pytorch_amd.ops.cast import enable_fused_weight_cast  # noqa: E402
 
 
-def build(base, dev, graphs: bool, amp: bool, fused_cast: bool):  # type: ignore[no-untyped-def]
+def build(base, dev, graphs: bool, amp: bool, fused_cast: bool, warmup: int = 1,
+          kfac_on: bool = True, factor_steps: int = 2):  # type: ignore[no-untyped-def]
     model = copy.deepcopy(base).to(dev).to(memory_format=torch.channels_last)
     if fused_cast and amp:
         enable_fused_weight_cast(model)
     opt = torch.optim.SGD(model.parameters(), lr=0.01, momentum=0.9, weight_decay=5e-5)
     pre = kfac.KFACPreconditioner(
-        model, factor_update_steps=2, inv_update_steps=8, damping=0.001, kl_clip=0.001,
-        lr=lambda s: opt.param_groups[0]['lr'], grad_worker_fraction=0.5)
+        model, factor_update_steps=factor_steps, inv_update_steps=8, damping=0.001,
+        kl_clip=0.001, lr=lambda s: opt.param_groups[0]['lr'],
+        grad_worker_fraction=0.5) if kfac_on else None
     x = torch.empty(8, 3, 64, 64, device=dev).contiguous(memory_format=torch.channels_last)
     y = torch.empty(8, dtype=torch.long, device=dev)
     crit = torch.nn.CrossEntropyLoss(label_smoothing=0.1)
@@ -45,12 +47,13 @@ def build(base, dev, graphs: bool, amp: bool, fused_cast: bool):  # type: ignore
         return loss
 
     if graphs:
-        runner = GraphedTrainStep(fb, opt, pre, warmup=1, enabled=True)
+        runner = GraphedTrainStep(fb, opt, pre, warmup=warmup, enabled=True)
     else:
         def runner() -> torch.Tensor:
             opt.zero_grad(set_to_none=False)
             loss = fb()
-            pre.step()
+            if pre is not None:
+                pre.step()
             opt.step()
             return loss.detach()
     return model, opt, pre, x, y, runner
@@ -69,7 +72,7 @@ def state(model, opt, pre) -> dict:  # type: ignore[no-untyped-def]
     for b in model.buffers():
         if b.is_floating_point():
             cats['buffer'].append(b)
-    for _, layer in pre._layers.values():
+    for _, layer in (pre._layers.values() if pre is not None else []):
         for t in (layer.a_factor, layer.g_factor):
             if t is not None:
                 cats['factor'].append(t)
@@ -93,19 +96,25 @@ def main() -> None:
     ap.add_argument('--fp32', action='store_true')
     ap.add_argument('--fused-cast', type=int, default=1)
     ap.add_argument('--deterministic', type=int, default=1)
+    ap.add_argument('--warmup', type=int, default=1)
+    ap.add_argument('--no-kfac', action='store_true')
+    ap.add_argument('--factor-steps', type=int, default=2)
     args = ap.parse_args()
     torch.backends.cudnn.deterministic = bool(args.deterministic)
     dev = torch.device('cuda')
     torch.manual_seed(0)
     base = resnet50(num_classes=10)
-    A = build(base, dev, True, not args.fp32, bool(args.fused_cast))
-    B = build(base, dev, False, not args.fp32, bool(args.fused_cast))
+    A = build(base, dev, True, not args.fp32, bool(args.fused_cast), args.warmup,
+              not args.no_kfac, args.factor_steps)
+    B = build(base, dev, False, not args.fp32, bool(args.fused_cast), 1,
+              not args.no_kfac, args.factor_steps)
     gen = torch.Generator(device='cpu').manual_seed(1)
     pool = [(torch.randn(8, 3, 64, 64, generator=gen), torch.randint(0, 10, (8,), generator=gen))
             for _ in range(4)]
     env = {k: v for k, v in os.environ.items() if k.startswith('KFAC_')}
     for i in range(args.steps):
         kind = A[5].kind()
+        cap0, rep0 = A[5].captures, A[5].replays
         x, y = pool[i % len(pool)]
         for m in (A, B):
             m[3].copy_(x)
@@ -114,11 +123,15 @@ def main() -> None:
         lb = B[5]()
         torch.cuda.synchronize()
         sa, sb = state(*A[:3]), state(*B[:3])
-        rec: dict = {'step': i, 'kind': kind, 'env': env,
+        how = 'replay' if A[5].replays > rep0 else 'eager'
+        if A[5].captures > cap0:
+            how += '+capture'
+        rec: dict = {'step': i, 'kind': kind, 'how': how, 'env': env,
                      'loss': [float(la), float(lb)]}
         # per layer: factor and P differences (first 3 worst)
-        per = []
-        for (name, la_), (_, lb_) in zip(A[2]._layers.values(), B[2]._layers.values()):
+        per = [(0.0, '-', 0, 0, 0)]
+        for (name, la_), (_, lb_) in zip(A[2]._layers.values() if A[2] else [],
+                                         B[2]._layers.values() if B[2] else []):
             fa = float((la_.a_factor - lb_.a_factor).abs().max() / lb_.a_factor.abs().max())
             fg = float((la_.g_factor - lb_.g_factor).abs().max() / lb_.g_factor.abs().max())
             pa, pb_ = la_._grad_buf, lb_._grad_buf
