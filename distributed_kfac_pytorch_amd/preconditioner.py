@@ -136,6 +136,7 @@ class KFACPreconditioner(BaseKFACPreconditioner):
         update_factors_in_hook: bool = True,
         loglevel: int = logging.DEBUG,
         register_embeddings: bool = False,
+        cost_model: str = 'auto',
     ) -> None:
         """Init KFACPreconditioner.
 
@@ -166,6 +167,10 @@ class KFACPreconditioner(BaseKFACPreconditioner):
             register_embeddings: also precondition ``nn.Embedding`` layers
                 (diagonal A factor, ``layers.embedding``).  Off by default
                 for parity with the reference, which ignores embeddings.
+            cost_model: factor cost of the ``COMPUTE`` placement: ``'flops'``
+                (the reference's n^3), ``'measured'`` (the MI355X per-size
+                solver-time table, ``parallel/costmodel.py``) or ``'auto'``
+                (measured for the eigen method on a CUDA model, else flops).
         """
         if allreduce_bucket_cap_mb < 0:
             raise ValueError('allreduce_bucket_cap_mb must be >= 0')
@@ -241,7 +246,15 @@ class KFACPreconditioner(BaseKFACPreconditioner):
         for name, layer in kfac_layers.values():
             logger.log(loglevel, f'Registered name="{name}": {layer!r}')
 
-        if assignment_strategy == AssignmentStrategy.COMPUTE:
+        if cost_model not in ('auto', 'flops', 'measured'):
+            raise ValueError(f'unknown cost_model {cost_model!r}')
+        if cost_model == 'auto':
+            on_gpu = any(p.is_cuda for p in model.parameters())
+            cost_model = 'measured' if (on_gpu and compute_method == ComputeMethod.EIGEN) else 'flops'
+        self.cost_model = cost_model
+        if assignment_strategy == AssignmentStrategy.COMPUTE and cost_model == 'measured':
+            from distributed_kfac_pytorch_amd.parallel.costmodel import solver_ms as cost
+        elif assignment_strategy == AssignmentStrategy.COMPUTE:
             def cost(n: int) -> float:
                 return float(n) ** 3
         elif assignment_strategy == AssignmentStrategy.MEMORY:
@@ -282,6 +295,7 @@ class KFACPreconditioner(BaseKFACPreconditioner):
             'skip_layers': self.skip_layers,
             'symmetry_aware': self.symmetry_aware,
             'register_embeddings': self.register_embeddings,
+            'cost_model': self.cost_model,
         }
         super().__init__(
             kfac_layers,
