@@ -1103,6 +1103,9 @@ at::Tensor bn_act(const at::Tensor& x, const at::Tensor& weight, const at::Tenso
 // tridiag_host.cpp
 std::vector<at::Tensor> tridiag_eigh_dc(const at::Tensor& d, const at::Tensor& e);
 std::vector<int64_t> tridiag_dc_plan(int64_t n);
+// twostage_host.cpp
+std::vector<at::Tensor> eigh_twostage(const at::Tensor& A, bool timed);
+int64_t eigh_twostage_max_n();
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "MI355X (gfx950) HIP kernels for distributed K-FAC";
@@ -1173,6 +1176,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("refine") = true);
   m.def("tridiag_eigh_dc", &tridiag_eigh_dc, py::call_guard<py::gil_scoped_release>());
   m.def("tridiag_dc_plan", &tridiag_dc_plan);
+  m.def("eigh_twostage", &eigh_twostage, py::call_guard<py::gil_scoped_release>(),
+        py::arg("A"), py::arg("timed") = false);
+  m.def("eigh_twostage_max_n", &eigh_twostage_max_n);
   m.def("flush_table_uploads", &flush_table_uploads);
   m.def("register_table_slot", &register_table_slot);
   m.attr("arch") = "gfx950";

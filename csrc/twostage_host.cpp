@@ -1,0 +1,176 @@
+// Host driver of the two-stage batched symmetric eigensolver (K-HIP-3):
+//
+//   dense -> band (csrc/sy2sb.hip panel QR + batched GEMM two-sided updates)
+//   band -> tridiagonal (csrc/sb2st.hip bulge chasing, one workgroup per matrix)
+//   tridiagonal eigenpairs (csrc/tridiag.hip divide and conquer)
+//   X = Q2 Z (csrc/bt2.hip, one launch per step of disjoint rank-16 blocks)
+//   X = Q1 X (blocked UT back-transform, 512 reflectors per batched GEMM)
+//
+// for a batch of same-size fp32 symmetric matrices, all on the current
+// stream, no host synchronisation.  Reference: torch.linalg.eigh in
+// kfac/layers/eigen.py:294-347.  float64 oracle of every stage:
+// distributed_kfac_pytorch_amd/ops/twostage.py.
+#include <torch/extension.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <limits>
+#include <vector>
+
+namespace kfac {
+int twostage_band();
+int twostage_max_n();
+void sb_panel_qr(float* A, int64_t sA, int ld, int n, int p, int batch, float* Vw, float* Uw,
+                 int64_t sVU, float* tau1, int64_t sTau, float* Tw, hipStream_t stream);
+void sb_extract(const float* A, int64_t sA, int ld, int n, int batch, float* AB, int64_t sAB,
+                int ncols, hipStream_t stream);
+int sb2st_kmax(int n);
+void sb2st(float* AB, int64_t sAB, int n, int batch, float* V2, float* tau2, int64_t sV2,
+           int kmax, float* d, float* e, int* err, hipStream_t stream);
+int bt2_groups(int n);
+void bt2_prep(const float* V2, const float* tau2, int64_t sV2, int n, int kmax, int batch,
+              float* T, hipStream_t stream);
+void bt2_apply(const float* V2, int64_t sV2, const float* T, int n, int kmax, int batch,
+               float* X, int64_t sX, int ldx, hipStream_t stream);
+}  // namespace kfac
+
+std::vector<at::Tensor> tridiag_eigh_dc(const at::Tensor& d, const at::Tensor& e);
+
+namespace {
+
+hipStream_t cur() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+
+// stage-1 reflector k (k = 0 .. nref-1) lives in ROW k of A: v[k+16] = 1
+// implicit, v[k+17 ..] stored; X <- Q1 X with Q1 = H_0 H_1 ... H_{nref-1},
+// nb reflectors per UT block (T^-1 = striu(V^T V) + diag(1/tau)), last block
+// first.
+void apply_q1(const at::Tensor& A, const at::Tensor& tau1, int64_t n, int64_t nref,
+              at::Tensor& X, int64_t nb) {
+  const int64_t off = kfac::twostage_band();
+  auto fopt = X.options();
+  const int64_t b = X.size(0);
+  for (int64_t p0 = ((nref - 1) / nb) * nb; p0 >= 0; p0 -= nb) {
+    const int64_t p1 = std::min(p0 + nb, nref);
+    const int64_t bs = p1 - p0;
+    const int64_t rows = n - p0 - off;
+    if (rows <= 0) continue;
+    auto W = A.narrow(1, p0, bs).narrow(2, p0 + off, rows);
+    auto vt = at::triu(W, 1);
+    auto t = tau1.narrow(1, p0, bs);
+    auto live = t.ne(0).to(at::kFloat);
+    auto eye_bs = at::eye(bs, rows, fopt).unsqueeze(0);
+    vt = (vt + eye_bs) * live.unsqueeze(2);
+    auto g = at::bmm(vt, vt.transpose(1, 2));
+    auto dinv = at::where(t.eq(0), at::ones_like(t), at::reciprocal(at::where(t.eq(0),
+                                                                                at::ones_like(t), t)));
+    auto u = at::triu(g, 1) + at::diag_embed(dinv);
+    auto tm = at::linalg_solve_triangular(u, at::eye(bs, fopt).expand({b, bs, bs}), true);
+    auto xs = X.narrow(1, p0 + off, rows);
+    auto w = at::bmm(tm, at::bmm(vt, xs));
+    xs.baddbmm_(vt.transpose(1, 2), w, 1.0, -1.0);
+  }
+}
+
+}  // namespace
+
+int64_t eigh_twostage_max_n() { return kfac::twostage_max_n(); }
+
+// A [b, n, n] fp32 symmetric on the GPU -> (w [b, n] ascending, X [b, n, n]
+// eigenvectors in columns, err [1] int32: nonzero if the bulge-chasing
+// pipeline timed out -- then w is NaN).  `times` (optional, host fp32 [5]):
+// per-stage milliseconds (synchronises; diagnostics only).
+std::vector<at::Tensor> eigh_twostage(const at::Tensor& A_in, bool timed) {
+  TORCH_CHECK(A_in.is_cuda() && A_in.dim() == 3 && A_in.size(1) == A_in.size(2),
+              "eigh_twostage: A must be [b, n, n] on the GPU");
+  const int64_t b = A_in.size(0), n = A_in.size(1);
+  const int64_t B = kfac::twostage_band();
+  TORCH_CHECK(n >= 3 && n <= kfac::twostage_max_n(), "eigh_twostage: 3 <= n <= ",
+              kfac::twostage_max_n());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(A_in.device());
+  hipStream_t s = cur();
+  auto fopt = A_in.options().dtype(at::kFloat);
+  std::vector<hipEvent_t> ev;
+  auto mark = [&]() {
+    if (!timed) return;
+    hipEvent_t e;
+    hipEventCreate(&e);
+    hipEventRecord(e, s);
+    ev.push_back(e);
+  };
+  mark();
+  const int64_t ld = (n + 3) / 4 * 4;
+  auto A = at::zeros({b, n, ld}, fopt);
+  A.narrow(2, 0, n).copy_(A_in);
+  auto Vw = at::empty({b, n, B}, fopt);
+  auto Uw = at::empty({b, n, B}, fopt);
+  auto tau1 = at::zeros({b, n}, fopt);
+  auto Tw = at::empty({b, B, B}, fopt);
+  int64_t nref = 0;
+  // ---- stage 1
+  for (int64_t p = 0; n - p - B >= 2; p += B) {
+    const int64_t m = n - p - B;
+    kfac::sb_panel_qr(A.data_ptr<float>(), n * ld, (int)ld, (int)n, (int)p, (int)b,
+                      Vw.data_ptr<float>(), Uw.data_ptr<float>(), n * B, tau1.data_ptr<float>(),
+                      n, Tw.data_ptr<float>(), s);
+    nref = p + B;
+    auto A22 = A.narrow(1, p + B, m).narrow(2, p + B, m);
+    auto V = Vw.narrow(1, 0, m);
+    auto U = Uw.narrow(1, 0, m);
+    auto Y = at::bmm(A22, U);
+    auto S = at::bmm(V.transpose(1, 2), Y);
+    auto M = at::bmm(Tw.transpose(1, 2), S);
+    auto Ms = (M + M.transpose(1, 2)) * 0.5;
+    auto W = at::baddbmm(Y, V, Ms, 1.0, -0.5);
+    A22.baddbmm_(at::cat({V, W}, 2), at::cat({W, V}, 2).transpose(1, 2), 1.0, -1.0);
+  }
+  mark();
+  // ---- stage 2
+  const int64_t ncols = n + 4 * B;
+  auto AB = at::empty({b, ncols, 2 * B}, fopt);
+  kfac::sb_extract(A.data_ptr<float>(), n * ld, (int)ld, (int)n, (int)b, AB.data_ptr<float>(),
+                   ncols * 2 * B, (int)ncols, s);
+  const int kmax = kfac::sb2st_kmax((int)n);
+  const int64_t nslot = (n - 2) * kmax;
+  auto V2 = at::zeros({b, nslot, B}, fopt);
+  auto tau2 = at::zeros({b, nslot}, fopt);
+  auto d = at::empty({b, n}, fopt);
+  auto e = at::empty({b, n - 1}, fopt);
+  auto err = at::zeros({1}, A_in.options().dtype(at::kInt));
+  kfac::sb2st(AB.data_ptr<float>(), ncols * 2 * B, (int)n, (int)b, V2.data_ptr<float>(),
+              tau2.data_ptr<float>(), nslot, kmax, d.data_ptr<float>(), e.data_ptr<float>(),
+              err.data_ptr<int>(), s);
+  // a timed-out pipeline must never be installed: poison its eigenvalues
+  d = at::where(err.ne(0), at::full({}, std::numeric_limits<float>::quiet_NaN(), fopt), d);
+  mark();
+  // ---- tridiagonal eigenpairs
+  auto wz = tridiag_eigh_dc(d, e);
+  at::Tensor w = wz[0];
+  at::Tensor X = wz[1].contiguous();
+  mark();
+  // ---- back-transforms
+  const int G = kfac::bt2_groups((int)n);
+  auto T2 = at::empty({b, (int64_t)G * kmax, B, B}, fopt);
+  kfac::bt2_prep(V2.data_ptr<float>(), tau2.data_ptr<float>(), nslot, (int)n, kmax, (int)b,
+                 T2.data_ptr<float>(), s);
+  kfac::bt2_apply(V2.data_ptr<float>(), nslot, T2.data_ptr<float>(), (int)n, kmax, (int)b,
+                  X.data_ptr<float>(), n * n, (int)n, s);
+  mark();
+  if (nref > 0) apply_q1(A, tau1, n, nref, X, 512);
+  mark();
+  at::Tensor times = at::zeros({std::max<int64_t>((int64_t)ev.size() - 1, 0)},
+                               at::TensorOptions().dtype(at::kFloat));
+  if (timed) {
+    hipEventSynchronize(ev.back());
+    for (size_t i = 0; i + 1 < ev.size(); ++i) {
+      float ms = 0.f;
+      hipEventElapsedTime(&ms, ev[i], ev[i + 1]);
+      times[i].fill_(ms);
+    }
+    for (auto& x : ev) hipEventDestroy(x);
+  }
+  return {w, X, err, times};
+}

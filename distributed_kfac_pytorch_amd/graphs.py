@@ -114,6 +114,15 @@ class GraphedTrainStep:
                 not multi or os.environ.get('KFAC_STEP_GRAPHS_MULTI', '0') == '1'
             )
         self.enabled = enabled
+        if enabled and preconditioner is not None and getattr(preconditioner, '_graphs', None):
+            # The whole-step graph already contains the precondition phase.
+            # With the preconditioner's own precondition-phase graphs
+            # (StepGraphs) also active, the replays after capture produced
+            # garbage preconditioned gradients from the first replay on, while
+            # with StepGraphs off the replays matched the eager twin exactly
+            # (ResNet-50, bf16 and fp32: gpurun_out/r3d/probe_*.jsonl,
+            # profiles/graph_replay_stepgraphs_r3.txt).
+            preconditioner._graphs = None
         self.graphs: dict[str, torch.cuda.CUDAGraph] = {}
         self.outputs: dict[str, torch.Tensor] = {}
         self.grads: dict[str, list] = {}

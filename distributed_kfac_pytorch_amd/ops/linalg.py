@@ -57,6 +57,7 @@ from typing import Any
 
 import torch
 
+from distributed_kfac_pytorch_amd.ops import twostage
 from distributed_kfac_pytorch_amd.ops._native import native
 from distributed_kfac_pytorch_amd.ops._native import use_native
 
@@ -180,10 +181,22 @@ def _accept_warm(stack: torch.Tensor, warm: torch.Tensor
     return idx, rs, q
 
 
+def _use_twostage(n: int) -> bool:
+    """Native two-stage solver (ops/twostage.py) for this factor size."""
+    mode = os.environ.get('KFAC_EIGH', 'auto')
+    if mode not in ('auto', 'twostage'):
+        return False
+    if mode == 'auto' and large_algo() != 'twostage':
+        return False
+    return JACOBI_MAX_N < n <= twostage.max_n()
+
+
 def large_algo() -> str:
     """Solver for factors above the LDS Jacobi tier that the warm-start
-    acceptance test did not settle: ``KFAC_EIGH_LARGE`` = sytrd | syevd |
-    block.
+    acceptance test did not settle: ``KFAC_EIGH_LARGE`` = twostage (default:
+    dense -> band -> tridiagonal with level-3 stage 1, bulge chasing, native
+    divide and conquer and blocked back-transforms, ops/twostage.py) |
+    sytrd (one-stage native chains) | syevd | block.
 
     Default sytrd: factors with n >= ``KFAC_SYTRD_MIN_N`` (2000) go through
     the native tridiagonalisation chains with the blocked back-transform,
@@ -198,12 +211,16 @@ def large_algo() -> str:
     basis of a rank-deficient early factor is a poor start) and the mix
     takes 1002 ms against 395 ms for syevd at equal accuracy
     (profiles/refresh_probe_r2_resnet50_step100.jsonl)."""
-    return os.environ.get('KFAC_EIGH_LARGE', 'sytrd')
+    return os.environ.get('KFAC_EIGH_LARGE', 'twostage')
 
 
 def _large_bucket(stack: torch.Tensor, warm: torch.Tensor | None
                   ) -> tuple[torch.Tensor, torch.Tensor]:
     n = stack.shape[-1]
+    if _use_twostage(n):
+        _tier('twostage', n, stack.shape[0])
+        w, x, _, _ = twostage.eigh_twostage(stack)
+        return w, x
     if block_jacobi_enabled() and (
         large_algo() == 'block' and (warm is not None or cold_algo() == 'block')
     ):
