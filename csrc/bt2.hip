@@ -30,7 +30,7 @@ namespace {
 
 constexpr int BB = 16;      // band width = reflector length = sweeps per block
 constexpr int BR = 2 * BB;  // block rows
-constexpr int SLAB = 64;    // columns per workgroup
+constexpr int SLAB = 256;   // columns per workgroup
 
 __device__ __forceinline__ int bt_ntasks(int j, int n) { return 1 + (n - 2 - j) / BB; }
 
@@ -82,7 +82,16 @@ __global__ void __launch_bounds__(64) bt2_prep_kernel(const float* __restrict__ 
   for (int e = l; e < BB * BB; e += 64) Tb[e] = T[e / BB][e % BB];
 }
 
-// one step: grid (slabs, G, batch), 256 threads; block (g, k = step - 2 (G-1-g))
+// one step: grid (slabs of 256 columns, active groups, batch), 256 threads;
+// block (g, k = step - 2 (G-1-g)).  Wave w owns columns c0 + 64 w .. +63
+// (four 16-column MFMA tiles); lane l of a tile holds rows
+// 16 rt + 4 (l >> 4) + i (rt = 0, 1; i = 0..3) of its column l & 15, and every
+// product below sums over a permuted k so that each operand the lane needs
+// is already in its own registers: W1 = V^T X (k = row: 8 MFMAs), W2 = T W1
+// (k = 4 (l >> 4) + q: 4 MFMAs), X -= V W2 (2 row tiles x 4 MFMAs), all on
+// v_mfma_f32_16x16x4_f32 (exact f32).
+typedef float v4f __attribute__((ext_vector_type(4)));
+
 __global__ void __launch_bounds__(256) bt2_apply_kernel(
     const float* __restrict__ V2all, int64_t sV2, const float* __restrict__ Tall, int n,
     int kmax, int G, int step, int g_lo, float* __restrict__ Xall, int64_t sX, int ldx) {
@@ -90,15 +99,12 @@ __global__ void __launch_bounds__(256) bt2_apply_kernel(
   const int k = step - 2 * (G - 1 - g);
   const int j0 = BB * g;
   if (k < 0 || j0 >= n - 2 || k >= bt_ntasks(j0, n)) return;
-  const int c0 = blockIdx.x * SLAB;
   const int s = BB * (g + k) + 1;
   const float* V2 = V2all + (int64_t)b * sV2 * BB;
   const float* Tb = Tall + (((int64_t)b * G + g) * kmax + k) * BB * BB;
   float* X = Xall + (int64_t)b * sX;
   __shared__ float Vs[BR][BB + 1];
   __shared__ float Ts[BB][BB + 1];
-  __shared__ float W1p[4][BB][SLAB];
-  __shared__ float W2[BB][SLAB];
   const int tid = threadIdx.x;
   for (int e = tid; e < BR * BB; e += 256) {
     const int rho = e / BB, t = e % BB;
@@ -110,47 +116,44 @@ __global__ void __launch_bounds__(256) bt2_apply_kernel(
     Vs[rho][t] = v;
   }
   Ts[tid / BB][tid % BB] = Tb[tid];
-  const int c = tid & (SLAB - 1), part = tid >> 6;
-  const int col = c0 + c;
-  const bool cok = col < n;
-  float xr[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int row = s + 8 * part + i;
-    xr[i] = (cok && row < n) ? X[(int64_t)row * ldx + col] : 0.f;
-  }
   __syncthreads();
-  // W1 = V^T X (partial over this thread's 8 rows)
+  const int w = tid >> 6, l = tid & 63;
+  const int li = l & 15, lh = l >> 4;
 #pragma unroll
-  for (int t = 0; t < BB; ++t) {
-    float a = 0.f;
+  for (int ct = 0; ct < 4; ++ct) {
+    const int col = blockIdx.x * 256 + 64 * w + 16 * ct + li;
+    const bool cok = col < n;
+    float xq[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) a += Vs[8 * part + i][t] * xr[i];
-    W1p[part][t][c] = a;
-  }
-  __syncthreads();
-  // W2 = T W1: this thread's 4 rows of W2
-#pragma unroll
-  for (int tt = 0; tt < 4; ++tt) {
-    const int t = 4 * part + tt;
-    float a = 0.f;
-#pragma unroll
-    for (int q = 0; q < BB; ++q) {
-      const float w1 = (W1p[0][q][c] + W1p[1][q][c]) + (W1p[2][q][c] + W1p[3][q][c]);
-      a += Ts[t][q] * w1;
+    for (int q = 0; q < 8; ++q) {
+      const int row = s + 16 * (q >> 2) + 4 * lh + (q & 3);
+      xq[q] = (cok && row < n) ? X[(int64_t)row * ldx + col] : 0.f;
     }
-    W2[t][c] = a;
-  }
-  __syncthreads();
-  // X -= V W2
+    // W1[t][col] = sum_rows V[row][t] X[row][col]
+    v4f w1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int rho = 8 * part + i;
-    float a = 0.f;
+    for (int q = 0; q < 8; ++q) {
+      const int rho = 16 * (q >> 2) + 4 * lh + (q & 3);
+      w1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Vs[rho][li], xq[q], w1, 0, 0, 0);
+    }
+    // w1[i] = W1[4 lh + i][col]; W2 = T W1 with k = 4 lh + q
+    v4f w2 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int t = 0; t < BB; ++t) a += Vs[rho][t] * W2[t][c];
-    const int row = s + rho;
-    if (cok && row < n) X[(int64_t)row * ldx + col] = xr[i] - a;
+    for (int q = 0; q < 4; ++q)
+      w2 = __builtin_amdgcn_mfma_f32_16x16x4f32(Ts[li][4 * lh + q], w1[q], w2, 0, 0, 0);
+    // X -= V W2 (row tiles rt = 0, 1; k = 4 lh + q)
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+      v4f d = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        d = __builtin_amdgcn_mfma_f32_16x16x4f32(Vs[16 * rt + li][4 * lh + q], w2[q], d, 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = s + 16 * rt + 4 * lh + i;
+        if (cok && row < n) X[(int64_t)row * ldx + col] = xq[4 * rt + i] - d[i];
+      }
+    }
   }
 }
 

@@ -10,20 +10,25 @@
 // columns and two-sidedly to the diagonal block [J1..J2]^2.  The rest of each
 // bulge stays (bandwidth <= 2*16-2) and is reduced by the next sweeps.
 // Every task touches the 32 x 32 window starting at column j+1+16(k-1), so
-// task (j, k) only has to follow task (j, k-1) and task (j-1, k+2): sweeps
-// run as a pipeline with a lag of three tasks (tools: the float64 oracle in
-// distributed_kfac_pytorch_amd/ops/twostage.py replays the schedule and
-// matches the sequential order bit for bit).
+// task (j, k) only has to follow task (j, k-1) and task (j-1, k+2) (the
+// float64 oracle, ops/twostage.py sb2st_reference(order='pipeline'), replays
+// any schedule with that rule and matches the sequential order bit for bit).
 //
-// One 1024-thread workgroup per matrix: wave w runs sweeps w, w+16, ...;
-// per-wave progress words in LDS order the pipeline (workgroup-scope
-// release / acquire: the waves share the CU's L1; band loads bypass it).
-// The band lives in L2-resident global memory, column-major with 32
-// distances per column (AB[c][d] = B[c+d][c]); padding columns past n are
-// zero so windows never need bounds checks.  A task's operands sit in
-// registers, one 16-row block per lane group: lane (r, grp) holds 8 columns
-// of row r of the bulge block (grp 0, 1) or of the diagonal block (grp 2, 3).
-// Reflectors (v[0] = 1 stored, tau) go to V2[j][k][16] / tau2[j][k] for the
+// Work layout: one 768-thread workgroup per matrix (12 waves, 150 VGPRs: no
+// spills); each wave runs FOUR
+// sweeps at once, one per 16-lane DPP row ("group"), lane r of a group owning
+// row r of the task's bulge block and of its diagonal block (16 + 16 values).
+// The four groups advance in lockstep, group g executing task k = t - 4g at
+// step t: a lag of four tasks (one more than the dependency rule needs), so
+// the operands of step t+1 were written two steps earlier and are loaded
+// while step t computes.  Row reductions are DPP row sums, column sums and
+// broadcasts go through the wave's LDS slice.  Wave w runs sweeps
+// 48 rho + 4 w + g in round rho; the first group of a wave follows the last
+// group of the previous wave through per-wave progress words in LDS
+// (workgroup-scope release / acquire; band loads bypass L1).  The band lives
+// in L2-resident global memory, column-major with 32 distances per column
+// (AB[c][d] = B[c+d][c]); padding columns past n are zero.  Reflectors
+// (v[0] = 1 stored, tau) go to V2[j][k][16] / tau2[j][k] for the
 // back-transform (csrc/bt2.hip).
 #include "common.h"
 
@@ -32,10 +37,13 @@ namespace kfac {
 namespace {
 
 constexpr int S2_B = 16;
-constexpr int S2_LD = 2 * S2_B;  // band storage: distances 0..31 per column
-constexpr int S2_WAVES = 16;
+constexpr int S2_LD = 2 * S2_B;   // band storage: distances 0..31 per column
+constexpr int S2_WAVES = 12;
 constexpr int S2_T = 64 * S2_WAVES;
+constexpr int S2_LAG = 4;         // tasks between consecutive sweeps
 constexpr int S2_SPIN_LIMIT = 1 << 24;  // ~1 s: a correct run waits microseconds
+constexpr int S2_RS = 1 << 20;    // progress word: round * S2_RS + steps done
+constexpr int S2_TLD = 20;        // LDS transpose row stride (16-B aligned rows)
 
 __device__ __forceinline__ int ntasks(int j, int n) { return 1 + (n - 2 - j) / S2_B; }
 
@@ -48,11 +56,43 @@ __device__ __forceinline__ float row_sum16(float v) {
   return v;
 }
 
-__device__ __forceinline__ float rdlane(float v, int lane) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), lane));
+__device__ __forceinline__ float ld_nt(const float* p) { return __builtin_nontemporal_load(p); }
+
+struct Task {
+  int j, k, g0;
+  bool on;
+};
+
+__device__ __forceinline__ Task task_of(int rho, int w, int g, int t, int n) {
+  Task s;
+  s.j = 4 * S2_WAVES * rho + 4 * w + g;
+  s.k = t - S2_LAG * g;
+  s.on = s.j < n - 2 && s.k >= 0 && s.k < ntasks(s.j, n);
+  s.g0 = s.k == 0 ? s.j - (S2_B - 1) : s.j + 1 + (s.k - 1) * S2_B;
+  return s;
 }
 
-__device__ __forceinline__ float ld_nt(const float* p) { return __builtin_nontemporal_load(p); }
+// bulge-block row r (task 0: only its last column, column j) and diagonal
+// block row r (both triangles from the symmetric band storage)
+__device__ __forceinline__ void load_task(const float* AB, const Task& s, int r,
+                                          float (&bk)[S2_B], float (&dd)[S2_B]) {
+#pragma unroll
+  for (int c = 0; c < S2_B; ++c) {
+    bk[c] = 0.f;
+    dd[c] = 0.f;
+  }
+  if (!s.on) return;
+  if (s.k == 0) {
+    bk[S2_B - 1] = ld_nt(AB + (int64_t)(s.g0 + S2_B - 1) * S2_LD + (r + 1));
+  } else {
+#pragma unroll
+    for (int c = 0; c < S2_B; ++c) bk[c] = ld_nt(AB + (int64_t)(s.g0 + c) * S2_LD + (S2_B + r - c));
+  }
+#pragma unroll
+  for (int c = 0; c < S2_B; ++c)
+    dd[c] = r >= c ? ld_nt(AB + (int64_t)(s.g0 + S2_B + c) * S2_LD + (r - c))
+                   : ld_nt(AB + (int64_t)(s.g0 + S2_B + r) * S2_LD + (c - r));
+}
 
 __global__ void __launch_bounds__(S2_T) sb2st_kernel(float* __restrict__ ABall, int64_t sAB,
                                                      int n, float* __restrict__ V2all,
@@ -65,77 +105,79 @@ __global__ void __launch_bounds__(S2_T) sb2st_kernel(float* __restrict__ ABall, 
   float* V2 = V2all + (int64_t)b * sV2 * S2_B;
   float* tau2s = tau2all + (int64_t)b * sV2;
   __shared__ int prog[S2_WAVES];
+  __shared__ __attribute__((aligned(16))) float tb[S2_WAVES][4][S2_B * S2_TLD];
+  __shared__ __attribute__((aligned(16))) float bc[S2_WAVES][4][S2_B];
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-  const int r = l & 15, grp = l >> 4;
-  const bool hi = (grp & 1) != 0;
-  const bool isD = grp >= 2;
-  if (l == 0) prog[w] = (w - S2_WAVES) * 65536 + 0xFFFF;  // "sweep w-16 done"
+  const int r = l & 15, g = l >> 4;
+  float* tbg = &tb[w][g][0];
+  float* bcg = &bc[w][g][0];
+  if (l == 0) prog[w] = -1;
   __syncthreads();
   bool abort = false;
   const int nsweep = n - 2;
+  const int rounds = (nsweep + 4 * S2_WAVES - 1) / (4 * S2_WAVES);
+  const int pw = (w + S2_WAVES - 1) % S2_WAVES;
 
-  for (int j = w; j < nsweep && !abort; j += S2_WAVES) {
-    const int nk = ntasks(j, n);
-    const int nkp = j > 0 ? ntasks(j - 1, n) : 0;
-    float vpc[8];  // previous reflector at this lane's 8 columns
+  // waits until the previous sweep (last group of the previous wave) has
+  // finished task q (its round prho); q >= its task count means "finished"
+  auto wait_pred = [&](int prho, int q) {
+    const int target = prho * S2_RS + q + 1 + S2_LAG * 3;
+    int spins = 0;
+    while (__hip_atomic_load(&prog[pw], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <
+           target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > S2_SPIN_LIMIT) {
+        abort = true;
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  };
+
+  for (int rho = 0; rho < rounds && !abort; ++rho) {
+    const int j0 = 4 * S2_WAVES * rho + 4 * w;  // this wave's group-0 sweep
+    if (j0 >= nsweep) break;
+    int steps = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) vpc[i] = 0.f;
+    for (int q = 0; q < 4; ++q) {
+      const int jq = j0 + q;
+      if (jq < nsweep) steps = max(steps, S2_LAG * q + ntasks(jq, n));
+    }
+    const int prho = w == 0 ? rho - 1 : rho;
+    const bool has_pred = j0 > 0;
+    const int nkp = has_pred ? ntasks(j0 - 1, n) : 0;
+    float bk[S2_B], dd[S2_B], nbk[S2_B], ndd[S2_B], vp[S2_B];
     float taup = 0.f;
-    for (int k = 0; k < nk; ++k) {
-      // ---- wait for task (j-1, min(k+2, nkp-1))
-      if (j > 0) {
-        const int need = k + 3 < nkp ? k + 3 : 0xFFFF;
-        const int target = (j - 1) * 65536 + need;
-        int spins = 0;
-        while (__hip_atomic_load(&prog[(w + S2_WAVES - 1) % S2_WAVES], __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_WORKGROUP) < target) {
-          __builtin_amdgcn_s_sleep(1);
-          if (++spins > S2_SPIN_LIMIT) {
-            abort = true;
-            break;
-          }
-        }
+#pragma unroll
+    for (int c = 0; c < S2_B; ++c) vp[c] = 0.f;
+    // operands of step 0 (group 0's task 0 needs the previous sweep's task 2)
+    if (has_pred) wait_pred(prho, min(2, nkp - 1));
+    if (abort) break;
+    load_task(AB, task_of(rho, w, g, 0, n), r, bk, dd);
+    for (int t = 0; t < steps; ++t) {
+      const Task s = task_of(rho, w, g, t, n);
+      // ---- prefetch step t+1 (written at step t-1 or earlier: complete)
+      if (has_pred && t + 1 < steps) {
+        const int k1 = t + 1;  // group 0's next task
+        if (k1 < ntasks(j0, n)) wait_pred(prho, min(k1 + 2, nkp - 1));
         if (abort) break;
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
       }
-      const bool first = k == 0;
-      const int g0 = first ? j - (S2_B - 1) : j + 1 + (k - 1) * S2_B;
+      load_task(AB, task_of(rho, w, g, t + 1, n), r, nbk, ndd);
+      const bool first = s.k == 0;
 
-      // ---- operands
-      float x[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int c = 8 * (hi ? 1 : 0) + i;
-        float v = 0.f;
-        if (!isD) {
-          const int C = g0 + c;
-          if (C >= 0) v = ld_nt(AB + (int64_t)C * S2_LD + (S2_B + r - c));
-        } else {
-          v = r >= c ? ld_nt(AB + (int64_t)(g0 + S2_B + c) * S2_LD + (r - c))
-                     : ld_nt(AB + (int64_t)(g0 + S2_B + r) * S2_LD + (c - r));
-        }
-        x[i] = v;
-      }
-
-      // ---- (1) bulge block <- bulge block * H_prev (rows dot v_prev)
+      // ---- (1) bulge block <- bulge block * H_prev (row r dot v_prev)
       if (!first) {
-        float s = 0.f;
+        float sdot = 0.f;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) s += x[i] * vpc[i];
-        s += __shfl_xor(s, 16, 64);
-        if (!isD) {
-          const float f = taup * s;
+        for (int c = 0; c < S2_B; ++c) sdot += bk[c] * vp[c];
+        const float f = taup * sdot;
 #pragma unroll
-          for (int i = 0; i < 8; ++i) x[i] -= f * vpc[i];
-        }
+        for (int c = 0; c < S2_B; ++c) bk[c] -= f * vp[c];
       }
-
       // ---- (2) reflector of the block's first column (task 0: column j)
-      const int hgrp = first ? 1 : 0;
-      const float hx = first ? x[7] : x[0];
-      const float alpha = rdlane(hx, hgrp * 16);
-      const float sq = row_sum16((grp == hgrp && r >= 1) ? hx * hx : 0.f);
-      const float xn2 = rdlane(sq, hgrp * 16);
+      const float hx = first ? bk[S2_B - 1] : bk[0];
+      const float alpha = row_sum16(r == 0 ? hx : 0.f);
+      const float xn2 = row_sum16(r >= 1 ? hx * hx : 0.f);
       float tau, beta, scale;
       if (xn2 == 0.f) {
         tau = 0.f;
@@ -146,69 +188,95 @@ __global__ void __launch_bounds__(S2_T) sb2st_kernel(float* __restrict__ ABall, 
         tau = (beta - alpha) / beta;
         scale = 1.f / (alpha - beta);
       }
-      const float vr_own = r == 0 ? 1.f : hx * scale;  // valid in group hgrp
-      // the new reflector at this lane's 8 columns and at its row
-      float v2c[8];
+      const float v2r = r == 0 ? 1.f : hx * scale;
+      const float hn = r == 0 ? beta : 0.f;
+      if (first) bk[S2_B - 1] = hn;
+      else bk[0] = hn;
+      // broadcast v2 to the group (vp is dead from here on: reuse it)
+      bcg[r] = v2r;
+      __builtin_amdgcn_wave_barrier();
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const float lo = rdlane(vr_own, hgrp * 16 + i), up = rdlane(vr_own, hgrp * 16 + 8 + i);
-        v2c[i] = hi ? up : lo;
+      for (int q = 0; q < S2_B / 4; ++q) {
+        const float4 v4 = reinterpret_cast<const float4*>(bcg)[q];
+        vp[4 * q] = v4.x;
+        vp[4 * q + 1] = v4.y;
+        vp[4 * q + 2] = v4.z;
+        vp[4 * q + 3] = v4.w;
       }
-      const float v2r = __shfl(vr_own, hgrp * 16 + r, 64);
-      if (grp == hgrp) {
-        const float hn = r == 0 ? beta : 0.f;
-        if (first) x[7] = hn;
-        else x[0] = hn;
-      }
-
-      // ---- (3) H v-left-apply to the bulge block's other columns
+      __builtin_amdgcn_wave_barrier();
+      // ---- (3) H left-applied to the bulge block's other columns
       if (!first) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const float wsum = row_sum16(v2r * x[i]);
-          if (!isD && !(grp == 0 && i == 0)) x[i] -= tau * v2r * wsum;
+        for (int q = 0; q < S2_B / 4; ++q)
+          reinterpret_cast<float4*>(tbg + r * S2_TLD)[q] =
+              make_float4(v2r * bk[4 * q], v2r * bk[4 * q + 1], v2r * bk[4 * q + 2],
+                          v2r * bk[4 * q + 3]);
+        __builtin_amdgcn_wave_barrier();
+        float wcol = 0.f;  // column r sum
+#pragma unroll
+        for (int q = 0; q < S2_B; ++q) wcol += tbg[q * S2_TLD + r];
+        __builtin_amdgcn_wave_barrier();
+        tbg[r] = wcol;  // row 0 of the slice is free again (every lane read it)
+        __builtin_amdgcn_wave_barrier();
+        const float f = tau * v2r;
+#pragma unroll
+        for (int q = 0; q < S2_B / 4; ++q) {
+          const float4 w4 = reinterpret_cast<const float4*>(tbg)[q];
+          if (q > 0) bk[4 * q] -= f * w4.x;  // column 0 holds the reflector
+          bk[4 * q + 1] -= f * w4.y;
+          bk[4 * q + 2] -= f * w4.z;
+          bk[4 * q + 3] -= f * w4.w;
         }
+        __builtin_amdgcn_wave_barrier();
       }
-
       // ---- (4) diagonal block <- H D H
       float y = 0.f;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) y += x[i] * v2c[i];
-      y += __shfl_xor(y, 16, 64);  // D rows: grp 2 <-> 3
-      const float gpart = row_sum16(grp == 2 ? v2r * y : 0.f);
-      const float gamma = rdlane(gpart, 32);
+      for (int c = 0; c < S2_B; ++c) y += dd[c] * vp[c];
+      const float gamma = row_sum16(v2r * y);
       const float z = tau * y - 0.5f * tau * tau * gamma * v2r;
+      bcg[r] = z;
+      __builtin_amdgcn_wave_barrier();
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const float lo = rdlane(z, 32 + i), up = rdlane(z, 40 + i);
-        const float zc = hi ? up : lo;
-        if (isD) x[i] -= v2r * zc + z * v2c[i];
+      for (int q = 0; q < S2_B / 4; ++q) {
+        const float4 z4 = reinterpret_cast<const float4*>(bcg)[q];
+        dd[4 * q] -= v2r * z4.x + z * vp[4 * q];
+        dd[4 * q + 1] -= v2r * z4.y + z * vp[4 * q + 1];
+        dd[4 * q + 2] -= v2r * z4.z + z * vp[4 * q + 2];
+        dd[4 * q + 3] -= v2r * z4.w + z * vp[4 * q + 3];
       }
-
+      __builtin_amdgcn_wave_barrier();
       // ---- (5) write back
+      if (s.on) {
+        if (first) {
+          AB[(int64_t)(s.g0 + S2_B - 1) * S2_LD + (r + 1)] = bk[S2_B - 1];
+        } else {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int c = 8 * (hi ? 1 : 0) + i;
-        if (!isD) {
-          if (!first || (grp == 1 && i == 7))
-            AB[(int64_t)(g0 + c) * S2_LD + (S2_B + r - c)] = x[i];
-        } else if (r >= c) {
-          AB[(int64_t)(g0 + S2_B + c) * S2_LD + (r - c)] = x[i];
+          for (int c = 0; c < S2_B; ++c)
+            AB[(int64_t)(s.g0 + c) * S2_LD + (S2_B + r - c)] = bk[c];
         }
-      }
-      if (grp == hgrp) V2[((int64_t)j * kmax + k) * S2_B + r] = vr_own;
-      if (l == 0) tau2s[(int64_t)j * kmax + k] = tau;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) vpc[i] = v2c[i];
+        for (int c = 0; c < S2_B; ++c)
+          if (c <= r) AB[(int64_t)(s.g0 + S2_B + c) * S2_LD + (r - c)] = dd[c];
+        V2[((int64_t)s.j * kmax + s.k) * S2_B + r] = v2r;
+        if (r == 0) tau2s[(int64_t)s.j * kmax + s.k] = tau;
+      }
       taup = tau;
-
-      // ---- publish (j, k) done
+      // ---- publish step t (its stores, and the prefetch, complete)
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (l == 0)
-        __hip_atomic_store(&prog[w], j * 65536 + (k + 1 == nk ? 0xFFFF : k + 1),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_store(&prog[w], rho * S2_RS + t + 1, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+      for (int c = 0; c < S2_B; ++c) {
+        bk[c] = nbk[c];
+        dd[c] = ndd[c];
+      }
     }
+    if (l == 0)
+      __hip_atomic_store(&prog[w], rho * S2_RS + (S2_RS - 1), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   if (abort && l == 0) atomicOr(err, 1);
   __syncthreads();

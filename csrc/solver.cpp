@@ -370,3 +370,7 @@ std::vector<at::Tensor> spd_inverse_blocked(at::Tensor F, double damping) {
                          (int)cnt, (float)damping, s);
   return {X, fail};
 }
+
+// rocBLAS handle bound to stream s (shared with the two-stage eigensolver's
+// strided GEMMs, csrc/twostage_host.cpp)
+rocblas_handle kfac_rocblas_handle(hipStream_t s) { return handle_for(s).handle; }

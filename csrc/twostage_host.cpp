@@ -15,6 +15,7 @@
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 
 #include <hip/hip_runtime.h>
+#include <rocblas/rocblas.h>
 
 #include <algorithm>
 #include <cstdlib>
@@ -26,6 +27,9 @@ int twostage_band();
 int twostage_max_n();
 void sb_panel_qr(float* A, int64_t sA, int ld, int n, int p, int batch, float* Vw, float* Uw,
                  int64_t sVU, float* tau1, int64_t sTau, float* Tw, hipStream_t stream);
+void sb_update(float* A, int64_t sA, int ld, int n, int p, int batch, const float* Vw,
+               const float* Uw, int64_t sVU, const float* Tw, float* Ypart, float* Spart,
+               float* Ms, float* Ww, hipStream_t stream);
 void sb_extract(const float* A, int64_t sA, int ld, int n, int batch, float* AB, int64_t sAB,
                 int ncols, hipStream_t stream);
 int sb2st_kmax(int n);
@@ -39,6 +43,13 @@ void bt2_apply(const float* V2, int64_t sV2, const float* T, int n, int kmax, in
 }  // namespace kfac
 
 std::vector<at::Tensor> tridiag_eigh_dc(const at::Tensor& d, const at::Tensor& e);
+rocblas_handle kfac_rocblas_handle(hipStream_t s);
+
+#define TS_ROCBLAS(expr)                                                         \
+  do {                                                                           \
+    rocblas_status _s = (expr);                                                  \
+    TORCH_CHECK(_s == rocblas_status_success, "rocBLAS error ", (int)_s, " in ", #expr); \
+  } while (0)
 
 namespace {
 
@@ -49,7 +60,7 @@ hipStream_t cur() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().str
 // nb reflectors per UT block (T^-1 = striu(V^T V) + diag(1/tau)), last block
 // first.
 void apply_q1(const at::Tensor& A, const at::Tensor& tau1, int64_t n, int64_t nref,
-              at::Tensor& X, int64_t nb) {
+              at::Tensor& X, int64_t nb, rocblas_handle hb) {
   const int64_t off = kfac::twostage_band();
   auto fopt = X.options();
   const int64_t b = X.size(0);
@@ -68,10 +79,34 @@ void apply_q1(const at::Tensor& A, const at::Tensor& tau1, int64_t n, int64_t nr
     auto dinv = at::where(t.eq(0), at::ones_like(t), at::reciprocal(at::where(t.eq(0),
                                                                                 at::ones_like(t), t)));
     auto u = at::triu(g, 1) + at::diag_embed(dinv);
-    auto tm = at::linalg_solve_triangular(u, at::eye(bs, fopt).expand({b, bs, bs}), true);
-    auto xs = X.narrow(1, p0 + off, rows);
-    auto w = at::bmm(tm, at::bmm(vt, xs));
-    xs.baddbmm_(vt.transpose(1, 2), w, 1.0, -1.0);
+    // tm = u^-1 (u upper triangular, row-major) by rocBLAS trsm on the
+    // column-major view (u^T, lower): the result read row-major is u^-1
+    u = u.contiguous();
+    auto tm = at::eye(bs, fopt).expand({b, bs, bs}).contiguous();
+    {
+      const float one1 = 1.f;
+      TS_ROCBLAS(rocblas_strsm_strided_batched(
+          hb, rocblas_side_left, rocblas_fill_lower, rocblas_operation_none,
+          rocblas_diagonal_non_unit, (int)bs, (int)bs, &one1, u.data_ptr<float>(), (int)bs,
+          bs * bs, tm.data_ptr<float>(), (int)bs, bs * bs, (int)b));
+    }
+    // rows p0+off.. of X in place (leading dimension n): rocBLAS, row-major
+    // operands as column-major transposes (ATen would copy the block)
+    vt = vt.contiguous();
+    float* xs = X.data_ptr<float>() + (p0 + off) * n;
+    auto w1 = at::empty({b, bs, n}, fopt);
+    const float one = 1.f, zero = 0.f, mone = -1.f;
+    // W1 = V^T-rows * Xs  <=>  W1^T = Xs^T vt^T
+    TS_ROCBLAS(rocblas_sgemm_strided_batched(
+        hb, rocblas_operation_none, rocblas_operation_none, (int)n, (int)bs, (int)rows, &one, xs,
+        (int)n, n * n, vt.data_ptr<float>(), (int)rows, bs * rows, &zero, w1.data_ptr<float>(),
+        (int)n, bs * n, (int)b));
+    auto w2 = at::bmm(tm, w1).contiguous();
+    // Xs -= vt^T W2  <=>  Xs^T -= W2^T vt
+    TS_ROCBLAS(rocblas_sgemm_strided_batched(
+        hb, rocblas_operation_none, rocblas_operation_transpose, (int)n, (int)rows, (int)bs,
+        &mone, w2.data_ptr<float>(), (int)n, bs * n, vt.data_ptr<float>(), (int)rows, bs * rows,
+        &one, xs, (int)n, n * n, (int)b));
   }
 }
 
@@ -110,6 +145,13 @@ std::vector<at::Tensor> eigh_twostage(const at::Tensor& A_in, bool timed) {
   auto tau1 = at::zeros({b, n}, fopt);
   auto Tw = at::empty({b, B, B}, fopt);
   int64_t nref = 0;
+  rocblas_handle hb = kfac_rocblas_handle(s);
+  TS_ROCBLAS(rocblas_set_pointer_mode(hb, rocblas_pointer_mode_host));
+  const int64_t nblk = (n + 63) / 64;
+  auto Ypart = at::empty({8, b, n, B}, fopt);
+  auto Spart = at::empty({b, nblk * 8, B * B}, fopt);
+  auto Ms = at::empty({b, B, B}, fopt);
+  auto Ww = at::empty({b, n, B}, fopt);
   // ---- stage 1
   for (int64_t p = 0; n - p - B >= 2; p += B) {
     const int64_t m = n - p - B;
@@ -117,15 +159,10 @@ std::vector<at::Tensor> eigh_twostage(const at::Tensor& A_in, bool timed) {
                       Vw.data_ptr<float>(), Uw.data_ptr<float>(), n * B, tau1.data_ptr<float>(),
                       n, Tw.data_ptr<float>(), s);
     nref = p + B;
-    auto A22 = A.narrow(1, p + B, m).narrow(2, p + B, m);
-    auto V = Vw.narrow(1, 0, m);
-    auto U = Uw.narrow(1, 0, m);
-    auto Y = at::bmm(A22, U);
-    auto S = at::bmm(V.transpose(1, 2), Y);
-    auto M = at::bmm(Tw.transpose(1, 2), S);
-    auto Ms = (M + M.transpose(1, 2)) * 0.5;
-    auto W = at::baddbmm(Y, V, Ms, 1.0, -0.5);
-    A22.baddbmm_(at::cat({V, W}, 2), at::cat({W, V}, 2).transpose(1, 2), 1.0, -1.0);
+    kfac::sb_update(A.data_ptr<float>(), n * ld, (int)ld, (int)n, (int)p, (int)b,
+                    Vw.data_ptr<float>(), Uw.data_ptr<float>(), n * B, Tw.data_ptr<float>(),
+                    Ypart.data_ptr<float>(), Spart.data_ptr<float>(), Ms.data_ptr<float>(),
+                    Ww.data_ptr<float>(), s);
   }
   mark();
   // ---- stage 2
@@ -159,7 +196,7 @@ std::vector<at::Tensor> eigh_twostage(const at::Tensor& A_in, bool timed) {
   kfac::bt2_apply(V2.data_ptr<float>(), nslot, T2.data_ptr<float>(), (int)n, kmax, (int)b,
                   X.data_ptr<float>(), n * n, (int)n, s);
   mark();
-  if (nref > 0) apply_q1(A, tau1, n, nref, X, 512);
+  if (nref > 0) apply_q1(A, tau1, n, nref, X, 512, hb);
   mark();
   at::Tensor times = at::zeros({std::max<int64_t>((int64_t)ev.size() - 1, 0)},
                                at::TensorOptions().dtype(at::kFloat));

@@ -219,6 +219,8 @@ def _large_bucket(stack: torch.Tensor, warm: torch.Tensor | None
     n = stack.shape[-1]
     if _use_twostage(n):
         _tier('twostage', n, stack.shape[0])
+        if twostage.graphs_enabled():
+            return twostage.eigh_twostage_graphed(stack)
         w, x, _, _ = twostage.eigh_twostage(stack)
         return w, x
     if block_jacobi_enabled() and (
@@ -247,7 +249,10 @@ def _gpu_bucket(stack: torch.Tensor, warm: torch.Tensor | None = None
     if n <= JACOBI_MAX_N:
         _tier('jacobi', n, stack.shape[0])
         return lib.jacobi_eigh(stack.contiguous(), JACOBI_SWEEPS, JACOBI_TOL)
-    if warm is not None and block_jacobi_enabled() and n <= WARM_ACCEPT_MAX_N:
+    # the two-stage tier needs no warm start: the acceptance test's host
+    # read-back would cost more than the solves it saves
+    if (warm is not None and block_jacobi_enabled() and n <= WARM_ACCEPT_MAX_N
+            and not _use_twostage(n)):
         idx, r, q = _accept_warm(stack, warm)
         last_stats.setdefault('accepted', []).extend([n] * len(idx))
         if len(idx) == stack.shape[0]:

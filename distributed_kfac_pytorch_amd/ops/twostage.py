@@ -27,10 +27,13 @@ kernels against them / float64 ``eigh`` on the GPU.
 """
 from __future__ import annotations
 
+import logging
+
 import torch
 
 from distributed_kfac_pytorch_amd.ops._native import native
 
+logger = logging.getLogger(__name__)
 BAND = 16
 
 
@@ -230,3 +233,52 @@ def eigh_twostage(stack: torch.Tensor, timed: bool = False
     tridiagonal solve, the stage-2 and the stage-1 back-transforms."""
     w, x, err, ms = native().eigh_twostage(stack.contiguous(), timed)
     return w, x, err, ms
+
+
+_graphs: dict = {}
+
+
+def graphs_enabled() -> bool:
+    """``KFAC_TWOSTAGE_GRAPHS=1`` (default off): replay each (size, batch)
+    signature's whole solve from one captured HIP graph."""
+    import os
+
+    return os.environ.get('KFAC_TWOSTAGE_GRAPHS', '0') == '1'
+
+
+def eigh_twostage_graphed(stack: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """``eigh_twostage`` replayed from a HIP graph per ``(device, n, batch)``.
+
+    A 4608 factor's stage 1 alone is ~290 panels of ~10 launches; issued
+    from the host one by one they are launch-bound.  The first call of a
+    signature runs eagerly (its result is returned) and then captures the
+    same solve on static buffers (thread-local capture: other eigensolver
+    lanes keep running); later calls copy the input in and replay.  The
+    returned tensors are the graph's static outputs: valid until the next
+    call with the same signature (the eigen layers copy them into their own
+    buffers when they install a refresh)."""
+    key = (stack.device, tuple(stack.shape), torch.cuda.current_stream(stack.device).cuda_stream)
+    if key not in _graphs:
+        static_in = stack.contiguous().clone()
+        w, x, err, _ = eigh_twostage(static_in)
+        g = torch.cuda.CUDAGraph()
+        ent = None
+        try:
+            g.capture_begin(capture_error_mode='thread_local')
+            try:
+                outs = eigh_twostage(static_in)
+            finally:
+                g.capture_end()
+            ent = (g, static_in, outs)
+        except RuntimeError as e:  # not capturable here: stay eager for this signature
+            logger.warning('two-stage eigensolver graph capture failed (%s); eager', e)
+        _graphs[key] = ent
+        return w, x
+    ent = _graphs[key]
+    if ent is None:
+        w, x, _, _ = eigh_twostage(stack)
+        return w, x
+    g, static_in, outs = ent
+    static_in.copy_(stack)
+    g.replay()
+    return outs[0], outs[1]

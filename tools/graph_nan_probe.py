@@ -26,18 +26,28 @@ from distributed_kfac_pytorch_amd.models.resnet import resnet50  # noqa: E402
 from distributed_kfac_pytorch_amd.ops.cast import enable_fused_weight_cast  # noqa: E402
 
 
+_FUSED_SGD = False
+_CL = True
+_IMG = 64
+_BATCH = 8
+
+
 def build(base, dev, graphs: bool, amp: bool, fused_cast: bool, warmup: int = 1,
           kfac_on: bool = True, factor_steps: int = 2):  # type: ignore[no-untyped-def]
-    model = copy.deepcopy(base).to(dev).to(memory_format=torch.channels_last)
+    model = copy.deepcopy(base).to(dev)
+    if _CL:
+        model = model.to(memory_format=torch.channels_last)
     if fused_cast and amp:
         enable_fused_weight_cast(model)
-    opt = torch.optim.SGD(model.parameters(), lr=0.01, momentum=0.9, weight_decay=5e-5)
+    opt = torch.optim.SGD(model.parameters(), lr=0.01, momentum=0.9, weight_decay=5e-5,
+                          **({'fused': True} if _FUSED_SGD else {}))
     pre = kfac.KFACPreconditioner(
         model, factor_update_steps=factor_steps, inv_update_steps=8, damping=0.001,
         kl_clip=0.001, lr=lambda s: opt.param_groups[0]['lr'],
         grad_worker_fraction=0.5) if kfac_on else None
-    x = torch.empty(8, 3, 64, 64, device=dev).contiguous(memory_format=torch.channels_last)
-    y = torch.empty(8, dtype=torch.long, device=dev)
+    x = torch.empty(_BATCH, 3, _IMG, _IMG, device=dev).contiguous(
+        memory_format=torch.channels_last if _CL else torch.contiguous_format)
+    y = torch.empty(_BATCH, dtype=torch.long, device=dev)
     crit = torch.nn.CrossEntropyLoss(label_smoothing=0.1)
 
     def fb() -> torch.Tensor:
@@ -99,22 +109,36 @@ def main() -> None:
     ap.add_argument('--warmup', type=int, default=1)
     ap.add_argument('--no-kfac', action='store_true')
     ap.add_argument('--factor-steps', type=int, default=2)
+    ap.add_argument('--benchmark', type=int, default=0)
+    ap.add_argument('--compare', default='graphs', choices=['graphs', 'stepgraphs'],
+                    help='graphs: A = GraphedTrainStep, B = eager; stepgraphs: A = eager '
+                         'with StepGraphs, B = eager without (both eager)')
+    ap.add_argument('--image', type=int, default=64)
+    ap.add_argument('--batch', type=int, default=8)
+    ap.add_argument('--fused-sgd', type=int, default=0)
+    ap.add_argument('--channels-last', type=int, default=1)
     args = ap.parse_args()
     torch.backends.cudnn.deterministic = bool(args.deterministic)
+    torch.backends.cudnn.benchmark = bool(args.benchmark)
+    global _FUSED_SGD, _CL, _IMG, _BATCH
+    _FUSED_SGD, _CL = bool(args.fused_sgd), bool(args.channels_last)
+    _IMG, _BATCH = args.image, args.batch
     dev = torch.device('cuda')
     torch.manual_seed(0)
     base = resnet50(num_classes=10)
-    A = build(base, dev, True, not args.fp32, bool(args.fused_cast), args.warmup,
-              not args.no_kfac, args.factor_steps)
+    A = build(base, dev, args.compare == 'graphs', not args.fp32, bool(args.fused_cast),
+              args.warmup, not args.no_kfac, args.factor_steps)
     B = build(base, dev, False, not args.fp32, bool(args.fused_cast), 1,
               not args.no_kfac, args.factor_steps)
+    if B[2] is not None:
+        B[2]._graphs = None  # the eager twin never replays precondition graphs
     gen = torch.Generator(device='cpu').manual_seed(1)
-    pool = [(torch.randn(8, 3, 64, 64, generator=gen), torch.randint(0, 10, (8,), generator=gen))
-            for _ in range(4)]
+    pool = [(torch.randn(_BATCH, 3, _IMG, _IMG, generator=gen),
+             torch.randint(0, 10, (_BATCH,), generator=gen)) for _ in range(4)]
     env = {k: v for k, v in os.environ.items() if k.startswith('KFAC_')}
     for i in range(args.steps):
-        kind = A[5].kind()
-        cap0, rep0 = A[5].captures, A[5].replays
+        kind = A[5].kind() if hasattr(A[5], 'kind') else '-'
+        cap0, rep0 = getattr(A[5], 'captures', 0), getattr(A[5], 'replays', 0)
         x, y = pool[i % len(pool)]
         for m in (A, B):
             m[3].copy_(x)
@@ -123,8 +147,8 @@ def main() -> None:
         lb = B[5]()
         torch.cuda.synchronize()
         sa, sb = state(*A[:3]), state(*B[:3])
-        how = 'replay' if A[5].replays > rep0 else 'eager'
-        if A[5].captures > cap0:
+        how = 'replay' if getattr(A[5], 'replays', 0) > rep0 else 'eager'
+        if getattr(A[5], 'captures', 0) > cap0:
             how += '+capture'
         rec: dict = {'step': i, 'kind': kind, 'how': how, 'env': env,
                      'loss': [float(la), float(lb)]}
