@@ -94,7 +94,8 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 
 __global__ void __launch_bounds__(256) bt2_apply_kernel(
     const float* __restrict__ V2all, int64_t sV2, const float* __restrict__ Tall, int n,
-    int kmax, int G, int step, int g_lo, float* __restrict__ Xall, int64_t sX, int ldx) {
+    int kmax, int G, int step, int g_lo, int per, float* __restrict__ Xall, int64_t sX,
+    int ldx) {
   const int g = g_lo + (int)blockIdx.y, b = blockIdx.z;
   const int k = step - 2 * (G - 1 - g);
   const int j0 = BB * g;
@@ -119,40 +120,60 @@ __global__ void __launch_bounds__(256) bt2_apply_kernel(
   __syncthreads();
   const int w = tid >> 6, l = tid & 63;
   const int li = l & 15, lh = l >> 4;
+  // `per` slabs of 256 columns per workgroup (V, T staged once); a slab's X
+  // (4 column tiles x 8 rows per lane) is loaded in one burst before its
+  // MFMAs, and the next slab's burst is issued before this slab's MFMAs
+  const int sl0 = blockIdx.x * per, sl1 = min((int)(blockIdx.x + 1) * per, (n + 255) / 256);
+  float xq[4][8], xn[4][8];
+  auto load_slab = [&](int sl, float (&dst)[4][8]) {
 #pragma unroll
-  for (int ct = 0; ct < 4; ++ct) {
-    const int col = blockIdx.x * 256 + 64 * w + 16 * ct + li;
-    const bool cok = col < n;
-    float xq[8];
+    for (int ct = 0; ct < 4; ++ct) {
+      const int col = sl * 256 + 64 * w + 16 * ct + li;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int row = s + 16 * (q >> 2) + 4 * lh + (q & 3);
-      xq[q] = (cok && row < n) ? X[(int64_t)row * ldx + col] : 0.f;
+      for (int q = 0; q < 8; ++q) {
+        const int row = s + 16 * (q >> 2) + 4 * lh + (q & 3);
+        dst[ct][q] = (col < n && row < n) ? X[(int64_t)row * ldx + col] : 0.f;
+      }
     }
-    // W1[t][col] = sum_rows V[row][t] X[row][col]
-    v4f w1 = {0.f, 0.f, 0.f, 0.f};
+  };
+  if (sl0 < sl1) load_slab(sl0, xq);
+  for (int sl = sl0; sl < sl1; ++sl) {
+    if (sl + 1 < sl1) load_slab(sl + 1, xn);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int rho = 16 * (q >> 2) + 4 * lh + (q & 3);
-      w1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Vs[rho][li], xq[q], w1, 0, 0, 0);
-    }
-    // w1[i] = W1[4 lh + i][col]; W2 = T W1 with k = 4 lh + q
-    v4f w2 = {0.f, 0.f, 0.f, 0.f};
+    for (int ct = 0; ct < 4; ++ct) {
+      const int col = sl * 256 + 64 * w + 16 * ct + li;
+      const bool cok = col < n;
+      // W1[t][col] = sum_rows V[row][t] X[row][col]
+      v4f w1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      w2 = __builtin_amdgcn_mfma_f32_16x16x4f32(Ts[li][4 * lh + q], w1[q], w2, 0, 0, 0);
-    // X -= V W2 (row tiles rt = 0, 1; k = 4 lh + q)
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt) {
-      v4f d = {0.f, 0.f, 0.f, 0.f};
+      for (int q = 0; q < 8; ++q) {
+        const int rho = 16 * (q >> 2) + 4 * lh + (q & 3);
+        w1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Vs[rho][li], xq[ct][q], w1, 0, 0, 0);
+      }
+      // w1[i] = W1[4 lh + i][col]; W2 = T W1 with k = 4 lh + q
+      v4f w2 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        d = __builtin_amdgcn_mfma_f32_16x16x4f32(Vs[16 * rt + li][4 * lh + q], w2[q], d, 0, 0, 0);
+        w2 = __builtin_amdgcn_mfma_f32_16x16x4f32(Ts[li][4 * lh + q], w1[q], w2, 0, 0, 0);
+      // X -= V W2 (row tiles rt = 0, 1; k = 4 lh + q)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = s + 16 * rt + 4 * lh + i;
-        if (cok && row < n) X[(int64_t)row * ldx + col] = xq[4 * rt + i] - d[i];
+      for (int rt = 0; rt < 2; ++rt) {
+        v4f d = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          d = __builtin_amdgcn_mfma_f32_16x16x4f32(Vs[16 * rt + li][4 * lh + q], w2[q], d, 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = s + 16 * rt + 4 * lh + i;
+          if (cok && row < n) X[(int64_t)row * ldx + col] = xq[ct][4 * rt + i] - d[i];
+        }
       }
+    }
+    if (sl + 1 < sl1) {
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) xq[ct][q] = xn[ct][q];
     }
   }
 }
@@ -181,8 +202,13 @@ void bt2_apply(const float* V2, int64_t sV2, const float* T, int n, int kmax, in
     const int g_lo = std::max(0, G - 1 - st / 2);
     const int g_hi = std::min(G - 1, G - 1 - (st - kmax + 2) / 2);
     if (g_hi < g_lo) continue;
-    hipLaunchKernelGGL(bt2_apply_kernel, dim3(slabs, g_hi - g_lo + 1, batch), dim3(256), 0,
-                       stream, V2, sV2, T, n, kmax, G, st, g_lo, X, sX, ldx);
+    // ~1024 workgroups per launch: small steps keep one slab per workgroup,
+    // large ones give each workgroup several slabs (dispatching thousands of
+    // one-slab workgroups per step cost more than their work)
+    const int64_t blocks = (int64_t)(g_hi - g_lo + 1) * batch;
+    const int per = (int)std::max<int64_t>(1, std::min<int64_t>(slabs, ceil_div(blocks * slabs, 1024)));
+    hipLaunchKernelGGL(bt2_apply_kernel, dim3((unsigned)ceil_div(slabs, per), g_hi - g_lo + 1, batch),
+                       dim3(256), 0, stream, V2, sV2, T, n, kmax, G, st, g_lo, per, X, sX, ldx);
   }
 }
 

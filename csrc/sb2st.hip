@@ -44,6 +44,7 @@ constexpr int S2_LAG = 4;         // tasks between consecutive sweeps
 constexpr int S2_SPIN_LIMIT = 1 << 24;  // ~1 s: a correct run waits microseconds
 constexpr int S2_RS = 1 << 20;    // progress word: round * S2_RS + steps done
 constexpr int S2_TLD = 20;        // LDS transpose row stride (16-B aligned rows)
+constexpr int S2_GST = S2_B * S2_TLD + 16;  // LDS words per group slice
 
 __device__ __forceinline__ int ntasks(int j, int n) { return 1 + (n - 2 - j) / S2_B; }
 
@@ -88,10 +89,25 @@ __device__ __forceinline__ void load_task(const float* AB, const Task& s, int r,
 #pragma unroll
     for (int c = 0; c < S2_B; ++c) bk[c] = ld_nt(AB + (int64_t)(s.g0 + c) * S2_LD + (S2_B + r - c));
   }
+  // lower triangle only (coalesced: lanes r of column c are consecutive
+  // words); the upper triangle comes from the transpose in fill_upper
 #pragma unroll
   for (int c = 0; c < S2_B; ++c)
-    dd[c] = r >= c ? ld_nt(AB + (int64_t)(s.g0 + S2_B + c) * S2_LD + (r - c))
-                   : ld_nt(AB + (int64_t)(s.g0 + S2_B + r) * S2_LD + (c - r));
+    if (r >= c) dd[c] = ld_nt(AB + (int64_t)(s.g0 + S2_B + c) * S2_LD + (r - c));
+}
+
+// dd[c] for c > r from the other lanes' lower rows (LDS transpose): the
+// upper-triangle band words of a row are 31 floats apart, one cache line per
+// lane -- loading them directly made the bulge chase VMEM-bound
+__device__ __forceinline__ void fill_upper(float* tbg, int r, float (&dd)[S2_B]) {
+#pragma unroll
+  for (int c = 0; c < S2_B; ++c)
+    if (c <= r) tbg[r * S2_TLD + c] = dd[c];
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int c = 0; c < S2_B; ++c)
+    if (c > r) dd[c] = tbg[c * S2_TLD + r];
+  __builtin_amdgcn_wave_barrier();
 }
 
 __global__ void __launch_bounds__(S2_T) sb2st_kernel(float* __restrict__ ABall, int64_t sAB,
@@ -105,11 +121,13 @@ __global__ void __launch_bounds__(S2_T) sb2st_kernel(float* __restrict__ ABall, 
   float* V2 = V2all + (int64_t)b * sV2 * S2_B;
   float* tau2s = tau2all + (int64_t)b * sV2;
   __shared__ int prog[S2_WAVES];
-  __shared__ __attribute__((aligned(16))) float tb[S2_WAVES][4][S2_B * S2_TLD];
+  // per-group transpose slices; group stride 336 words = 16 banks apart, so
+  // the four groups of a wave never collide
+  __shared__ __attribute__((aligned(16))) float tb[S2_WAVES][4 * S2_GST];
   __shared__ __attribute__((aligned(16))) float bc[S2_WAVES][4][S2_B];
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int r = l & 15, g = l >> 4;
-  float* tbg = &tb[w][g][0];
+  float* tbg = &tb[w][g * S2_GST];
   float* bcg = &bc[w][g][0];
   if (l == 0) prog[w] = -1;
   __syncthreads();
@@ -156,6 +174,7 @@ __global__ void __launch_bounds__(S2_T) sb2st_kernel(float* __restrict__ ABall, 
     load_task(AB, task_of(rho, w, g, 0, n), r, bk, dd);
     for (int t = 0; t < steps; ++t) {
       const Task s = task_of(rho, w, g, t, n);
+      fill_upper(tbg, r, dd);
       // ---- prefetch step t+1 (written at step t-1 or earlier: complete)
       if (has_pred && t + 1 < steps) {
         const int k1 = t + 1;  // group 0's next task

@@ -19,10 +19,9 @@
 // reflector with the previous ones come out of the same reduction as the
 // trailing-column products, so the compact-WY factor T (LAPACK larft,
 // forward / columnwise) costs nothing extra.  Outputs:
-//   A lower panel  <- R (upper triangular 16 x 16) and zeros below: the band;
-//   A row p+a      <- column a of the factored panel (R^T in the band, the
-//                     reflector v_a beyond it: v_a[p+16+a] = 1 implicit), the
-//                     layout the blocked back-transform reads (offset 16);
+//   A lower panel  <- R (upper triangular 16 x 16: the band) and the
+//                     reflectors below it (column p+a holds v_a, v_a[p+16+a] = 1
+//                     implicit: the layout the blocked back-transform reads);
 //   V [m][16], U = V T [m][16], T [16][16], tau1[p+a].
 #include "common.h"
 
@@ -49,7 +48,9 @@ __device__ __forceinline__ float row_sum16(float v) {
 
 // block-wide sums of 16 per-thread values; every thread receives the totals.
 // Per value a 4-step DPP row sum; lane 0 of each 16-lane row deposits its 16
-// row sums (red: [QR_W * 4][16]), 16 threads add the 64 row sums of a value.
+// row sums (red: [QR_T / 16][16]); wave q then folds the 64 row sums of value
+// q with one LDS read per lane and a wave reduction (a serial loop over the
+// 64 partials cost ~1.5 us per column).
 __device__ __forceinline__ void block_sum16(float (&v)[TS_B], float* red, float* tot) {
   const int row = threadIdx.x >> 4, l16 = threadIdx.x & 15;
 #pragma unroll
@@ -58,17 +59,10 @@ __device__ __forceinline__ void block_sum16(float (&v)[TS_B], float* red, float*
     if (l16 == 0) red[row * TS_B + c] = s;
   }
   __syncthreads();
-  if (threadIdx.x < TS_B) {
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-#pragma unroll 4
-    for (int q = 0; q < QR_T / 16; q += 4) {
-      s0 += red[q * TS_B + threadIdx.x];
-      s1 += red[(q + 1) * TS_B + threadIdx.x];
-      s2 += red[(q + 2) * TS_B + threadIdx.x];
-      s3 += red[(q + 3) * TS_B + threadIdx.x];
-    }
-    tot[threadIdx.x] = (s0 + s1) + (s2 + s3);
-  }
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  static_assert(QR_W == TS_B && QR_T / 16 == 64, "one wave per value, 64 row sums each");
+  const float t = wave_sum_uniform(red[l * TS_B + w]);
+  if (l == 0) tot[w] = t;
   __syncthreads();
 #pragma unroll
   for (int c = 0; c < TS_B; ++c) v[c] = tot[c];
@@ -79,11 +73,9 @@ __device__ __forceinline__ float block_sum1(float v, float* red, float* tot) {
   const float s = wave_sum_uniform(v);
   if (l == 0) red[w] = s;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    float t = 0.f;
-#pragma unroll
-    for (int q = 0; q < QR_W; ++q) t += red[q];
-    tot[0] = t;
+  if (w == 0) {
+    const float t = wave_sum_uniform(l < QR_W ? red[l] : 0.f);
+    if (l == 0) tot[0] = t;
   }
   __syncthreads();
   return tot[0];
@@ -226,18 +218,14 @@ __global__ void __launch_bounds__(QR_T) sb_qr_kernel(
       vrow[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
       urow[q] = make_float4(uq[0], uq[1], uq[2], uq[3]);
     }
-    // lower panel: R on and above the diagonal, zeros below (the band)
+    // lower panel <- the factored panel: R on and above the diagonal (the
+    // band), reflector v_a below it in column p+a (v_a[p+16+a] = 1 implicit;
+    // the blocked back-transform reads it there).  Nothing here is inside the
+    // trailing matrix, so the next panel's QR may overlap this panel's update.
     float4* arow = reinterpret_cast<float4*>(Ab + (int64_t)(p + TS_B + i) * ld + p);
 #pragma unroll
-    for (int q = 0; q < TS_B / 4; ++q) {
-      float r4[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) r4[e] = i <= 4 * q + e ? PX(s, 4 * q + e) : 0.f;
-      arow[q] = make_float4(r4[0], r4[1], r4[2], r4[3]);
-    }
-    // row storage: A[p+a][p+16+i] = factored column a (R^T, then v_a)
-#pragma unroll
-    for (int a = 0; a < TS_B; ++a) Ab[(int64_t)(p + a) * ld + p + TS_B + i] = PX(s, a);
+    for (int q = 0; q < TS_B / 4; ++q)
+      arow[q] = make_float4(PX(s, 4 * q), PX(s, 4 * q + 1), PX(s, 4 * q + 2), PX(s, 4 * q + 3));
   }
   if (tid < TS_B * TS_B) {
     const int a = tid / TS_B, c = tid % TS_B;
@@ -337,10 +325,17 @@ __global__ void __launch_bounds__(1024) sb_sred_kernel(const float* __restrict__
   __shared__ float part[4][TS_B * TS_B];
   __shared__ float S[TS_B][TS_B + 1];
   __shared__ float M[TS_B][TS_B + 1];
-  float s = 0.f;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   const float* sp = Spart + (int64_t)b * nparts * TS_B * TS_B;
-  for (int i = q; i < nparts; i += 4) s += sp[(int64_t)i * TS_B * TS_B + e];
-  part[q][e] = s;
+  int i = q;
+  for (; i + 12 < nparts; i += 16) {  // four independent loads in flight
+    s0 += sp[(int64_t)i * TS_B * TS_B + e];
+    s1 += sp[(int64_t)(i + 4) * TS_B * TS_B + e];
+    s2 += sp[(int64_t)(i + 8) * TS_B * TS_B + e];
+    s3 += sp[(int64_t)(i + 12) * TS_B * TS_B + e];
+  }
+  for (; i < nparts; i += 4) s0 += sp[(int64_t)i * TS_B * TS_B + e];
+  part[q][e] = (s0 + s1) + (s2 + s3);
   __syncthreads();
   if (threadIdx.x < 256) S[e / TS_B][e % TS_B] = (part[0][e] + part[1][e]) + (part[2][e] + part[3][e]);
   __syncthreads();
@@ -409,15 +404,37 @@ __global__ void __launch_bounds__(256) sb_w_kernel(int n, int p, const float* __
 // grid (ceil(m/64) col tiles, ceil(m/64) row tiles, batch), 256 threads
 __global__ void __launch_bounds__(256) sb_upd_kernel(
     float* __restrict__ A, int64_t sA, int ld, int n, int p, const float* __restrict__ Vw,
-    int64_t sVU, const float* __restrict__ Ww) {
+    int64_t sVU, const float* __restrict__ Ww, int ctile0) {
   const int b = blockIdx.z;
   const int m = n - p - TS_B;
-  const int R0 = blockIdx.y * 64, C0 = blockIdx.x * 64;
+  const int R0 = blockIdx.y * 64, C0 = (blockIdx.x + ctile0) * 64;
   const int tid = threadIdx.x;
   __shared__ __attribute__((aligned(16))) float Vr[64][TS_B + 4], Wr[64][TS_B + 4];
   __shared__ __attribute__((aligned(16))) float Vc[64][TS_B + 4], Wc[64][TS_B + 4];
   const float* V = Vw + (int64_t)b * sVU;
   const float* W = Ww + (int64_t)b * sVU;
+  // this thread's 4 x 4 block of the tile (rows R0 + 4 ty + i, columns
+  // C0 + 4 tx .. +3: 16-B loads), in flight while V / W are staged
+  const int ty = tid >> 4, tx = tid & 15;
+  float* A22 = A + (int64_t)b * sA + (int64_t)(p + TS_B) * ld + (p + TS_B);
+  const int cb = C0 + 4 * tx;
+  const bool cfull = cb + 3 < m;
+  float4 a4[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = R0 + 4 * ty + i;
+    a4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (r < m) {
+      const float* ar = A22 + (int64_t)r * ld + cb;
+      if (cfull) {
+        a4[i] = *reinterpret_cast<const float4*>(ar);
+      } else {
+        if (cb < m) a4[i].x = ar[0];
+        if (cb + 1 < m) a4[i].y = ar[1];
+        if (cb + 2 < m) a4[i].z = ar[2];
+      }
+    }
+  }
   for (int e = tid; e < 2 * 64 * (TS_B / 4); e += 256) {
     const int side = e / (64 * (TS_B / 4)), rr = (e / (TS_B / 4)) % 64, q = e % (TS_B / 4);
     const int r = (side ? C0 : R0) + rr;
@@ -435,7 +452,6 @@ __global__ void __launch_bounds__(256) sb_upd_kernel(
     }
   }
   __syncthreads();
-  const int ty = tid >> 4, tx = tid & 15;
   float acc[4][4] = {};
 #pragma unroll
   for (int t4 = 0; t4 < TS_B; t4 += 4) {
@@ -444,8 +460,8 @@ __global__ void __launch_bounds__(256) sb_upd_kernel(
     for (int i = 0; i < 4; ++i) {
       vr[i] = *reinterpret_cast<const float4*>(&Vr[4 * ty + i][t4]);
       wr[i] = *reinterpret_cast<const float4*>(&Wr[4 * ty + i][t4]);
-      vc[i] = *reinterpret_cast<const float4*>(&Vc[tx + 16 * i][t4]);
-      wc[i] = *reinterpret_cast<const float4*>(&Wc[tx + 16 * i][t4]);
+      vc[i] = *reinterpret_cast<const float4*>(&Vc[4 * tx + i][t4]);
+      wc[i] = *reinterpret_cast<const float4*>(&Wc[4 * tx + i][t4]);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -454,15 +470,19 @@ __global__ void __launch_bounds__(256) sb_upd_kernel(
         acc[i][j] += (vr[i].x * wc[j].x + wr[i].x * vc[j].x) + (vr[i].y * wc[j].y + wr[i].y * vc[j].y) +
                      (vr[i].z * wc[j].z + wr[i].z * vc[j].z) + (vr[i].w * wc[j].w + wr[i].w * vc[j].w);
   }
-  float* A22 = A + (int64_t)b * sA + (int64_t)(p + TS_B) * ld + (p + TS_B);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int r = R0 + 4 * ty + i;
     if (r >= m) continue;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int c = C0 + tx + 16 * j;
-      if (c < m) A22[(int64_t)r * ld + c] -= acc[i][j];
+    float* ar = A22 + (int64_t)r * ld + cb;
+    const float4 o = make_float4(a4[i].x - acc[i][0], a4[i].y - acc[i][1], a4[i].z - acc[i][2],
+                                 a4[i].w - acc[i][3]);
+    if (cfull) {
+      *reinterpret_cast<float4*>(ar) = o;
+    } else {
+      if (cb < m) ar[0] = o.x;
+      if (cb + 1 < m) ar[1] = o.y;
+      if (cb + 2 < m) ar[2] = o.z;
     }
   }
 }
@@ -506,9 +526,13 @@ int sb_update_splits(int m, int batch) {
   return ks;
 }
 
-void sb_update(float* A, int64_t sA, int ld, int n, int p, int batch, const float* Vw,
-               const float* Uw, int64_t sVU, const float* Tw, float* Ypart, float* Spart,
-               float* Ms, float* Ww, hipStream_t stream) {
+// front part of panel p's update on `stream`: Y / S partials, Ms, W and the
+// first 64 columns of the trailing matrix (they hold the next panel, so the
+// next panel QR can start); sb_update_back updates the other columns (on a
+// second stream, overlapping that QR)
+void sb_update_front(float* A, int64_t sA, int ld, int n, int p, int batch, const float* Vw,
+                     const float* Uw, int64_t sVU, const float* Tw, float* Ypart, float* Spart,
+                     float* Ms, float* Ww, hipStream_t stream) {
   const int m = n - p - TS_B;
   if (m <= 0 || batch <= 0) return;
   const int nblk = (int)ceil_div(m, 64);
@@ -520,8 +544,20 @@ void sb_update(float* A, int64_t sA, int ld, int n, int p, int batch, const floa
   hipLaunchKernelGGL(sb_sred_kernel, dim3(batch), dim3(1024), 0, stream, Spart, nparts, Tw, Ms);
   hipLaunchKernelGGL(sb_w_kernel, dim3((unsigned)ceil_div(m, 256), batch), dim3(256), 0, stream,
                      n, p, Vw, sVU, Ypart, ks, Ms, Ww);
-  hipLaunchKernelGGL(sb_upd_kernel, dim3(nblk, nblk, batch), dim3(256), 0, stream, A, sA, ld, n,
-                     p, Vw, sVU, Ww);
+  hipLaunchKernelGGL(sb_upd_kernel, dim3(1, nblk, batch), dim3(256), 0, stream, A, sA, ld, n, p,
+                     Vw, sVU, Ww, 0);
+}
+
+// true when there are columns left for sb_update_back
+bool sb_update_back(float* A, int64_t sA, int ld, int n, int p, int batch, const float* Vw,
+                    int64_t sVU, const float* Ww, hipStream_t stream) {
+  const int m = n - p - TS_B;
+  if (m <= 0 || batch <= 0) return false;
+  const int nblk = (int)ceil_div(m, 64);
+  if (nblk < 2) return false;
+  hipLaunchKernelGGL(sb_upd_kernel, dim3(nblk - 1, nblk, batch), dim3(256), 0, stream, A, sA, ld,
+                     n, p, Vw, sVU, Ww, 1);
+  return true;
 }
 
 }  // namespace kfac

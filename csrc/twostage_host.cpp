@@ -27,9 +27,11 @@ int twostage_band();
 int twostage_max_n();
 void sb_panel_qr(float* A, int64_t sA, int ld, int n, int p, int batch, float* Vw, float* Uw,
                  int64_t sVU, float* tau1, int64_t sTau, float* Tw, hipStream_t stream);
-void sb_update(float* A, int64_t sA, int ld, int n, int p, int batch, const float* Vw,
-               const float* Uw, int64_t sVU, const float* Tw, float* Ypart, float* Spart,
-               float* Ms, float* Ww, hipStream_t stream);
+void sb_update_front(float* A, int64_t sA, int ld, int n, int p, int batch, const float* Vw,
+                     const float* Uw, int64_t sVU, const float* Tw, float* Ypart, float* Spart,
+                     float* Ms, float* Ww, hipStream_t stream);
+bool sb_update_back(float* A, int64_t sA, int ld, int n, int p, int batch, const float* Vw,
+                    int64_t sVU, const float* Ww, hipStream_t stream);
 void sb_extract(const float* A, int64_t sA, int ld, int n, int batch, float* AB, int64_t sAB,
                 int ncols, hipStream_t stream);
 int sb2st_kmax(int n);
@@ -55,8 +57,8 @@ namespace {
 
 hipStream_t cur() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
 
-// stage-1 reflector k (k = 0 .. nref-1) lives in ROW k of A: v[k+16] = 1
-// implicit, v[k+17 ..] stored; X <- Q1 X with Q1 = H_0 H_1 ... H_{nref-1},
+// stage-1 reflector k (k = 0 .. nref-1) lives in COLUMN k of A below the
+// band: v[k+16] = 1 implicit, v[k+17 ..] stored; X <- Q1 X with Q1 = H_0 H_1 ... H_{nref-1},
 // nb reflectors per UT block (T^-1 = striu(V^T V) + diag(1/tau)), last block
 // first.
 void apply_q1(const at::Tensor& A, const at::Tensor& tau1, int64_t n, int64_t nref,
@@ -69,7 +71,8 @@ void apply_q1(const at::Tensor& A, const at::Tensor& tau1, int64_t n, int64_t nr
     const int64_t bs = p1 - p0;
     const int64_t rows = n - p0 - off;
     if (rows <= 0) continue;
-    auto W = A.narrow(1, p0, bs).narrow(2, p0 + off, rows);
+    // reflector p0+kk in column p0+kk below the band: vt[kk][j] = A[p0+off+j][p0+kk]
+    auto W = A.narrow(2, p0, bs).narrow(1, p0 + off, rows).transpose(1, 2);
     auto vt = at::triu(W, 1);
     auto t = tau1.narrow(1, p0, bs);
     auto live = t.ne(0).to(at::kFloat);
@@ -140,10 +143,13 @@ std::vector<at::Tensor> eigh_twostage(const at::Tensor& A_in, bool timed) {
   const int64_t ld = (n + 3) / 4 * 4;
   auto A = at::zeros({b, n, ld}, fopt);
   A.narrow(2, 0, n).copy_(A_in);
-  auto Vw = at::empty({b, n, B}, fopt);
-  auto Uw = at::empty({b, n, B}, fopt);
+  // double-buffered panel operands (panel parity): the next panel's QR writes
+  // one set while this panel's back update (side stream) reads the other
+  auto Vw = at::empty({2, b, n, B}, fopt);
+  auto Uw = at::empty({2, b, n, B}, fopt);
+  auto Ww = at::empty({2, b, n, B}, fopt);
+  auto Tw = at::empty({2, b, B, B}, fopt);
   auto tau1 = at::zeros({b, n}, fopt);
-  auto Tw = at::empty({b, B, B}, fopt);
   int64_t nref = 0;
   rocblas_handle hb = kfac_rocblas_handle(s);
   TS_ROCBLAS(rocblas_set_pointer_mode(hb, rocblas_pointer_mode_host));
@@ -151,19 +157,35 @@ std::vector<at::Tensor> eigh_twostage(const at::Tensor& A_in, bool timed) {
   auto Ypart = at::empty({8, b, n, B}, fopt);
   auto Spart = at::empty({b, nblk * 8, B * B}, fopt);
   auto Ms = at::empty({b, B, B}, fopt);
-  auto Ww = at::empty({b, n, B}, fopt);
-  // ---- stage 1
+  // ---- stage 1: panel p's QR and the front of its update on s; the rest of
+  // its trailing update on the side stream, overlapping panel p+1's QR
+  hipStream_t side = c10::hip::getStreamFromPool(false, A_in.device().index()).stream();
+  hipEvent_t ev_front, ev_back;
+  C10_HIP_CHECK(hipEventCreateWithFlags(&ev_front, hipEventDisableTiming));
+  C10_HIP_CHECK(hipEventCreateWithFlags(&ev_back, hipEventDisableTiming));
+  bool back_pending = false;
   for (int64_t p = 0; n - p - B >= 2; p += B) {
-    const int64_t m = n - p - B;
-    kfac::sb_panel_qr(A.data_ptr<float>(), n * ld, (int)ld, (int)n, (int)p, (int)b,
-                      Vw.data_ptr<float>(), Uw.data_ptr<float>(), n * B, tau1.data_ptr<float>(),
-                      n, Tw.data_ptr<float>(), s);
+    const int par = (int)((p / B) & 1);
+    float* vw = Vw[par].data_ptr<float>();
+    float* uw = Uw[par].data_ptr<float>();
+    float* ww = Ww[par].data_ptr<float>();
+    float* tw = Tw[par].data_ptr<float>();
+    kfac::sb_panel_qr(A.data_ptr<float>(), n * ld, (int)ld, (int)n, (int)p, (int)b, vw, uw,
+                      n * B, tau1.data_ptr<float>(), n, tw, s);
     nref = p + B;
-    kfac::sb_update(A.data_ptr<float>(), n * ld, (int)ld, (int)n, (int)p, (int)b,
-                    Vw.data_ptr<float>(), Uw.data_ptr<float>(), n * B, Tw.data_ptr<float>(),
-                    Ypart.data_ptr<float>(), Spart.data_ptr<float>(), Ms.data_ptr<float>(),
-                    Ww.data_ptr<float>(), s);
+    if (back_pending) C10_HIP_CHECK(hipStreamWaitEvent(s, ev_back, 0));
+    kfac::sb_update_front(A.data_ptr<float>(), n * ld, (int)ld, (int)n, (int)p, (int)b, vw, uw,
+                          n * B, tw, Ypart.data_ptr<float>(), Spart.data_ptr<float>(),
+                          Ms.data_ptr<float>(), ww, s);
+    C10_HIP_CHECK(hipEventRecord(ev_front, s));
+    C10_HIP_CHECK(hipStreamWaitEvent(side, ev_front, 0));
+    back_pending = kfac::sb_update_back(A.data_ptr<float>(), n * ld, (int)ld, (int)n, (int)p,
+                                        (int)b, vw, n * B, ww, side);
+    if (back_pending) C10_HIP_CHECK(hipEventRecord(ev_back, side));
   }
+  if (back_pending) C10_HIP_CHECK(hipStreamWaitEvent(s, ev_back, 0));
+  C10_HIP_CHECK(hipEventDestroy(ev_front));
+  C10_HIP_CHECK(hipEventDestroy(ev_back));
   mark();
   // ---- stage 2
   const int64_t ncols = n + 4 * B;

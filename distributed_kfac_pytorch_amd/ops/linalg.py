@@ -181,22 +181,35 @@ def _accept_warm(stack: torch.Tensor, warm: torch.Tensor
     return idx, rs, q
 
 
+def twostage_min_n() -> int:
+    """Smallest factor the auto tier sends to the two-stage solver
+    (``KFAC_TWOSTAGE_MIN_N``, default 4000): its bulge chase runs one
+    workgroup per factor, so it wins where one factor alone is the critical
+    path of the refresh (ResNet-50's 4608 x 4608 A factors) and the batched
+    one-stage chains win on the many mid-size factors they advance together."""
+    return int(os.environ.get('KFAC_TWOSTAGE_MIN_N', '4000'))
+
+
 def _use_twostage(n: int) -> bool:
     """Native two-stage solver (ops/twostage.py) for this factor size."""
     mode = os.environ.get('KFAC_EIGH', 'auto')
     if mode not in ('auto', 'twostage'):
         return False
-    if mode == 'auto' and large_algo() != 'twostage':
+    if not JACOBI_MAX_N < n <= twostage.max_n():
         return False
-    return JACOBI_MAX_N < n <= twostage.max_n()
+    if mode == 'twostage' or large_algo() == 'twostage':
+        return True
+    return large_algo() == 'sytrd' and n >= twostage_min_n()
 
 
 def large_algo() -> str:
     """Solver for factors above the LDS Jacobi tier that the warm-start
-    acceptance test did not settle: ``KFAC_EIGH_LARGE`` = twostage (default:
-    dense -> band -> tridiagonal with level-3 stage 1, bulge chasing, native
-    divide and conquer and blocked back-transforms, ops/twostage.py) |
-    sytrd (one-stage native chains) | syevd | block.
+    acceptance test did not settle: ``KFAC_EIGH_LARGE`` = sytrd (default:
+    one-stage native chains, with factors of ``KFAC_TWOSTAGE_MIN_N`` and more
+    on the two-stage solver -- dense -> band -> tridiagonal with a level-3
+    stage 1, bulge chasing, native divide and conquer and blocked
+    back-transforms, ops/twostage.py) | twostage (every factor) | syevd |
+    block.
 
     Default sytrd: factors with n >= ``KFAC_SYTRD_MIN_N`` (2000) go through
     the native tridiagonalisation chains with the blocked back-transform,
@@ -211,7 +224,7 @@ def large_algo() -> str:
     basis of a rank-deficient early factor is a poor start) and the mix
     takes 1002 ms against 395 ms for syevd at equal accuracy
     (profiles/refresh_probe_r2_resnet50_step100.jsonl)."""
-    return os.environ.get('KFAC_EIGH_LARGE', 'twostage')
+    return os.environ.get('KFAC_EIGH_LARGE', 'sytrd')
 
 
 def _large_bucket(stack: torch.Tensor, warm: torch.Tensor | None
@@ -502,8 +515,9 @@ def _launch_jobs(
     """
     main = torch.cuda.current_stream(dev)
     out: dict[int, tuple[torch.Tensor, torch.Tensor]] = {}
-    # chain membership is decided on the full buckets (before acceptance)
-    chain_keys = {k for k, v in gpu if _use_sytrd(k[0], len(v))}
+    # chain membership is decided on the full buckets (before acceptance);
+    # two-stage buckets run as ordinary lane jobs beside the chains
+    chain_keys = {k for k, v in gpu if _use_sytrd(k[0], len(v)) and not _use_twostage(k[0])}
     if warms and chain_keys:
         gpu = _settle_warm(gpu, stacks, warms, out)
     ready = torch.cuda.Event()
@@ -515,6 +529,11 @@ def _launch_jobs(
         out.update(_launch_sytrd(big, rest, stacks, main, ready, streams))
         return out
     jobs = sorted(_jobs(gpu), key=lambda j: -_bucket_cost(j[0][0], j[3] - j[2]))
+    # one lane per hardware queue: streams beyond GPU_MAX_HW_QUEUES share a
+    # queue, and a lane queued behind another lane's long kernel (a two-stage
+    # bulge chase runs for tens of ms on one CU) waits for all of it
+    hwq = int(os.environ.get('GPU_MAX_HW_QUEUES', '4'))
+    streams = streams[:max(1, min(len(streams), hwq))]
     lanes: list[list] = [[] for _ in streams]
     loads = [0.0] * len(streams)
     for job in jobs:
