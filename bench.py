@@ -7,7 +7,9 @@ K-FAC factor update every 10 steps, second-order update every 100 steps,
 damping 0.001, factor decay 0.95, KL clip 0.001, hybrid-opt (gwf 0.5),
 25 MB factor all-reduce buckets, eigen method with eigenvalue outer product.
 Data is synthetic (random images / labels of that shape, generated on the
-device), weights random-init.  bf16 autocast, channels_last.
+device), weights random-init.  fp32 by default (the reference's ImageNet
+default); ``--dtype bf16`` (autocast) is also timed as the ``bf16`` field.
+channels_last.
 
 Single GPU:     python bench.py
 N GPUs:         python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
@@ -60,11 +62,13 @@ from distributed_kfac_pytorch_amd.ops.cast import enable_fused_weight_cast  # no
 # under the earlier harness settings).  For N GPUs the comparison point is
 # the reference's linear-scaling upper bound N * 753.96.
 # bf16 (autocast) row; the fp32 row (the reference's ImageNet default, no
-# --fp16) is measured the same way with --dtype fp32.  None = not measured.
-REFERENCE_IMG_S_PER_GPU = {'bf16': 753.96, 'fp32': None}
-# the reference's K-FAC-only cost on the same box and harness: 42.44 ms/step
-# with K-FAC minus 10.93 ms/step for its own SGD step (bf16)
-REFERENCE_KFAC_OVERHEAD_MS = {'bf16': 31.51, 'fp32': None}
+# --fp16, examples/torch_imagenet_resnet.py:73-76) measured the same way with
+# --dtype fp32 in round 3: 692.57 img/s, 46.204 ms/step, SGD 17.711 ms/step
+# (profiles/bench_reference_impl_mi355x_1gpu_fp32_r3.json).
+REFERENCE_IMG_S_PER_GPU = {'bf16': 753.96, 'fp32': 692.57}
+# the reference's K-FAC-only cost on the same box and harness: ms/step with
+# K-FAC minus its own SGD step (bf16: 42.44 - 10.93; fp32: 46.204 - 17.711)
+REFERENCE_KFAC_OVERHEAD_MS = {'bf16': 31.51, 'fp32': 28.49}
 
 
 

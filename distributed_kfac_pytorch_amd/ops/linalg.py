@@ -183,11 +183,14 @@ def _accept_warm(stack: torch.Tensor, warm: torch.Tensor
 
 def twostage_min_n() -> int:
     """Smallest factor the auto tier sends to the two-stage solver
-    (``KFAC_TWOSTAGE_MIN_N``, default 4000): its bulge chase runs one
-    workgroup per factor, so it wins where one factor alone is the critical
-    path of the refresh (ResNet-50's 4608 x 4608 A factors) and the batched
-    one-stage chains win on the many mid-size factors they advance together."""
-    return int(os.environ.get('KFAC_TWOSTAGE_MIN_N', '4000'))
+    (``KFAC_TWOSTAGE_MIN_N``; default: none).  Measured on the ResNet-50
+    step-100 refresh (gpurun_out r3z, one box): chains only 246 ms, two-stage
+    for the 3 x 4608 bucket + chains below 307 ms, two-stage for everything
+    409 ms -- at these sizes f32 MFMA runs at the f32 VALU rate, so the
+    two-stage's 2.5x back-transform flops and its one-workgroup bulge chase
+    (69 ms at n = 4608) do not pay for the level-3 stage 1 yet
+    (profiles/twostage_r3.md)."""
+    return int(os.environ.get('KFAC_TWOSTAGE_MIN_N', str(1 << 30)))
 
 
 def _use_twostage(n: int) -> bool:
