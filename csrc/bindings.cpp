@@ -32,6 +32,8 @@ void syrk(int in_dtype, const void* x, int64_t N, int64_t K, int64_t ldx,
           bool bias, float* C, int64_t D, int64_t ldc, float alpha,
           float beta, int splits, hipStream_t s, const ConvGeom* geom,
           float* ws, const float* ascale, bool fp32_exact);
+void syrk_split_planes(const float* x, int64_t B, int H, int W, int C, int64_t sB, int64_t sH,
+                       int64_t sW, uint16_t* planes, hipStream_t s);
 // im2col.hip
 void im2col_nhwc(int dtype, const void* x, int64_t B, int64_t H, int64_t W,
                  int64_t C, int64_t sB, int64_t sH, int64_t sW, int kh, int kw,
@@ -90,14 +92,13 @@ void cast_multi(const CastDesc* table, int n, int64_t total_blocks, bool to_bf16
 // bnact.hip
 void bn_partition(int64_t M, int C, int64_t* rows_per_block, int* nblk);
 int bn_max_c();
-void bn_forward(const uint16_t* x, const uint16_t* res, const float* weight,
+void bn_forward(int dtype, const void* x, const void* res, const float* weight,
                 const float* bias, float* running_mean, float* running_var,
                 int64_t* num_batches, float momentum, float eps, int relu, int64_t M,
-                int C, float* part, float* stats, uint16_t* y, hipStream_t s);
-void bn_backward(const uint16_t* x, const uint16_t* dy, const uint16_t* y,
-                 const float* weight, const float* stats, int relu, int64_t M, int C,
-                 float* part, float* coef, float* dweight, float* dbias, uint16_t* dx,
-                 uint16_t* dres, hipStream_t s);
+                int C, float* part, float* stats, void* y, hipStream_t s);
+void bn_backward(int dtype, const void* x, const void* dy, const void* y, const float* weight,
+                 const float* stats, int relu, int64_t M, int C, float* part, float* coef,
+                 float* dweight, float* dbias, void* dx, void* dres, hipStream_t s);
 }  // namespace kfac
 
 // solver.cpp
@@ -271,6 +272,23 @@ void syrk_conv(const at::Tensor& x, at::Tensor& C, int64_t kh, int64_t kw,
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   int sp = splits > 0 ? (int)splits : (int)kfac::syrk_workspace_splits(N, D);
   at::Tensor ws = syrk_ws(C, D, sp);
+  // fp32 input on the bf16x3 path: split it once into contiguous bf16 hi / lo
+  // planes (stream-ordered temporary) so the SYRK loop converts nothing
+  const int64_t elems = B * H * W * Cin;
+  if (x.scalar_type() == at::kFloat && !fp32_exact && Cin % 8 == 0 && N < (1LL << 24) &&
+      elems < (1LL << 29)) {
+    at::Tensor planes = at::empty({2 * elems}, x.options().dtype(at::kBFloat16));
+    kfac::syrk_split_planes(x.data_ptr<float>(), B, (int)H, (int)W, (int)Cin, x.stride(0),
+                            x.stride(2), x.stride(3),
+                            reinterpret_cast<uint16_t*>(planes.data_ptr()), cur_stream());
+    kfac::ConvGeom gp{H * W * Cin, W * Cin, Cin, (int32_t)H, (int32_t)W, (int32_t)Cin,
+                      (int32_t)kw, (int32_t)sh, (int32_t)sw, (int32_t)ph, (int32_t)pw,
+                      (int32_t)OH, (int32_t)OW, elems, 0};
+    kfac::syrk(kfac::kF32, planes.data_ptr(), N, K, /*ldx=*/K, bias, C.data_ptr<float>(), D,
+               ldc, (float)alpha, (float)beta, sp, cur_stream(), &gp,
+               ws.defined() ? ws.data_ptr<float>() : nullptr, syrk_ascale(ascale, C), false);
+    return;
+  }
   kfac::syrk(dtype_tag(x), x.data_ptr(), N, K, /*ldx=*/K, bias, C.data_ptr<float>(), D,
              ldc, (float)alpha, (float)beta, sp, cur_stream(), &g,
              ws.defined() ? ws.data_ptr<float>() : nullptr, syrk_ascale(ascale, C),
@@ -970,7 +988,8 @@ void gemm3_grouped(const at::Tensor& table, int64_t nlayers, int64_t total_tiles
 // ------------------------------------------------------------ fused BN
 namespace {
 bool bn_ok(const at::Tensor& t) {
-  return t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.dim() == 4 &&
+  return t.is_cuda() && (t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kFloat) &&
+         t.dim() == 4 &&
          t.is_contiguous(at::MemoryFormat::ChannelsLast) &&
          (reinterpret_cast<uintptr_t>(t.data_ptr()) % 16) == 0;
 }
@@ -998,7 +1017,9 @@ std::vector<at::Tensor> bn_act_forward(const at::Tensor& x,
   const int64_t C = x.size(1), M = x.numel() / C;
   const bool has_res = residual.has_value() && residual->defined();
   if (has_res) {
-    TORCH_CHECK(bn_ok(*residual) && residual->sizes() == x.sizes(), "residual layout");
+    TORCH_CHECK(bn_ok(*residual) && residual->sizes() == x.sizes() &&
+                    residual->scalar_type() == x.scalar_type(),
+                "residual layout");
   }
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   int64_t rpb;
@@ -1017,11 +1038,10 @@ std::vector<at::Tensor> bn_act_forward(const at::Tensor& x,
                   ? running_mean->data_ptr<float>() : nullptr;
   float* rv = running_var.has_value() && running_var->defined()
                   ? running_var->data_ptr<float>() : nullptr;
-  kfac::bn_forward(reinterpret_cast<const uint16_t*>(x.data_ptr()),
-                   has_res ? reinterpret_cast<const uint16_t*>(residual->data_ptr()) : nullptr,
+  kfac::bn_forward(dtype_tag(x), x.data_ptr(), has_res ? residual->data_ptr() : nullptr,
                    opt_f(weight), opt_f(bias), rm, rv, nb, (float)momentum, (float)eps,
                    relu ? 1 : 0, M, (int)C, part.data_ptr<float>(), stats.data_ptr<float>(),
-                   reinterpret_cast<uint16_t*>(y.data_ptr()), cur_stream());
+                   y.data_ptr(), cur_stream());
   return {y, stats};
 }
 
@@ -1034,8 +1054,9 @@ std::vector<at::Tensor> bn_act_backward(const at::Tensor& x, const at::Tensor& d
   TORCH_CHECK(bn_act_supported(x) && stats.is_contiguous());
   const int64_t C = x.size(1), M = x.numel() / C;
   at::Tensor g = dy;
-  if (!bn_ok(g)) g = dy.to(at::kBFloat16).contiguous(at::MemoryFormat::ChannelsLast);
-  TORCH_CHECK(bn_ok(y));
+  if (!bn_ok(g) || g.scalar_type() != x.scalar_type())
+    g = dy.to(x.scalar_type()).contiguous(at::MemoryFormat::ChannelsLast);
+  TORCH_CHECK(bn_ok(y) && y.scalar_type() == x.scalar_type());
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   int64_t rpb;
   int nblk;
@@ -1047,13 +1068,10 @@ std::vector<at::Tensor> bn_act_backward(const at::Tensor& x, const at::Tensor& d
   auto dx = at::empty_like(x, at::MemoryFormat::ChannelsLast);
   at::Tensor dres;
   if (has_res) dres = at::empty_like(x, at::MemoryFormat::ChannelsLast);
-  kfac::bn_backward(reinterpret_cast<const uint16_t*>(x.data_ptr()),
-                    reinterpret_cast<const uint16_t*>(g.data_ptr()),
-                    reinterpret_cast<const uint16_t*>(y.data_ptr()), opt_f(weight),
+  kfac::bn_backward(dtype_tag(x), x.data_ptr(), g.data_ptr(), y.data_ptr(), opt_f(weight),
                     stats.data_ptr<float>(), relu ? 1 : 0, M, (int)C,
                     part.data_ptr<float>(), coef.data_ptr<float>(), dw.data_ptr<float>(),
-                    db.data_ptr<float>(), reinterpret_cast<uint16_t*>(dx.data_ptr()),
-                    has_res ? reinterpret_cast<uint16_t*>(dres.data_ptr()) : nullptr,
+                    db.data_ptr<float>(), dx.data_ptr(), has_res ? dres.data_ptr() : nullptr,
                     cur_stream());
   return {dx, dw, db, dres};
 }

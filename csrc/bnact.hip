@@ -1,5 +1,5 @@
 // Fused training-mode BatchNorm2d (+ residual add) (+ ReLU) for NHWC bf16
-// activations, forward and backward, for the ResNet models.
+// or fp32 activations, forward and backward, for the ResNet models.
 //
 // Why: in a ResNet-50 step at batch 32 on MI355X the BatchNorm family is
 // the largest non-conv cost: MIOpen's 3 forward + 3 backward BN kernels,
@@ -11,8 +11,8 @@
 //             shift) -> apply (x*scale + shift [+ residual], ReLU, bf16)
 //   backward: partials of dz = dy*(y > 0) and dz*(x - mean) -> finalize
 //             (dgamma, dbeta, dx coefficients) -> apply (dx [, d residual])
-// All passes move 16 B (8 channels of bf16) per thread per access, rows are
-// [N*H*W, C] with C % 8 == 0.  Statistics accumulate in fp32 per workgroup
+// All passes move 8 channels per thread per access (one 16-B load of bf16,
+// two of fp32), rows are [N*H*W, C] with C % 8 == 0.  Statistics accumulate in fp32 per workgroup
 // and in fp64 across workgroups (E[x^2] - E[x]^2 in fp64 does not cancel).
 // Semantics follow torch.nn.functional.batch_norm (training=True): biased
 // variance to normalise, unbiased variance into running_var, momentum
@@ -57,13 +57,26 @@ __device__ __forceinline__ void store8(uint16_t* p, const float* v) {
   *reinterpret_cast<uint4*>(p) = u;
 }
 
+// fp32 activations: 8 channels = two 16-B accesses
+__device__ __forceinline__ void load8(const float* p, float* v) {
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  const float4 b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+__device__ __forceinline__ void store8(float* p, const float* v) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+
 // Per-block channel partial sums.  mode 0 (forward): s0 = sum x,
 // s1 = sum x^2.  mode 1 (backward): dz = dy * (y > 0 | !relu),
 // s0 = sum dz, s1 = sum dz * (x - mean).
-template <int MODE>
+template <typename E, int MODE>
 __global__ void __launch_bounds__(BN_T) bn_partial_kernel(
-    const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
-    const uint16_t* __restrict__ y, const float* __restrict__ mean, int relu,
+    const E* __restrict__ x, const E* __restrict__ dy,
+    const E* __restrict__ y, const float* __restrict__ mean, int relu,
     int64_t M, int C, int64_t rows_per_block, float* __restrict__ part) {
   extern __shared__ float sh[];  // [2][RPI][C]
   const int tpr = C / 8;
@@ -212,10 +225,11 @@ __global__ void __launch_bounds__(BN_FIN_T) bn_fwd_finalize_kernel(
 // Apply passes: each thread owns one 8-channel group for the whole launch
 // (per-channel constants in registers, no index division) and streams 4
 // rows per iteration with independent 16-B loads.
+template <typename E>
 __global__ void __launch_bounds__(BN_T) bn_fwd_apply_kernel(
-    const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
+    const E* __restrict__ x, const E* __restrict__ res,
     const float* __restrict__ stats, int relu, int64_t M, int C,
-    uint16_t* __restrict__ y) {
+    E* __restrict__ y) {
   const int tpr = C / 8;
   const int rpi = BN_T / tpr;
   const int cg = threadIdx.x % tpr, rs = threadIdx.x / tpr;
@@ -272,11 +286,12 @@ __global__ void __launch_bounds__(BN_FIN_T) bn_bwd_finalize_kernel(
   coef[2 * C + c] = (float)(-k1 * invstd * invstd * sdzx / (double)M);
 }
 
+template <typename E>
 __global__ void __launch_bounds__(BN_T) bn_bwd_apply_kernel(
-    const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
-    const uint16_t* __restrict__ y, const float* __restrict__ stats,
+    const E* __restrict__ x, const E* __restrict__ dy,
+    const E* __restrict__ y, const float* __restrict__ stats,
     const float* __restrict__ coef, int relu, int64_t M, int C,
-    uint16_t* __restrict__ dx, uint16_t* __restrict__ dres) {
+    E* __restrict__ dx, E* __restrict__ dres) {
   const int tpr = C / 8;
   const int rpi = BN_T / tpr;
   const int cg = threadIdx.x % tpr, rs = threadIdx.x / tpr;
@@ -332,10 +347,10 @@ constexpr int SB_PMAX = 64;  // row chunks of the partial pass
 
 __device__ __host__ __forceinline__ int sliced_cw(int C) { return C < SB_CW ? C : SB_CW; }
 
-template <int MODE>
+template <typename E, int MODE>
 __global__ void __launch_bounds__(BN_T) bn_partial_sliced_kernel(
-    const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
-    const uint16_t* __restrict__ y, const float* __restrict__ mean, int relu,
+    const E* __restrict__ x, const E* __restrict__ dy,
+    const E* __restrict__ y, const float* __restrict__ mean, int relu,
     int64_t M, int C, int64_t rows_per_chunk, float* __restrict__ part) {
   __shared__ float sh[2][BN_T * 8];  // [RT][cw] per statistic
   const int cw = sliced_cw(C);
@@ -427,13 +442,14 @@ __device__ __forceinline__ void sliced_reduce(const float* __restrict__ part, in
 }
 
 // forward: finalise this slice's channels, then x*scale + shift (+ res) (ReLU)
+template <typename E>
 __global__ void __launch_bounds__(BN_T) bn_fwd_apply_sliced_kernel(
-    const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
+    const E* __restrict__ x, const E* __restrict__ res,
     const float* __restrict__ part, int P, int64_t M, int C, int64_t rows_per_chunk,
     const float* __restrict__ weight, const float* __restrict__ bias,
     float* __restrict__ running_mean, float* __restrict__ running_var,
     int64_t* __restrict__ num_batches, float momentum, float eps, int relu,
-    float* __restrict__ stats, uint16_t* __restrict__ y) {
+    float* __restrict__ stats, E* __restrict__ y) {
   __shared__ double tot[2][SB_CW];
   __shared__ float ssc[SB_CW], ssf[SB_CW];
   const int cw = sliced_cw(C);
@@ -503,12 +519,13 @@ __global__ void __launch_bounds__(BN_T) bn_fwd_apply_sliced_kernel(
 
 // backward: finalise dweight / dbias and the dx coefficients of this slice,
 // then dx = k1*dz + k2 + k3*(x - mean) (and d residual = dz)
+template <typename E>
 __global__ void __launch_bounds__(BN_T) bn_bwd_apply_sliced_kernel(
-    const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
-    const uint16_t* __restrict__ y, const float* __restrict__ part, int P, int64_t M, int C,
+    const E* __restrict__ x, const E* __restrict__ dy,
+    const E* __restrict__ y, const float* __restrict__ part, int P, int64_t M, int C,
     int64_t rows_per_chunk, const float* __restrict__ weight, const float* __restrict__ stats,
     float* __restrict__ dweight, float* __restrict__ dbias, int relu,
-    uint16_t* __restrict__ dx, uint16_t* __restrict__ dres) {
+    E* __restrict__ dx, E* __restrict__ dres) {
   __shared__ double tot[2][SB_CW];
   __shared__ float sk1[SB_CW], sk2[SB_CW], sk3[SB_CW], smu[SB_CW];
   const int cw = sliced_cw(C);
@@ -635,18 +652,21 @@ void bn_partition(int64_t M, int C, int64_t* rows_per_block, int* nblk) {
 
 int bn_max_c() { return 8 * BN_T; }
 
-void bn_forward(const uint16_t* x, const uint16_t* res, const float* weight,
-                const float* bias, float* running_mean, float* running_var,
-                int64_t* num_batches, float momentum, float eps, int relu, int64_t M,
-                int C, float* part, float* stats, uint16_t* y, hipStream_t s) {
+namespace {
+
+template <typename E>
+void bn_forward_t(const E* x, const E* res, const float* weight, const float* bias,
+                  float* running_mean, float* running_var, int64_t* num_batches, float momentum,
+                  float eps, int relu, int64_t M, int C, float* part, float* stats, E* y,
+                  hipStream_t s) {
   {
     int P, Q;
     int64_t rp, rq;
     if (sliced_plan(M, C, &P, &Q, &rp, &rq)) {
       const unsigned nsl = (unsigned)(C / sliced_cw(C));
-      hipLaunchKernelGGL(bn_partial_sliced_kernel<0>, dim3(nsl, (unsigned)P), dim3(BN_T), 0, s,
-                         x, nullptr, nullptr, nullptr, 0, M, C, rp, part);
-      hipLaunchKernelGGL(bn_fwd_apply_sliced_kernel, dim3(nsl, (unsigned)Q), dim3(BN_T), 0, s,
+      hipLaunchKernelGGL((bn_partial_sliced_kernel<E, 0>), dim3(nsl, (unsigned)P), dim3(BN_T), 0,
+                         s, x, nullptr, nullptr, nullptr, 0, M, C, rp, part);
+      hipLaunchKernelGGL(bn_fwd_apply_sliced_kernel<E>, dim3(nsl, (unsigned)Q), dim3(BN_T), 0, s,
                          x, res, part, P, M, C, rq, weight, bias, running_mean, running_var,
                          num_batches, momentum, eps, relu, stats, y);
       return;
@@ -657,27 +677,27 @@ void bn_forward(const uint16_t* x, const uint16_t* res, const float* weight,
   bn_partition(M, C, &rpb, &nblk);
   const int rpi = BN_T / (C / 8);
   const size_t shm = (size_t)2 * rpi * C * sizeof(float);
-  hipLaunchKernelGGL(bn_partial_kernel<0>, dim3(nblk), dim3(BN_T), shm, s, x, nullptr,
+  hipLaunchKernelGGL((bn_partial_kernel<E, 0>), dim3(nblk), dim3(BN_T), shm, s, x, nullptr,
                      nullptr, nullptr, 0, M, C, rpb, part);
   hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((unsigned)ceil_div(C, BN_FIN_CH)),
                      dim3(BN_FIN_T), 0, s, part, nblk, M, C, weight, bias, running_mean,
                      running_var, num_batches, momentum, eps, stats);
-  hipLaunchKernelGGL(bn_fwd_apply_kernel, dim3(apply_grid(M, C)), dim3(BN_T), 0, s, x,
-                     res, stats, relu, M, C, y);
+  hipLaunchKernelGGL(bn_fwd_apply_kernel<E>, dim3(apply_grid(M, C)), dim3(BN_T), 0, s, x, res,
+                     stats, relu, M, C, y);
 }
 
-void bn_backward(const uint16_t* x, const uint16_t* dy, const uint16_t* y,
-                 const float* weight, const float* stats, int relu, int64_t M, int C,
-                 float* part, float* coef, float* dweight, float* dbias, uint16_t* dx,
-                 uint16_t* dres, hipStream_t s) {
+template <typename E>
+void bn_backward_t(const E* x, const E* dy, const E* y, const float* weight, const float* stats,
+                   int relu, int64_t M, int C, float* part, float* coef, float* dweight,
+                   float* dbias, E* dx, E* dres, hipStream_t s) {
   {
     int P, Q;
     int64_t rp, rq;
     if (sliced_plan(M, C, &P, &Q, &rp, &rq)) {
       const unsigned nsl = (unsigned)(C / sliced_cw(C));
-      hipLaunchKernelGGL(bn_partial_sliced_kernel<1>, dim3(nsl, (unsigned)P), dim3(BN_T), 0, s,
-                         x, dy, y, stats, relu, M, C, rp, part);
-      hipLaunchKernelGGL(bn_bwd_apply_sliced_kernel, dim3(nsl, (unsigned)Q), dim3(BN_T), 0, s,
+      hipLaunchKernelGGL((bn_partial_sliced_kernel<E, 1>), dim3(nsl, (unsigned)P), dim3(BN_T), 0,
+                         s, x, dy, y, stats, relu, M, C, rp, part);
+      hipLaunchKernelGGL(bn_bwd_apply_sliced_kernel<E>, dim3(nsl, (unsigned)Q), dim3(BN_T), 0, s,
                          x, dy, y, part, P, M, C, rq, weight, stats, dweight, dbias, relu, dx,
                          dres);
       (void)coef;  // the sliced path keeps its coefficients in LDS
@@ -689,13 +709,39 @@ void bn_backward(const uint16_t* x, const uint16_t* dy, const uint16_t* y,
   bn_partition(M, C, &rpb, &nblk);
   const int rpi = BN_T / (C / 8);
   const size_t shm = (size_t)2 * rpi * C * sizeof(float);
-  hipLaunchKernelGGL(bn_partial_kernel<1>, dim3(nblk), dim3(BN_T), shm, s, x, dy, y,
-                     stats, relu, M, C, rpb, part);
+  hipLaunchKernelGGL((bn_partial_kernel<E, 1>), dim3(nblk), dim3(BN_T), shm, s, x, dy, y, stats,
+                     relu, M, C, rpb, part);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((unsigned)ceil_div(C, BN_FIN_CH)),
-                     dim3(BN_FIN_T), 0, s, part, nblk, M, C, weight, stats, dweight, dbias,
-                     coef);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(apply_grid(M, C)), dim3(BN_T), 0, s, x,
-                     dy, y, stats, coef, relu, M, C, dx, dres);
+                     dim3(BN_FIN_T), 0, s, part, nblk, M, C, weight, stats, dweight, dbias, coef);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel<E>, dim3(apply_grid(M, C)), dim3(BN_T), 0, s, x, dy, y,
+                     stats, coef, relu, M, C, dx, dres);
+}
+
+}  // namespace
+
+// dtype: kBF16 (NHWC bf16, the autocast path) or kF32 (NHWC fp32)
+void bn_forward(int dtype, const void* x, const void* res, const float* weight,
+                const float* bias, float* running_mean, float* running_var,
+                int64_t* num_batches, float momentum, float eps, int relu, int64_t M,
+                int C, float* part, float* stats, void* y, hipStream_t s) {
+  if (dtype == kF32)
+    bn_forward_t((const float*)x, (const float*)res, weight, bias, running_mean, running_var,
+                 num_batches, momentum, eps, relu, M, C, part, stats, (float*)y, s);
+  else
+    bn_forward_t((const uint16_t*)x, (const uint16_t*)res, weight, bias, running_mean,
+                 running_var, num_batches, momentum, eps, relu, M, C, part, stats,
+                 (uint16_t*)y, s);
+}
+
+void bn_backward(int dtype, const void* x, const void* dy, const void* y, const float* weight,
+                 const float* stats, int relu, int64_t M, int C, float* part, float* coef,
+                 float* dweight, float* dbias, void* dx, void* dres, hipStream_t s) {
+  if (dtype == kF32)
+    bn_backward_t((const float*)x, (const float*)dy, (const float*)y, weight, stats, relu, M, C,
+                  part, coef, dweight, dbias, (float*)dx, (float*)dres, s);
+  else
+    bn_backward_t((const uint16_t*)x, (const uint16_t*)dy, (const uint16_t*)y, weight, stats,
+                  relu, M, C, part, coef, dweight, dbias, (uint16_t*)dx, (uint16_t*)dres, s);
 }
 
 }  // namespace kfac

@@ -81,6 +81,8 @@ struct SplitDesc {
 struct ConvGeom {
   int64_t sB, sH, sW;  // element strides of the input (channel stride 1)
   int32_t H, W, C, kw, sh, sw, ph, pw, OH, OW;
+  int64_t plane;   // > 0: x holds two bf16 planes (hi, lo) this many elements apart
+  int64_t nbytes;  // set by syrk(): bytes the buffer loads may read
 };
 
 // sytrd.hip: one matrix of a batched mixed-size tridiagonalisation

@@ -39,6 +39,7 @@ constexpr int LDS_W32 = 132;  // fp32 LDS row (128 + 4 pad)
 
 typedef short v4i16 __attribute__((ext_vector_type(4)));
 typedef short v8i16 __attribute__((ext_vector_type(8)));
+typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
 typedef __bf16 v8bf16 __attribute__((ext_vector_type(8)));
 typedef float v16f __attribute__((ext_vector_type(16)));
 typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
@@ -340,6 +341,182 @@ struct PatchStaging<float> {
   }
 };
 
+// ---- implicit im2col, 32-bit fast path (fp32 inputs, N < 2^24 rows and an
+// input of < 2^31 elements: every ResNet-50 conv).  PMC of the generic
+// staging above (profiles/pmc/syrk_r3.md): ~23 VALU instructions per MFMA,
+// most of them the two 64-bit divisions of decode_row per row pass and the
+// 64-bit patch offsets, so the SIMDs issued VALU, not MFMA.  Here a row is
+// decoded with float-reciprocal divisions (one +-1 correction: exact for
+// n < 2^24), the tap of each column chunk is folded into one int32 offset at
+// init, and a row pass costs one base offset shared by both operands.
+__device__ __forceinline__ int fdivmod(int n, int d, float inv, int& r) {
+  int q = (int)((float)n * inv);
+  r = n - q * d;
+  if (r < 0) {
+    q -= 1;
+    r += d;
+  } else if (r >= d) {
+    q += 1;
+    r -= d;
+  }
+  return q;
+}
+
+struct Tap32 {
+  int off;   // i * sH + j * sW + c
+  int i, j;  // tap position (bounds)
+  int kind;  // 0: image chunk, 1: the bias column (1 at col == K), 2: zero pad
+  bool one;  // kind 1 and this chunk holds column K in its first element
+};
+
+__device__ __forceinline__ Tap32 tap32(int64_t col, int64_t K, const ConvGeom& g) {
+  Tap32 t;
+  if (col >= K) {
+    t.kind = col == K ? 1 : 2;
+    t.one = col == K;
+    t.off = t.i = t.j = 0;
+    return t;
+  }
+  const int tap = (int)col / g.C;
+  const int c = (int)col - tap * g.C;
+  t.i = tap / g.kw;
+  t.j = tap - t.i * g.kw;
+  t.off = t.i * (int)g.sH + t.j * (int)g.sW + c;
+  t.kind = 0;
+  t.one = false;
+  return t;
+}
+
+template <typename TIn>
+struct PatchStaging32;
+
+template <>
+struct PatchStaging32<float> {
+  float4 r[2][4];
+  Tap32 ti, tj;
+  float inv_ohw, inv_ow;
+
+  __device__ __forceinline__ void init(int64_t c0i, int64_t c0j, int64_t K, const ConvGeom& g) {
+    const int chunk = threadIdx.x & 31;
+    ti = tap32(c0i + chunk * 4, K, g);
+    tj = tap32(c0j + chunk * 4, K, g);
+    inv_ohw = 1.f / (float)(g.OH * g.OW);
+    inv_ow = 1.f / (float)g.OW;
+  }
+
+  __device__ __forceinline__ static float4 chunk_of(const float* X, bool live, int base, int ih0,
+                                                    int iw0, const Tap32& t, const ConvGeom& g,
+                                                    bool bias) {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (!live) return v;
+    if (t.kind == 0) {
+      const int ih = ih0 + t.i, iw = iw0 + t.j;
+      if ((unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W)
+        v = *reinterpret_cast<const float4*>(X + (base + t.off));
+    } else if (bias && t.one) {
+      v.x = 1.f;
+    }
+    return v;
+  }
+
+  __device__ __forceinline__ void load(const void* Xv, int64_t, int64_t n0, int64_t row_end,
+                                       int64_t, bool bias, bool, int64_t, int64_t, bool diag,
+                                       const ConvGeom& g) {
+    const float* X = (const float*)Xv;
+    const int rloc = threadIdx.x >> 5;
+    const int ohw = g.OH * g.OW;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int row = (int)n0 + rloc + 8 * p;
+      const bool live = row < (int)row_end;
+      int rem, ow;
+      const int b = fdivmod(row, ohw, inv_ohw, rem);
+      const int oh = fdivmod(rem, g.OW, inv_ow, ow);
+      const int ih0 = oh * g.sh - g.ph, iw0 = ow * g.sw - g.pw;
+      const int base = b * (int)g.sB + ih0 * (int)g.sH + iw0 * (int)g.sW;
+      r[0][p] = chunk_of(X, live, base, ih0, iw0, ti, g, bias);
+      if (!diag) r[1][p] = chunk_of(X, live, base, ih0, iw0, tj, g, bias);
+    }
+  }
+};
+
+// ---- implicit im2col on bf16 planes, 32-bit addressing: NPL = 1 (bf16
+// input) or 2 (an fp32 input pre-split once into hi / lo bf16 planes by
+// split_planes_kernel, so the SYRK loop does no fp32 -> bf16 conversion:
+// each input element is otherwise split kh*kw*T times, once per tap and
+// column tile that reads it).  Thread t stages one row (t >> 3) of the
+// k-tile and the 8-element chunks (t & 7) and (t & 7) + 8 of each operand:
+// one row decode per k-tile instead of one per chunk.  Needs C % 8 == 0.
+template <int NPL>
+struct PatchPlanes32 {
+  v8i16 r[2][NPL][2];  // [operand][plane][chunk]
+  Tap32 ti[2], tj[2];
+  float inv_ohw, inv_ow;
+
+  __device__ __forceinline__ void init(int64_t c0i, int64_t c0j, int64_t K, const ConvGeom& g) {
+    const int c = threadIdx.x & 7;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      ti[q] = tap32(c0i + (c + 8 * q) * 8, K, g);
+      tj[q] = tap32(c0j + (c + 8 * q) * 8, K, g);
+    }
+    inv_ohw = 1.f / (float)(g.OH * g.OW);
+    inv_ow = 1.f / (float)g.OW;
+  }
+
+  // buffer loads: a chunk outside the image (padding), past the last row or
+  // in the pad columns gets an offset beyond the descriptor's range, and the
+  // hardware returns zeros (no exec masking, no zero-init moves)
+  __device__ __forceinline__ static v8i16 chunk_of(__amdgpu_buffer_rsrc_t rs, int poff, bool live,
+                                                   int base, int ih0, int iw0, const Tap32& t,
+                                                   const ConvGeom& g, bool bias, bool hi_plane) {
+    const int ih = ih0 + t.i, iw = iw0 + t.j;
+    const bool ok = live && t.kind == 0 && (unsigned)ih < (unsigned)g.H &&
+                    (unsigned)iw < (unsigned)g.W;
+    const int off = ok ? (base + t.off) * 2 + poff : (int)0x80000000u;
+    const v4u32 raw = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+    v8i16 v = __builtin_bit_cast(v8i16, raw);
+    if (bias && hi_plane && t.one && live) v[0] = (short)0x3F80;  // bf16(1.0)
+    return v;
+  }
+
+  __device__ __forceinline__ void load(const void* Xv, int64_t, int64_t n0, int64_t row_end,
+                                       int64_t, bool bias, bool, int64_t, int64_t, bool diag,
+                                       const ConvGeom& g) {
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(Xv), (short)0, (int)g.nbytes, 0x00020000);
+    const int row = (int)n0 + (threadIdx.x >> 3);
+    const bool live = row < (int)row_end;
+    int rem, ow;
+    const int b = fdivmod(row, g.OH * g.OW, inv_ohw, rem);
+    const int oh = fdivmod(rem, g.OW, inv_ow, ow);
+    const int ih0 = oh * g.sh - g.ph, iw0 = ow * g.sw - g.pw;
+    const int base = b * (int)g.sB + ih0 * (int)g.sH + iw0 * (int)g.sW;
+#pragma unroll
+    for (int pl = 0; pl < NPL; ++pl) {
+      const int poff = pl * (int)g.plane * 2;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        r[0][pl][q] = chunk_of(rs, poff, live, base, ih0, iw0, ti[q], g, bias, pl == 0);
+        if (!diag) r[1][pl][q] = chunk_of(rs, poff, live, base, ih0, iw0, tj[q], g, bias, pl == 0);
+      }
+    }
+  }
+
+  // plane pl of an operand at L + pl * BK * LDS_W16 (the SPLIT layout)
+  __device__ __forceinline__ void store(short* Li, short* Lj, bool diag) {
+    const int row = threadIdx.x >> 3, c = threadIdx.x & 7;
+#pragma unroll
+    for (int pl = 0; pl < NPL; ++pl)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int off = pl * BK * LDS_W16 + row * LDS_W16 + (c + 8 * q) * 8;
+        *reinterpret_cast<v8i16*>(Li + off) = r[0][pl][q];
+        if (!diag) *reinterpret_cast<v8i16*>(Lj + off) = r[1][pl][q];
+      }
+  }
+};
+
 // dense mode: the existing Staging with the common load signature
 template <typename TIn>
 struct DenseStaging : Staging<TIn> {
@@ -396,6 +573,28 @@ struct SplitStaging : Base {
     }
   }
 };
+
+// fp32 NHWC input (any batch / row / pixel strides, channel stride 1) ->
+// contiguous NHWC bf16 planes hi = bf16_rn(x), lo = bf16_rn(x - hi)
+__global__ void __launch_bounds__(256) split_planes_kernel(
+    const float* __restrict__ x, int64_t sB, int64_t sH, int64_t sW, int H, int W, int C,
+    int64_t total4, uint16_t* __restrict__ hi, uint16_t* __restrict__ lo) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total4;
+       i += (int64_t)gridDim.x * 256) {
+    const int64_t e = i * 4;
+    const int c = (int)(e % C);
+    const int64_t pix = e / C;
+    const int w = (int)(pix % W);
+    const int64_t bh = pix / W;
+    const int h = (int)(bh % H);
+    const int64_t b = bh / H;
+    const float4 v = *reinterpret_cast<const float4*>(x + b * sB + h * sH + w * sW + c);
+    v4i16 vh, vl;
+    split_f4(v, vh, vl);
+    *reinterpret_cast<v4i16*>(hi + e) = vh;
+    *reinterpret_cast<v4i16*>(lo + e) = vl;
+  }
+}
 
 // bf16 operand fragment for a 32-wide column block `cb` at k offset `kk`:
 // lane l gets X[k = kk + 8h + j][col = cb + (l & 31)], j = 0..7, h = l >> 5,
@@ -542,10 +741,13 @@ syrk_kernel(const void* __restrict__ X, int64_t N, int64_t K, int64_t ldx,
           // stores; 32 lanes write 128 contiguous bytes per row)
           float* slab = ws + ((int64_t)tile * splits + split) * (BM * BM);
           const int lc = wc * 64 + nj * 32 + (l & 31);
+          // (rows / columns past D are never read: skip them)
+          if (gc < D) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int lr = wr * 64 + mi * 32 + 8 * rb + 4 * (l >> 5) + e;
-            slab[lr * BM + lc] = acc[mi][nj][rb * 4 + e];
+            for (int e = 0; e < 4; ++e) {
+              const int lr = wr * 64 + mi * 32 + 8 * rb + 4 * (l >> 5) + e;
+              if (gr0 + e < D) slab[lr * BM + lc] = acc[mi][nj][rb * 4 + e];
+            }
           }
         } else if (packed) {
           // packed upper triangle (the all-reduce wire layout): owned
@@ -601,8 +803,15 @@ syrk_kernel(const void* __restrict__ X, int64_t N, int64_t K, int64_t ldx,
 // Split-K reduction: one 32x32 sub-block of the upper triangle per block.
 // C[i][j] = beta*C[i][j] + alpha * sum_s slab[s][i][j]  (s ascending), and
 // C[j][i] = C[i][j] through an LDS transpose (both writes coalesced).
+// Two passes when the triangle has too few sub-blocks to fill the chip
+// (D = 64 with 512 slabs: 3 blocks, 30-120 us in the r3 step trace):
+// pass 1, grid (sub-blocks, groups), sums the `count` slabs of one group
+// (slabs g*gs .. g*gs+count-1, ascending) back into slab g*gs; pass 2
+// (final) sums the group slabs 0, gs, 2gs, ... in order.  The summation
+// order is fixed by (splits, gs) alone, so results stay bitwise
+// reproducible run to run.
 __global__ void __launch_bounds__(256)
-splitk_reduce_kernel(const float* __restrict__ ws, int splits, int T,
+splitk_reduce_kernel(float* __restrict__ ws, int splits, int T, int gs, int final_pass,
                      float* __restrict__ C, int64_t D, int64_t ldc, int packed,
                      float alpha, const float* __restrict__ ascale, float beta, int T32) {
   if (ascale != nullptr) alpha *= ascale[0];
@@ -615,15 +824,20 @@ splitk_reduce_kernel(const float* __restrict__ ws, int splits, int T,
   const int ti = bi >> 2, tj = bj >> 2;
   const int64_t tidx = (int64_t)ti * T - (int64_t)ti * (ti - 1) / 2 + (tj - ti);
   const int lr = (bi & 3) * 32 + r, lc = (bj & 3) * 32 + c4;
-  const float* src = ws + tidx * splits * (BM * BM) + lr * BM + lc;
+  // pass 1: slabs g*gs + u (u < count); final: slabs u*gs (u < count)
+  const int g = (int)blockIdx.y;
+  const int first = final_pass ? 0 : g * gs;
+  const int count = final_pass ? (int)ceil_div(splits, gs) : min(gs, splits - first);
+  const int64_t step = (int64_t)(final_pass ? gs : 1) * (BM * BM);
+  float* src = ws + (tidx * splits + first) * (BM * BM) + lr * BM + lc;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   // 8 independent loads in flight per thread (fixed summation order)
   int s = 0;
-  for (; s + 8 <= splits; s += 8) {
+  for (; s + 8 <= count; s += 8) {
     float4 v[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u)
-      v[u] = *reinterpret_cast<const float4*>(src + (int64_t)(s + u) * (BM * BM));
+      v[u] = *reinterpret_cast<const float4*>(src + (int64_t)(s + u) * step);
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       acc.x += v[u].x;
@@ -632,12 +846,16 @@ splitk_reduce_kernel(const float* __restrict__ ws, int splits, int T,
       acc.w += v[u].w;
     }
   }
-  for (; s < splits; ++s) {
-    const float4 v = *reinterpret_cast<const float4*>(src + (int64_t)s * (BM * BM));
+  for (; s < count; ++s) {
+    const float4 v = *reinterpret_cast<const float4*>(src + (int64_t)s * step);
     acc.x += v.x;
     acc.y += v.y;
     acc.z += v.z;
     acc.w += v.w;
+  }
+  if (!final_pass) {
+    *reinterpret_cast<float4*>(src) = acc;
+    return;
   }
   const int64_t gr = (int64_t)bi * 32 + r;
   const float a4[4] = {acc.x, acc.y, acc.z, acc.w};
@@ -696,6 +914,18 @@ int64_t syrk_workspace_floats(int64_t D, int64_t splits) {
   return T * (T + 1) / 2 * splits * BM * BM;
 }
 
+// fp32 NHWC conv input -> contiguous bf16 hi / lo planes (hi at `planes`,
+// lo at planes + B*H*W*C) for the pre-split implicit-im2col SYRK
+void syrk_split_planes(const float* x, int64_t B, int H, int W, int C, int64_t sB, int64_t sH,
+                       int64_t sW, uint16_t* planes, hipStream_t s) {
+  const int64_t total = B * H * W * (int64_t)C;
+  if (total == 0) return;
+  const int64_t total4 = total / 4;
+  const unsigned blocks = (unsigned)std::min<int64_t>(ceil_div(total4, 256), 8192);
+  split_planes_kernel<<<dim3(blocks), dim3(256), 0, s>>>(x, sB, sH, sW, H, W, C, total4, planes,
+                                                         planes + total);
+}
+
 // geom == nullptr: X is a dense [N, K] matrix (row stride ldx); otherwise
 // X is an NHWC conv input and its rows are the conv patches (implicit im2col).
 // ws: syrk_workspace_floats(D, splits) floats when splits > 1.
@@ -713,7 +943,15 @@ void syrk(int in_dtype, const void* x, int64_t N, int64_t K, int64_t ldx,
   const int64_t rows_per_split =
       splits > 1 ? ceil_div(ceil_div(N, splits), BK) * BK : (N > 0 ? N : 1);
   const dim3 grid((unsigned)(tiles * splits));
-  const ConvGeom g = geom != nullptr ? *geom : ConvGeom{};
+  ConvGeom g = geom != nullptr ? *geom : ConvGeom{};
+  if (geom != nullptr) {
+    // bytes the implicit-im2col buffer loads may touch (bf16 elements: the
+    // planes, or the bf16 input's last element + 1)
+    const int64_t nb = N / ((int64_t)g.OH * g.OW);
+    g.nbytes = g.plane > 0 ? 4 * g.plane
+                           : 2 * ((nb - 1) * g.sB + (int64_t)(g.H - 1) * g.sH +
+                                  (int64_t)(g.W - 1) * g.sW + g.C);
+  }
   if (in_dtype == kF32) {
     const int vec_ok = ((ldx & 3) == 0) &&
                        ((reinterpret_cast<uintptr_t>(x) & 15) == 0);
@@ -721,8 +959,17 @@ void syrk(int in_dtype, const void* x, int64_t N, int64_t K, int64_t ldx,
   syrk_kernel<float, STAGE, SPLIT_><<<grid, dim3(NT), 0, s>>>(                      \
       x, N, K, ldx, bias ? 1 : 0, C, D, ldc, packed, alpha, ascale, beta, T, splits, \
       rows_per_split, vec_ok, g, ws)
-    if (geom != nullptr) {
+    if (geom != nullptr && g.plane > 0) {
+      // pre-split bf16 planes (syrk_split_planes)
+      SYRK_F32(PatchPlanes32<2>, true);
+    } else if (geom != nullptr) {
+      // 32-bit patch addressing when every row index and input offset fits
+      // (fdivmod is exact below 2^24 rows)
+      const int64_t in_elems = (int64_t)(N / ((int64_t)g.OH * g.OW) + 1) * g.sB;
+      const bool fast = N < (int64_t(1) << 24) && in_elems < (int64_t(1) << 31) &&
+                        g.sB < (int64_t(1) << 31);
       if (fp32_exact) SYRK_F32(PatchStaging<float>, false);
+      else if (fast) SYRK_F32(SplitStaging<PatchStaging32<float>>, true);
       else SYRK_F32(SplitStaging<PatchStaging<float>>, true);
     } else {
       if (fp32_exact) SYRK_F32(DenseStaging<float>, false);
@@ -732,7 +979,14 @@ void syrk(int in_dtype, const void* x, int64_t N, int64_t K, int64_t ldx,
   } else {
     const int vec_ok = ((ldx & 7) == 0) &&
                        ((reinterpret_cast<uintptr_t>(x) & 15) == 0);
-    if (geom != nullptr)
+    const bool fast32 = geom != nullptr && N < (int64_t(1) << 24) && g.C % 8 == 0 &&
+                        g.nbytes < (int64_t(1) << 31) &&
+                        (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+    if (geom != nullptr && fast32)
+      syrk_kernel<bf16_t, PatchPlanes32<1>><<<grid, dim3(NT), 0, s>>>(
+          x, N, K, ldx, bias ? 1 : 0, C, D, ldc, packed, alpha, ascale, beta, T, splits,
+          rows_per_split, vec_ok, g, ws);
+    else if (geom != nullptr)
       syrk_kernel<bf16_t, PatchStaging<bf16_t>><<<grid, dim3(NT), 0, s>>>(
           x, N, K, ldx, bias ? 1 : 0, C, D, ldc, packed, alpha, ascale, beta, T, splits,
           rows_per_split, vec_ok, g, ws);
@@ -744,8 +998,22 @@ void syrk(int in_dtype, const void* x, int64_t N, int64_t K, int64_t ldx,
   if (splits > 1) {
     const int T32 = (int)ceil_div(D, 32);
     const unsigned blocks = (unsigned)((int64_t)T32 * (T32 + 1) / 2);
+    // groups for pass 1: enough blocks to fill the chip, <= 16 group slabs
+    // for the final pass, >= 4 slabs per group
+    // (gs = 1: no pass 1, the final pass sums every slab)
+    int gs = 1;
+    if (blocks < 512 && splits >= 8) {
+      int groups = (int)std::min<int64_t>(ceil_div(512, blocks), splits / 4);
+      groups = std::max(groups, (int)ceil_div(splits, 64));
+      gs = (int)ceil_div(splits, groups);
+    }
+    if (gs > 1) {
+      const unsigned groups = (unsigned)ceil_div(splits, gs);
+      splitk_reduce_kernel<<<dim3(blocks, groups), dim3(256), 0, s>>>(
+          ws, splits, T, gs, 0, C, D, ldc, packed, alpha, ascale, beta, T32);
+    }
     splitk_reduce_kernel<<<dim3(blocks), dim3(256), 0, s>>>(
-        ws, splits, T, C, D, ldc, packed, alpha, ascale, beta, T32);
+        ws, splits, T, gs, 1, C, D, ldc, packed, alpha, ascale, beta, T32);
   }
 }
 

@@ -3,13 +3,14 @@
 ``BatchNormAct2d`` is an ``nn.BatchNorm2d`` (same parameters, buffers and
 state-dict keys as torchvision's) with one extra entry point,
 ``act(x, residual=None, relu=True)`` = ``relu(bn(x) + residual)``.  In
-training mode on NHWC (channels_last) bf16 activations -- the layout and
-dtype of a ResNet under bf16 autocast on MI355X -- it runs the native
+training mode on NHWC (channels_last) bf16 or fp32 activations -- the
+layouts of a ResNet under bf16 autocast or in fp32 on MI355X -- it runs the native
 kernels of ``csrc/bnact.hip``: 3 launches forward and 3 backward per layer,
 replacing MIOpen's BN kernels, its tensor ops, the separate ReLU forward /
 backward, the residual add and the ``num_batches_tracked`` increment.
-Everything else (eval mode, fp32 / NCHW inputs, CPU) takes the PyTorch
-path with identical semantics.  ``KFAC_FUSED_BN=0`` disables the kernels.
+Everything else (eval mode, NCHW inputs, CPU) takes the PyTorch path with
+identical semantics.  ``KFAC_FUSED_BN=0`` disables the kernels,
+``KFAC_FUSED_BN_FP32=0`` only their fp32 use.
 """
 from __future__ import annotations
 
@@ -27,6 +28,13 @@ __all__ = ['BatchNormAct2d', 'bn_act']
 
 def _enabled() -> bool:
     return os.environ.get('KFAC_FUSED_BN', '1') != '0'
+
+
+def _dtypes() -> tuple[torch.dtype, ...]:
+    # KFAC_FUSED_BN_FP32=0 keeps fp32 activations on the PyTorch / MIOpen path
+    if os.environ.get('KFAC_FUSED_BN_FP32', '1') == '0':
+        return (torch.bfloat16,)
+    return (torch.bfloat16, torch.float32)
 
 
 class _BNActFunction(torch.autograd.Function):
@@ -78,13 +86,13 @@ def _fusable(bn: nn.BatchNorm2d, x: torch.Tensor, residual: torch.Tensor | None)
     if not (_enabled() and bn.training and bn.track_running_stats and bn.momentum is not None
             and bn.affine):
         return False
-    if not x.is_cuda or x.dtype != torch.bfloat16:
+    if not x.is_cuda or x.dtype not in _dtypes():
         return False
     lib = native()
     if lib is None or not lib.bn_act_supported(x):
         return False
     if residual is not None:
-        if residual.dtype != torch.bfloat16 or residual.shape != x.shape:
+        if residual.dtype != x.dtype or residual.shape != x.shape:
             return False
         if not lib.bn_act_supported(residual):
             return False

@@ -1,5 +1,5 @@
 """Fused BatchNorm (+ residual) (+ ReLU) kernels (csrc/bnact.hip) vs the
-PyTorch fp32 math on the same bf16 inputs."""
+PyTorch fp32 math on the same bf16 / fp32 inputs."""
 from __future__ import annotations
 
 import pytest
@@ -23,12 +23,13 @@ def _cl(t: torch.Tensor) -> torch.Tensor:
                                    (16, 32, 32, 32)])
 @pytest.mark.parametrize('relu', [True, False])
 @pytest.mark.parametrize('residual', [True, False])
-def test_bn_act_matches_reference(cuda, shape, relu, residual):
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float32])
+def test_bn_act_matches_reference(cuda, shape, relu, residual, dtype):
     torch.manual_seed(sum(shape))
     n, c, h, w = shape
-    x = _cl((torch.randn(shape, device=cuda) * 2 + 0.5).to(torch.bfloat16))
-    res = _cl(torch.randn(shape, device=cuda).to(torch.bfloat16)) if residual else None
-    dy = _cl(torch.randn(shape, device=cuda).to(torch.bfloat16))
+    x = _cl((torch.randn(shape, device=cuda) * 2 + 0.5).to(dtype))
+    res = _cl(torch.randn(shape, device=cuda).to(dtype)) if residual else None
+    dy = _cl(torch.randn(shape, device=cuda).to(dtype))
     bn = bnact.BatchNormAct2d(c).to(cuda)
     with torch.no_grad():
         bn.weight.uniform_(0.5, 1.5)
@@ -51,15 +52,17 @@ def test_bn_act_matches_reference(cuda, shape, relu, residual):
         yr = F.relu(yr)
     yr.backward(dy.float())
 
-    assert y.dtype == torch.bfloat16 and y.is_contiguous(memory_format=torch.channels_last)
-    tol = 2e-2
-    assert (y.float() - yr).abs().max().item() <= tol * yr.abs().max().item() + 1e-2
+    assert y.dtype == dtype and y.is_contiguous(memory_format=torch.channels_last)
+    fp32 = dtype == torch.float32
+    tol, atol = (1e-5, 1e-5) if fp32 else (2e-2, 1e-2)
+    assert (y.float() - yr).abs().max().item() <= tol * yr.abs().max().item() + atol
     gx = xr.grad.abs().max().item()
-    assert (xa.grad.float() - xr.grad).abs().max().item() <= tol * gx + 1e-3
-    assert torch.allclose(bn.weight.grad, ref_bn.weight.grad, rtol=1e-2, atol=1e-2)
-    assert torch.allclose(bn.bias.grad, ref_bn.bias.grad, rtol=1e-2, atol=1e-2)
+    assert (xa.grad.float() - xr.grad).abs().max().item() <= (1e-4 if fp32 else tol) * gx + 1e-5
+    gtol = 1e-4 if fp32 else 1e-2
+    assert torch.allclose(bn.weight.grad, ref_bn.weight.grad, rtol=gtol, atol=gtol)
+    assert torch.allclose(bn.bias.grad, ref_bn.bias.grad, rtol=gtol, atol=gtol)
     if residual:
-        assert (ra.grad.float() - rr.grad).abs().max().item() <= 1e-2 * rr.grad.abs().max().item() + 1e-3
+        assert (ra.grad.float() - rr.grad).abs().max().item() <= gtol * rr.grad.abs().max().item() + 1e-5
     assert torch.allclose(bn.running_mean, ref_bn.running_mean, rtol=1e-4, atol=1e-5)
     assert torch.allclose(bn.running_var, ref_bn.running_var, rtol=1e-4, atol=1e-5)
     assert int(bn.num_batches_tracked) == int(ref_bn.num_batches_tracked) == 1

@@ -140,8 +140,13 @@ def _natural_patches(x: torch.Tensor, k, s, p) -> torch.Tensor:
     (3, 32, 16, 16, (1, 1), (2, 2), (0, 0), False),
     (2, 8, 9, 11, (5, 3), (1, 2), (2, 0), True),
     (2, 136, 7, 7, (3, 3), (1, 1), (1, 1), False),
+    # C % 8 != 0: fp32 takes the in-loop split staging, not the bf16 planes
+    (2, 12, 10, 9, (3, 3), (1, 1), (1, 1), True),
+    (3, 20, 8, 8, (3, 3), (2, 2), (1, 1), False),
 ])
 def test_syrk_conv_implicit_im2col(cuda, cfg, dtype):
+    if dtype == torch.bfloat16 and cfg[1] % 8:
+        pytest.skip('bf16 implicit im2col needs C % 8 == 0 (explicit patches otherwise)')
     b, c, h, w, k, s, p, bias = cfg
     torch.manual_seed(sum(cfg[:4]))
     x = torch.randn(b, c, h, w, device=cuda).to(dtype).contiguous(
@@ -159,6 +164,22 @@ def test_syrk_conv_implicit_im2col(cuda, cfg, dtype):
     tol = 1e-5 if dtype == torch.float32 else 1e-4
     assert (out.double() - ref).abs().max().item() <= tol * ref.abs().max().item()
     assert torch.equal(out, out.t())
+
+
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float32])
+def test_syrk_conv_batch_slice(cuda, dtype):
+    """A batch slice of a larger channels_last activation (the buffer-load
+    range of the implicit im2col covers only the slice's extent)."""
+    torch.manual_seed(3)
+    full = torch.randn(6, 32, 12, 12, device=cuda).to(dtype).contiguous(
+        memory_format=torch.channels_last)
+    x = full[2:5]
+    pm, _ = _natural_patches(x.double(), (3, 3), (1, 1), (1, 1))
+    ref = pm.t() @ pm / pm.shape[0]
+    out = torch.zeros(pm.shape[1], pm.shape[1], device=cuda)
+    assert factors.conv_cov_accumulate_(out, x, (3, 3), (1, 1), (1, 1), alpha=1.0 / pm.shape[0])
+    tol = 1e-5 if dtype == torch.float32 else 1e-4
+    assert (out.double() - ref).abs().max().item() <= tol * ref.abs().max().item()
 
 
 def test_syrk_conv_rejects_unaligned_channels(cuda):

@@ -8,6 +8,8 @@ timeout -k 10 240 python3 -u tools/syrk_probe.py --json $O/v2.jsonl > $O/v2.log 
 tail -1 $O/v2.log
 timeout -k 10 300 python3 -u bench.py --steps 100 --warmup 10 > $O/bench.json 2> $O/bench.err || { echo "bench rc=$?"; tail -5 $O/bench.err; exit 1; }
 python3 -c "import json;d=json.load(open('$O/bench.json'));print(d['value'],d['ms_per_step'],d['kind_ms'],d.get('sgd_ms_per_step'),d['params_finite'])"
+KFAC_GRAPH_KINDS=plain timeout -k 10 300 python3 -u bench.py --steps 100 --warmup 10 --secondary-bf16 0 > $O/bench_plainonly.json 2> $O/bench_plainonly.err || { echo "bench2 rc=$?"; tail -5 $O/bench_plainonly.err; exit 1; }
+python3 -c "import json;d=json.load(open('$O/bench_plainonly.json'));print('plain-only graphs', d['value'],d['ms_per_step'],d['kind_ms'],d['params_finite'])"
 timeout -k 10 400 python -u tools/graph_nan_probe.py --steps 26 --image 224 --batch 32 --fused-sgd 1 --factor-steps 10 > $O/nan_bf16.jsonl 2> $O/nan_bf16.err || { echo "nanprobe rc=$?"; tail -3 $O/nan_bf16.err; exit 1; }
 python3 -c "
 import json
