@@ -275,8 +275,11 @@ void syrk_conv(const at::Tensor& x, at::Tensor& C, int64_t kh, int64_t kw,
   // fp32 input on the bf16x3 path: split it once into contiguous bf16 hi / lo
   // planes (stream-ordered temporary) so the SYRK loop converts nothing
   const int64_t elems = B * H * W * Cin;
-  if (x.scalar_type() == at::kFloat && !fp32_exact && Cin % 8 == 0 && N < (1LL << 24) &&
-      elems < (1LL << 29)) {
+  // (only for kernels with several taps: a 1x1 strided conv reads a
+  // quarter of its input once, so splitting all of it costs more than the
+  // in-loop split it saves)
+  if (x.scalar_type() == at::kFloat && !fp32_exact && Cin % 8 == 0 && kh * kw > 1 &&
+      N < (1LL << 24) && elems < (1LL << 29)) {
     at::Tensor planes = at::empty({2 * elems}, x.options().dtype(at::kBFloat16));
     kfac::syrk_split_planes(x.data_ptr<float>(), B, (int)H, (int)W, (int)Cin, x.stride(0),
                             x.stride(2), x.stride(3),

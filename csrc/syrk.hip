@@ -1002,7 +1002,10 @@ void syrk(int in_dtype, const void* x, int64_t N, int64_t K, int64_t ldx,
     // for the final pass, >= 4 slabs per group
     // (gs = 1: no pass 1, the final pass sums every slab)
     int gs = 1;
-    if (blocks < 512 && splits >= 8) {
+    // (a second launch only pays when one pass would take > ~16 rounds of
+    // 8 loads per thread: measured 25 -> 31 us for 49 slabs, 59 -> 45 us
+    // for 512, profiles/syrk_probe_r3_v2.jsonl)
+    if (blocks < 512 && splits >= 128) {
       int groups = (int)std::min<int64_t>(ceil_div(512, blocks), splits / 4);
       groups = std::max(groups, (int)ceil_div(splits, 64));
       gs = (int)ceil_div(splits, groups);

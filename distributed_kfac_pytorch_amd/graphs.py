@@ -26,9 +26,12 @@ fixed addresses; the descriptor tables that the grouped K-FAC kernels build
 from those addresses during the capture are uploaded from pinned host
 buffers the table caches keep alive (``ops.precondition._TableCache``).
 Eager steps in between (second-order updates) keep the gradients allocated
-(``zero_grad(set_to_none=False)``).  Both kinds are captured together (the other kind with
-the step counter temporarily set to its next occurrence), so no capture
-lands inside a timed run later.  Replays advance the host-side
+(``zero_grad(set_to_none=False)``).  By default only ``plain`` steps are
+replayed (``kinds``): an eager factor-update step overlaps its SYRKs with
+backward on the factor side stream, which a replayed graph does not.  The
+captured kinds are captured together (the other kind with the step counter
+temporarily set to its next occurrence), so no capture lands inside a timed
+run later.  Replays advance the host-side
 K-FAC state (``steps``) exactly as an eager step would.  Values baked into a
 graph -- K-FAC hyperparameters, the optimizer's learning rates -- form a
 signature; when it changes the affected graphs are dropped and re-captured.
@@ -103,6 +106,7 @@ class GraphedTrainStep:
         *,
         warmup: int = 1,
         enabled: bool | None = None,
+        kinds: tuple[str, ...] = ('plain',),
     ) -> None:
         self.forward_backward = forward_backward
         self.optimizer = optimizer
@@ -114,6 +118,17 @@ class GraphedTrainStep:
                 not multi or os.environ.get('KFAC_STEP_GRAPHS_MULTI', '0') == '1'
             )
         self.enabled = enabled
+        # Step kinds replayed from graphs.  Factor-update steps stay eager by
+        # default: their SYRKs run on the factor side stream concurrently with
+        # backward, and a replayed graph executes its nodes in one queue, so
+        # the captured factor step was slower than the eager one (ResNet-50
+        # fp32: 24.9 vs 22.6 ms, 1485 vs 1555 img/s;
+        # profiles/bench_r3_fp32_fusedbn_*graphs.json).  KFAC_GRAPH_KINDS
+        # overrides (e.g. "plain,factor").
+        env = os.environ.get('KFAC_GRAPH_KINDS')
+        if env:
+            kinds = tuple(k.strip() for k in env.split(',') if k.strip())
+        self.kinds = tuple(k for k in kinds if k in ('plain', 'factor'))
         if enabled and preconditioner is not None and getattr(preconditioner, '_graphs', None):
             # The whole-step graph already contains the precondition phase.
             # With the preconditioner's own precondition-phase graphs
@@ -289,10 +304,7 @@ class GraphedTrainStep:
             if self.seen < self.warmup or not self._capturable():
                 self.seen += 1
                 return self._eager()
-            kinds = ('plain', 'factor') if self.preconditioner is not None else ('plain',)
-            only = os.environ.get('KFAC_GRAPH_KINDS')  # diagnostics: capture a subset
-            if only:
-                kinds = tuple(k for k in only.split(',') if k in kinds)
+            kinds = self.kinds if self.preconditioner is not None else ('plain',)
             for k in kinds:
                 if k not in self.graphs:
                     failed = None

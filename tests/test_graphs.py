@@ -110,13 +110,15 @@ def _state_diff(ma, oa, pa, mb, ob, pb) -> float:
 
 @pytest.mark.gpu
 @pytest.mark.parametrize('method', ['eigen', 'inverse'])
-def test_graph_replay_matches_eager(cuda, deterministic, method) -> None:
+@pytest.mark.parametrize('kinds', [('plain',), ('plain', 'factor')])
+def test_graph_replay_matches_eager(cuda, deterministic, method, kinds) -> None:
     """Whole-step graph replay vs eager steps, compared after EVERY step
     over 20 steps (3 second-order updates: the eigenbases / inverses are
-    reinstalled in place under the captured graphs)."""
+    reinstalled in place under the captured graphs); plain steps replayed
+    with factor steps eager (the default) or both replayed."""
     steps = 20
     model, opt, pre, fb = _setup(cuda, method=method)
-    runner = GraphedTrainStep(fb, opt, pre)
+    runner = GraphedTrainStep(fb, opt, pre, kinds=kinds)
     mb, ob, pb, run_b = _eager_runner(cuda, method)
     for i in range(steps):
         la = float(runner())
@@ -125,8 +127,8 @@ def test_graph_replay_matches_eager(cuda, deterministic, method) -> None:
         assert abs(la - lb) <= 1e-6 * max(1.0, abs(lb)), (i, la, lb)
         d = _state_diff(model, opt, pre, mb, ob, pb)
         assert d <= 1e-6, (i, runner.kind(), d)
-    assert runner.captures == 2, runner.captures
-    assert runner.replays >= 14, runner.replays
+    assert runner.captures == len(kinds), runner.captures
+    assert runner.replays >= (14 if 'factor' in kinds else 10), runner.replays
     assert pre.steps == pb.steps == steps
 
 

@@ -117,6 +117,9 @@ def main() -> None:
     ap.add_argument('--batch', type=int, default=8)
     ap.add_argument('--fused-sgd', type=int, default=0)
     ap.add_argument('--channels-last', type=int, default=1)
+    ap.add_argument('--sequential', action='store_true',
+                    help='run the graph model through all steps first (CPU snapshots), '
+                         'then the eager twin: no eager work between replays')
     args = ap.parse_args()
     torch.backends.cudnn.deterministic = bool(args.deterministic)
     torch.backends.cudnn.benchmark = bool(args.benchmark)
@@ -126,6 +129,9 @@ def main() -> None:
     dev = torch.device('cuda')
     torch.manual_seed(0)
     base = resnet50(num_classes=10)
+    if args.sequential:
+        sequential(base, dev, args)
+        return
     A = build(base, dev, args.compare == 'graphs', not args.fp32, bool(args.fused_cast),
               args.warmup, not args.no_kfac, args.factor_steps)
     B = build(base, dev, False, not args.fp32, bool(args.fused_cast), 1,
@@ -172,6 +178,33 @@ def main() -> None:
         print(json.dumps(rec), flush=True)
         if any(rec[k]['nonfinite'] for k in sa):
             break
+
+
+def sequential(base, dev, args) -> None:  # type: ignore[no-untyped-def]
+    gen = torch.Generator(device='cpu').manual_seed(1)
+    pool = [(torch.randn(_BATCH, 3, _IMG, _IMG, generator=gen),
+             torch.randint(0, 10, (_BATCH,), generator=gen)) for _ in range(4)]
+    snaps = []
+    for graphs in (True, False):
+        m = build(base, dev, graphs, not args.fp32, bool(args.fused_cast), args.warmup,
+                  not args.no_kfac, args.factor_steps)
+        run = []
+        for i in range(args.steps):
+            x, y = pool[i % len(pool)]
+            m[3].copy_(x)
+            m[4].copy_(y)
+            loss = float(m[5]())
+            torch.cuda.synchronize()
+            run.append((loss, [p.detach().float().cpu() for p in m[0].parameters()],
+                        getattr(m[5], 'replays', 0)))
+        snaps.append(run)
+        del m
+        torch.cuda.synchronize()
+    for i, ((la, pa, ra), (lb, pb, _)) in enumerate(zip(*snaps)):
+        bad = sum(int(not bool(torch.isfinite(a).all())) for a in pa)
+        rel = max(float((a - b).abs().max() / b.abs().max().clamp_min(1e-30)) for a, b in zip(pa, pb))
+        print(json.dumps({'step': i, 'replays': ra, 'loss': [la, lb], 'nonfinite': bad,
+                          'param_maxrel': rel}), flush=True)
 
 
 if __name__ == '__main__':
