@@ -128,7 +128,7 @@ def test_graph_replay_matches_eager(cuda, deterministic, method, kinds) -> None:
         d = _state_diff(model, opt, pre, mb, ob, pb)
         assert d <= 1e-6, (i, runner.kind(), d)
     assert runner.captures == len(kinds), runner.captures
-    assert runner.replays >= (14 if 'factor' in kinds else 10), runner.replays
+    assert runner.replays >= (14 if 'factor' in kinds else 9), runner.replays
     assert pre.steps == pb.steps == steps
 
 

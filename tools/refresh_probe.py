@@ -122,6 +122,11 @@ def main() -> None:
     print(json.dumps({'factors': len(mats), 'sizes': dict(sorted(sizes.items()))}), flush=True)
 
     def run(mode: str):  # type: ignore[no-untyped-def]
+        if mode.startswith('default'):
+            # the library's default tiers, untouched (default / default_warm)
+            w = list(warm) if '_warm' in mode else None
+            linalg.last_stats.clear()
+            return linalg.eigh_many([m.clone() for m in mats], w)
         os.environ['KFAC_EIGH_BLOCK'] = '0' if mode == 'syevd' else '1'
         os.environ['KFAC_EIGH_LARGE'] = 'block' if mode.startswith('block') else 'syevd'
         if mode.startswith('sytrd'):
