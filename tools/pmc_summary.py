@@ -63,7 +63,16 @@ def load(base: str, prefix: str) -> dict:
             if k and c and v:
                 counters[short(r[k])][r[c]] += float(r[v] or 0)
         if p == 'sq':
-            for r in _read(os.path.join(d, f'{prefix}_{p}_kernel_trace.csv')):
+            trace = _read(os.path.join(d, f'{prefix}_{p}_kernel_trace.csv'))
+            if not trace:
+                # counter-only pass (no --kernel-trace): one row per
+                # (dispatch, counter) carries the dispatch's timestamps
+                seen = {}
+                for r in rows:
+                    if 'Dispatch_Id' in r:
+                        seen[r['Dispatch_Id']] = r
+                trace = list(seen.values())
+            for r in trace:
                 k = _col(r, 'Kernel_Name', 'Kernel-Name')
                 s = _col(r, 'Start_Timestamp', 'Start-Timestamp')
                 e = _col(r, 'End_Timestamp', 'End-Timestamp')
