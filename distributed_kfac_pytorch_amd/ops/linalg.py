@@ -193,6 +193,32 @@ def twostage_min_n() -> int:
     return int(os.environ.get('KFAC_TWOSTAGE_MIN_N', str(1 << 30)))
 
 
+def twostage_bucket_rows() -> int:
+    """Size buckets of n >= 700 holding >= 8 factors and >= this many matrix
+    rows in total (count x n; ``KFAC_TWOSTAGE_BUCKET_ROWS``, default 18000)
+    go to the two-stage solver: its bulge chase runs one workgroup per
+    matrix, so a large batch of equal-size factors fills the chip where a
+    one-stage chain over the same bucket is one long latency-bound sequence.
+    GPT-NeoX-125M (12 x 2304 / 3072 / 3073 = 27.6k-36.9k rows, 36 x 769,
+    24 x 768 = 18.4k): eigen refresh 667 ms on the chains, 405 ms two-stage
+    (profiles/neox_twostage_r3.txt).  ResNet-50's largest bucket has 14.3k
+    rows (14 x 1024) and stays on the chains, which win there
+    (profiles/twostage_r3.md)."""
+    return int(os.environ.get('KFAC_TWOSTAGE_BUCKET_ROWS', '18000'))
+
+
+def twostage_sizes(counts: dict) -> set:
+    """Factor sizes the bucket-population rule sends to the two-stage solver,
+    from ``{n: number of factors of size n}``."""
+    rows = twostage_bucket_rows()
+    return {n for n, c in counts.items() if n >= 700 and c >= 8 and c * n >= rows}
+
+
+# sizes routed to the two-stage solver by bucket population (set per call of
+# eigh_many, read by every tier decision of that call)
+_TS_BATCH_SIZES: set = set()
+
+
 def _use_twostage(n: int) -> bool:
     """Native two-stage solver (ops/twostage.py) for this factor size."""
     mode = os.environ.get('KFAC_EIGH', 'auto')
@@ -202,7 +228,7 @@ def _use_twostage(n: int) -> bool:
         return False
     if mode == 'twostage' or large_algo() == 'twostage':
         return True
-    return large_algo() == 'sytrd' and n >= twostage_min_n()
+    return large_algo() == 'sytrd' and (n >= twostage_min_n() or n in _TS_BATCH_SIZES)
 
 
 def large_algo() -> str:
@@ -328,6 +354,11 @@ def eigh_many(
                 for k, i in enumerate(idxs):
                     out[i] = (evals[k], evecs[k])
         else:
+            counts: dict[int, int] = defaultdict(int)
+            for key, idxs in gpu:
+                counts[key[0]] += len(idxs)
+            _TS_BATCH_SIZES.clear()
+            _TS_BATCH_SIZES.update(twostage_sizes(counts))
             stacks = {
                 key: torch.stack([mats[i].to(torch.float32) for i in idxs])
                 for key, idxs in gpu
