@@ -241,8 +241,9 @@ def run(args: argparse.Namespace, use_kfac: bool, rank: int, world: int,
     if amp and not args.graphs_bf16:
         # bf16 autocast runs eager: whole-step replays of the bf16 K-FAC step
         # went non-finite 1-13 steps after the step-100 refresh in round-3
-        # bench runs (gpurun_out/r3bn4: with or without the fused casts, the
-        # fused BN, the factor side stream, a sync after the refresh), while
+        # bench runs (profiles/graph_replay_r3_investigation.txt: with or
+        # without the fused casts, the fused BN, the factor side stream, a
+        # sync after the refresh), while
         # eager bf16 and the fp32 replays (bit-exact vs eager in
         # tests/test_graphs_refresh_gpu.py) stayed finite
         use_graphs = False

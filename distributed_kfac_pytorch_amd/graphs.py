@@ -135,7 +135,7 @@ class GraphedTrainStep:
             # (StepGraphs) also active, the replays after capture produced
             # garbage preconditioned gradients from the first replay on, while
             # with StepGraphs off the replays matched the eager twin exactly
-            # (ResNet-50, bf16 and fp32: gpurun_out/r3d/probe_*.jsonl,
+            # (ResNet-50, bf16 and fp32:
             # profiles/graph_replay_stepgraphs_r3.txt).
             preconditioner._graphs = None
         self.graphs: dict[str, torch.cuda.CUDAGraph] = {}

@@ -17,7 +17,7 @@ with three refreshes inside the replay window.  The graph run goes first
 refresh), then an eager twin from the same weights and data; with
 deterministic MIOpen the two agree to the bit (round 3).  The twin runs
 AFTER the graph run: interleaving a second model's eager steps between
-replays perturbed the replays (tools/graph_nan_probe.py, gpurun_out/r3bn*),
+replays perturbed the replays (profiles/graph_replay_r3_investigation.txt),
 while runs with no foreign work between replays -- eager factor / refresh
 steps of the same model included -- matched exactly.
 """
