@@ -34,11 +34,13 @@ import time
 # immediate mode picks the recorded fastest solution for every conv instead
 # of re-running a noisy find in each process.  Must be set before MIOpen
 # initialises; an explicit MIOPEN_USER_DB_PATH wins.
-# Hardware queues per process (HIP's default is 4): the eigensolver refresh
+# Hardware queues per process: HIP's default of 4.  The eigensolver refresh
 # runs its size buckets on independent streams, one per hardware queue
-# (ops/linalg.py), so more queues let more buckets overlap.  Must be set
-# before the HIP runtime initialises; an explicit value wins.
-os.environ.setdefault('GPU_MAX_HW_QUEUES', '8')
+# (ops/linalg.py); with the native chains 4 queues beat 8 on every paired
+# run (refresh step 257 / 270 / 285 ms vs 325 / 330 / 325 ms, alternating
+# runs on one box: profiles/refresh_hwq_r3.txt).  Must be set before the HIP
+# runtime initialises; an explicit value wins.
+os.environ.setdefault('GPU_MAX_HW_QUEUES', '4')
 _MIOPEN_DB = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'miopen_db')
 if os.path.isdir(_MIOPEN_DB):
     os.environ.setdefault('MIOPEN_USER_DB_PATH', _MIOPEN_DB)
