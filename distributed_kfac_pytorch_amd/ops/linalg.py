@@ -149,9 +149,14 @@ def _block_jacobi(stack: torch.Tensor, warm: torch.Tensor | None) -> tuple[torch
 
 
 WARM_ACCEPT_TOL = float(os.environ.get('KFAC_EIGH_ACCEPT_TOL', '1e-6'))
-# the acceptance GEMM sits on the critical path of a lane: the largest
-# (A) factors essentially never pass, so they go straight to the solver
-WARM_ACCEPT_MAX_N = int(os.environ.get('KFAC_EIGH_ACCEPT_MAX_N', '2048'))
+# Warm-basis acceptance (reuse the previous eigenbasis when it still
+# diagonalises the new factor to KFAC_EIGH_ACCEPT_TOL) for n <= this; off by
+# default: its batched Q^T A Q GEMMs and host read-back sit on the lanes'
+# critical path, and the ResNet-50 refresh step was faster and steadier
+# without it (248 / 253 ms vs 328 / 277 ms with n <= 2048, alternating
+# runs: profiles/refresh_accept_r3.txt) -- every factor is then solved
+# afresh, as the reference's torch.linalg.eigh does
+WARM_ACCEPT_MAX_N = int(os.environ.get('KFAC_EIGH_ACCEPT_MAX_N', '0'))
 
 
 def _accept_warm(stack: torch.Tensor, warm: torch.Tensor

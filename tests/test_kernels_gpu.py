@@ -312,6 +312,7 @@ def test_eigh_many_sytrd_warm_acceptance(cuda, monkeypatch):
     matches float64."""
     monkeypatch.setenv('KFAC_EIGH_LARGE', 'sytrd')
     monkeypatch.setenv('KFAC_SYTRD_MIN_N', '250')  # 300: chain; 130, 200: syevd
+    monkeypatch.setattr(linalg, 'WARM_ACCEPT_MAX_N', 2048)  # opt-in since round 3
     torch.manual_seed(11)
     mats, warm = [], []
     for j, n in enumerate((200, 200, 300, 130)):
@@ -440,9 +441,10 @@ def test_block_jacobi_cold_and_warm(cuda, n):
     assert sweeps['warm'] < sweeps['cold'], sweeps
 
 
-def test_eigh_many_warm_accept(cuda):
+def test_eigh_many_warm_accept(cuda, monkeypatch):
     """A factor its previous basis still diagonalises keeps that basis (one
     GEMM, no solve); the others of the bucket are solved; all exact."""
+    monkeypatch.setattr(linalg, 'WARM_ACCEPT_MAX_N', 2048)  # opt-in since round 3
     mats, warms = [], []
     for j, n in enumerate((200, 200, 200, 333)):
         old, new = _kfac_like(n, 200 + j, cuda)
