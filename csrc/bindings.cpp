@@ -502,7 +502,11 @@ std::tuple<at::Tensor, at::Tensor> upload_table(
   std::memcpy(cpu.data_ptr(), data, nbytes);
   const bool capturing = current_stream_capturing();
   at::Tensor dev_t;
-  if (host.has_value()) {
+  // Only a capture writes into the slot's persistent device twin.  An eager
+  // upload gets a fresh stream-ordered allocation: the caller may launch the
+  // table on another stream (it record_stream()s it at each launch), and a
+  // recycled twin could be rewritten while such a launch is still queued.
+  if (host.has_value() && capturing) {
     std::lock_guard<std::mutex> lk(g_slot_mu);
     auto it = g_slot_dev.find(host->data_ptr());
     if (it != g_slot_dev.end() && it->second.numel() >= std::max<int64_t>(nbytes, 1) &&
@@ -540,6 +544,20 @@ void register_table_slot(const at::Tensor& host, const at::Tensor& dev) {
               "register_table_slot: pinned byte host slot and a device byte buffer as large");
   std::lock_guard<std::mutex> lk(g_slot_mu);
   g_slot_dev[host.data_ptr()] = dev;
+}
+
+// Diagnostics (tools/graph_oop_audit.py): fill a raw device byte range that
+// the caching allocator holds but has not handed out, to find graph nodes
+// that read memory their graph does not own.
+void memset_raw(int64_t addr, int64_t nbytes, int64_t value) {
+  TORCH_CHECK(addr != 0 && nbytes >= 0, "memset_raw: bad range");
+  C10_HIP_CHECK(hipMemsetAsync(reinterpret_cast<void*>(addr), static_cast<int>(value),
+                               static_cast<size_t>(nbytes), cur_stream()));
+}
+
+void unregister_table_slot(const at::Tensor& host) {
+  std::lock_guard<std::mutex> lk(g_slot_mu);
+  g_slot_dev.erase(host.data_ptr());
 }
 
 int64_t flush_table_uploads() {
@@ -1202,5 +1220,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("eigh_twostage_max_n", &eigh_twostage_max_n);
   m.def("flush_table_uploads", &flush_table_uploads);
   m.def("register_table_slot", &register_table_slot);
+  m.def("memset_raw", &memset_raw);
+  m.def("unregister_table_slot", &unregister_table_slot);
   m.attr("arch") = "gfx950";
 }

@@ -28,6 +28,7 @@ from torch import nn
 
 from distributed_kfac_pytorch_amd.ops._native import native
 from distributed_kfac_pytorch_amd.ops.precondition import _TableCache
+from distributed_kfac_pytorch_amd.ops.precondition import _used_here
 
 _ALIGN = 8  # elements: 16-B aligned bf16 segments, 32-B fp32
 
@@ -65,7 +66,7 @@ class _Caster:
             tab, blocks, host = lib.build_cast_table(srcs, outs, slots[0])
             ent = self._cache.put(key, (tab, blocks, host), slots)
         tab, blocks, _ = ent
-        lib.cast_multi(tab, len(srcs), blocks, dtype == torch.bfloat16)
+        lib.cast_multi(_used_here(tab), len(srcs), blocks, dtype == torch.bfloat16)
         return outs
 
 

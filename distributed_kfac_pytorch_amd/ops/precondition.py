@@ -134,6 +134,18 @@ def apply_grad_(
         wgrad.copy_(src.reshape(rows, -1).reshape(wgrad.shape))
 
 
+def _used_here(tab: torch.Tensor) -> torch.Tensor:
+    """Mark an eagerly uploaded descriptor table as used by the current
+    stream before a launch reads it, so the caching allocator does not hand
+    its block to another stream's allocation while that launch is queued
+    (a table may be uploaded on one stream and launched on another, e.g. the
+    precondition GEMMs issued from the early side stream).  Tables built
+    during a capture live in persistent device slots and need no marking."""
+    if tab.is_cuda and not torch.cuda.is_current_stream_capturing():
+        tab.record_stream(torch.cuda.current_stream(tab.device))
+    return tab
+
+
 class _TableCache:
     """Small LRU of device descriptor tables keyed by operand addresses,
     with the pinned host staging buffers they are uploaded from.
@@ -172,6 +184,17 @@ class _TableCache:
         self._pins: dict = {}
         # device twins of the staging slots (kept alive here)
         self._dev_slots: list[torch.Tensor] = []
+        self._slot_hosts: list[torch.Tensor] = []
+
+    def __del__(self) -> None:
+        # drop the native slot registry's references to this cache's twins
+        try:
+            lib = native()
+            if lib is not None and hasattr(lib, 'unregister_table_slot'):
+                for h in self._slot_hosts:
+                    lib.unregister_table_slot(h)
+        except Exception:  # noqa: BLE001  (interpreter shutdown)
+            pass
 
     @staticmethod
     def _capturing() -> bool:
@@ -239,6 +262,7 @@ class _TableCache:
                                       device=torch.device('cuda', torch.cuda.current_device()))
                     lib.register_table_slot(host, dev)
                     self._dev_slots.append(dev)
+                    self._slot_hosts.append(host)
                 self._free.append(host)
         out: list[torch.Tensor | None] = []
         for _ in range(self.per):
@@ -376,6 +400,7 @@ class MultiLayerApply:
         scale is finalised from the global sum -- one scalar collective for
         the whole model."""
         lib = native()
+        _used_here(self._table)
         if not with_kl:
             lib.apply_multi(self._table, self._n, self._blocks, None)
             return
@@ -587,7 +612,7 @@ class GroupedPrecondition:
         for entry in self._tables:
             if entry is not None:
                 tab, n, tiles, akc, bkc, _ = entry
-                lib.gemm3_grouped(tab, n, tiles, akc, bkc)
+                lib.gemm3_grouped(_used_here(tab), n, tiles, akc, bkc)
 
     def run(self, layers: list, damping: float) -> bool:
         """prepare + launch; sets each layer's ``grad`` to its buffer."""
@@ -750,10 +775,10 @@ class SplitGroupedPrecondition(GroupedPrecondition):
         for entry in self._tables:
             if entry[0] == 'split':
                 _, tab, n, blocks, _ = entry
-                lib.split_pad_multi(tab, n, blocks)
+                lib.split_pad_multi(_used_here(tab), n, blocks)
             else:
                 _, tab, n, tiles, (amc, bmc, osplit), _ = entry
-                lib.gemm3s_grouped(tab, n, tiles, amc, bmc, osplit)
+                lib.gemm3s_grouped(_used_here(tab), n, tiles, amc, bmc, osplit)
 
 
 def grouped_gemm_mode() -> str:
