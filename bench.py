@@ -260,7 +260,7 @@ def run(args: argparse.Namespace, use_kfac: bool, rank: int, world: int,
 
     runner = None
     if use_graphs:
-        runner = GraphedTrainStep(forward_backward, opt, precond)
+        runner = GraphedTrainStep(forward_backward, opt, precond, model=model)
 
     def step() -> None:
         next_batch()

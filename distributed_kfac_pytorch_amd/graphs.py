@@ -82,6 +82,19 @@ def _no_gc() -> Iterator[None]:
         if was:
             gc.enable()
 
+def _graph_safe(model: torch.nn.Module | None, preconditioner: Any) -> int:
+    from distributed_kfac_pytorch_amd.ops.conv import StridedConv1x1
+    from distributed_kfac_pytorch_amd.ops.conv import is_strided_1x1
+    from distributed_kfac_pytorch_amd.ops.conv import make_graph_safe
+
+    n = make_graph_safe(model) if model is not None else 0
+    for module in list(getattr(preconditioner, '_layers', None) or {}):
+        if type(module) is torch.nn.Conv2d and is_strided_1x1(module):
+            module.__class__ = StridedConv1x1
+            n += 1
+    return n
+
+
 class GraphedTrainStep:
     """Run (and graph-capture) a full training step.
 
@@ -96,6 +109,9 @@ class GraphedTrainStep:
             before the graphs are captured.
         enabled: force graphs on / off (default: on when CUDA is available
             and the job has a single rank).
+        model: the trained module; its strided 1x1 convolutions are switched
+            to the graph-safe formulation of ``ops.conv`` (same parameters
+            and values).  Without it only K-FAC's registered layers are.
     """
 
     def __init__(
@@ -107,6 +123,7 @@ class GraphedTrainStep:
         warmup: int = 1,
         enabled: bool | None = None,
         kinds: tuple[str, ...] = ('plain',),
+        model: torch.nn.Module | None = None,
     ) -> None:
         self.forward_backward = forward_backward
         self.optimizer = optimizer
@@ -118,6 +135,11 @@ class GraphedTrainStep:
                 not multi or os.environ.get('KFAC_STEP_GRAPHS_MULTI', '0') == '1'
             )
         self.enabled = enabled
+        if enabled:
+            # strided 1x1 convolutions through the graph-safe formulation
+            # (MIOpen's own backward-data of them reads memory outside the
+            # graph: ops/conv.py); the model's, or at least K-FAC's layers'
+            _graph_safe(model, preconditioner)
         # Step kinds replayed from graphs.  Factor-update steps stay eager by
         # default: their SYRKs run on the factor side stream concurrently with
         # backward, and a replayed graph executes its nodes in one queue, so

@@ -20,6 +20,7 @@ import torch
 import torch.nn as nn
 
 from distributed_kfac_pytorch_amd.ops.bnact import BatchNormAct2d
+from distributed_kfac_pytorch_amd.ops.conv import StridedConv1x1
 
 __all__ = [
     'Bottleneck',
@@ -39,7 +40,11 @@ def _conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
 
 
 def _conv1x1(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
-    return nn.Conv2d(cin, cout, 1, stride=stride, bias=False)
+    # strided projection shortcuts: subsample + stride-1 conv, same module
+    # attributes and values (MIOpen's strided 1x1 backward-data is not
+    # HIP-graph safe: ops/conv.py)
+    cls = StridedConv1x1 if stride != 1 else nn.Conv2d
+    return cls(cin, cout, 1, stride=stride, bias=False)
 
 
 def _shortcut(ds: nn.Module | None, x: torch.Tensor) -> torch.Tensor:

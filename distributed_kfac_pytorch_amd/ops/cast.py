@@ -155,7 +155,7 @@ class FusedWeightCast:
         self.device_type = device_type
         self.mods: list[nn.Module] = []
         for m in model.modules():
-            if type(m) in (nn.Conv2d, nn.Linear) and m.weight.dtype == torch.float32:
+            if isinstance(m, (nn.Conv2d, nn.Linear)) and m.weight.dtype == torch.float32:
                 self.mods.append(m)
         for m in self.mods:
             m.forward = (_conv_forward if isinstance(m, nn.Conv2d) else _linear_forward).__get__(m)

@@ -1,0 +1,73 @@
+"""Graph-safe strided 1x1 convolutions.
+
+Root cause of the whole-step graph corruption of rounds 2-3
+(``profiles/graph_replay_r3_investigation.txt``; found with
+``tools/graph_oop_audit.py`` / ``tools/graph_oop_bisect.py``, evidence in
+``profiles/graph_oop_r4.md``): on MI355X, the HIP graph of MIOpen's
+backward-data of a 1x1 convolution with stride 2 (ResNet's projection
+shortcuts ``layer{2,3,4}.0.downsample.0``; fp32 and bf16, NHWC; a HIP memset
+of ``dX`` followed by a composable-kernel ``grouped_conv_bwd_data`` launch)
+reads device memory that neither the graph's private pool nor any live
+tensor owns -- free blocks of the caching allocator's global pool.  Replays
+are then correct only while nothing else writes those blocks: a second
+model's eager steps, an eval pass or the K-FAC refresh step reuse them and
+the shortcut's ``dX`` -- and every gradient upstream of it -- turns into
+garbage or NaN.  Each of ResNet-50's 53 convolutions was captured alone and
+replayed after every free global block was filled with 0xFF: only these
+three changed, only in ``dX``, in fp32 and in bf16.
+
+``StridedConv1x1`` computes the same convolution as a stride-1 1x1
+convolution of the subsampled input, ``conv(x[:, :, ::s, ::s])``: identical
+forward values, and a backward made of a stride-1 1x1 convolution (a GEMM in
+MIOpen, graph-safe) plus the slice's scatter into a zero ``dX``.  The module
+keeps ``stride == (s, s)``, its parameters and its state-dict keys, so K-FAC
+sees exactly the layer it saw before (its hooks read the full-resolution
+input and the module's stride) and checkpoints are unchanged.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+__all__ = ['StridedConv1x1', 'make_graph_safe', 'is_strided_1x1']
+
+
+def is_strided_1x1(m: nn.Module) -> bool:
+    """A 1x1, unpadded, undilated ``nn.Conv2d`` with a stride > 1."""
+    return (
+        isinstance(m, nn.Conv2d)
+        and tuple(m.kernel_size) == (1, 1)
+        and tuple(m.stride) != (1, 1)
+        and m.padding in (0, (0, 0))
+        and tuple(m.dilation) == (1, 1)
+        and m.padding_mode == 'zeros'
+    )
+
+
+class StridedConv1x1(nn.Conv2d):
+    """``nn.Conv2d`` (1x1, stride > 1) evaluated as subsample + stride-1
+    conv (see the module docstring)."""
+
+    def _conv_forward(  # type: ignore[override]
+        self,
+        input: torch.Tensor,
+        weight: torch.Tensor,
+        bias: torch.Tensor | None,
+    ) -> torch.Tensor:
+        sh, sw = self.stride
+        sub = input[:, :, ::sh, ::sw]
+        if input.is_contiguous(memory_format=torch.channels_last):
+            sub = sub.contiguous(memory_format=torch.channels_last)
+        return F.conv2d(sub, weight, bias, 1, 0, 1, self.groups)
+
+
+def make_graph_safe(model: nn.Module) -> int:
+    """Switch every strided 1x1 ``nn.Conv2d`` of ``model`` (in place, same
+    parameters) to ``StridedConv1x1``.  Returns the number switched."""
+    n = 0
+    for m in model.modules():
+        if type(m) is nn.Conv2d and is_strided_1x1(m):
+            m.__class__ = StridedConv1x1
+            n += 1
+    return n

@@ -17,6 +17,7 @@ import os
 import sys
 
 import torch
+from torch import nn
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
@@ -30,6 +31,18 @@ _FUSED_SGD = False
 _CL = True
 _IMG = 64
 _BATCH = 8
+_NC = 10
+_INV = 8
+_LR = 0.01
+_POOL = 4
+
+
+def unsafe(model: nn.Module) -> None:
+    """Undo ops/conv.py: plain nn.Conv2d strided 1x1 shortcuts."""
+    from distributed_kfac_pytorch_amd.ops.conv import StridedConv1x1
+    for mm in model.modules():
+        if type(mm) is StridedConv1x1:
+            mm.__class__ = nn.Conv2d
 
 
 def build(base, dev, graphs: bool, amp: bool, fused_cast: bool, warmup: int = 1,
@@ -39,10 +52,10 @@ def build(base, dev, graphs: bool, amp: bool, fused_cast: bool, warmup: int = 1,
         model = model.to(memory_format=torch.channels_last)
     if fused_cast and amp:
         enable_fused_weight_cast(model)
-    opt = torch.optim.SGD(model.parameters(), lr=0.01, momentum=0.9, weight_decay=5e-5,
+    opt = torch.optim.SGD(model.parameters(), lr=_LR, momentum=0.9, weight_decay=5e-5,
                           **({'fused': True} if _FUSED_SGD else {}))
     pre = kfac.KFACPreconditioner(
-        model, factor_update_steps=factor_steps, inv_update_steps=8, damping=0.001,
+        model, factor_update_steps=factor_steps, inv_update_steps=_INV, damping=0.001,
         kl_clip=0.001, lr=lambda s: opt.param_groups[0]['lr'],
         grad_worker_fraction=0.5) if kfac_on else None
     x = torch.empty(_BATCH, 3, _IMG, _IMG, device=dev).contiguous(
@@ -114,8 +127,15 @@ def main() -> None:
                     help='graphs: A = GraphedTrainStep, B = eager; stepgraphs: A = eager '
                          'with StepGraphs, B = eager without (both eager)')
     ap.add_argument('--image', type=int, default=64)
+    ap.add_argument('--num-classes', type=int, default=10)
+    ap.add_argument('--inv-steps', type=int, default=8)
+    ap.add_argument('--lr', type=float, default=0.01)
+    ap.add_argument('--pool', type=int, default=4)
+    ap.add_argument('--print-every', type=int, default=1)
     ap.add_argument('--batch', type=int, default=8)
     ap.add_argument('--fused-sgd', type=int, default=0)
+    ap.add_argument('--graph-safe', type=int, default=1,
+                    help='0: plain nn.Conv2d for the strided 1x1 shortcuts (reproduces the bug)')
     ap.add_argument('--channels-last', type=int, default=1)
     ap.add_argument('--sequential', action='store_true',
                     help='run the graph model through all steps first (CPU snapshots), '
@@ -123,12 +143,15 @@ def main() -> None:
     args = ap.parse_args()
     torch.backends.cudnn.deterministic = bool(args.deterministic)
     torch.backends.cudnn.benchmark = bool(args.benchmark)
-    global _FUSED_SGD, _CL, _IMG, _BATCH
+    global _FUSED_SGD, _CL, _IMG, _BATCH, _NC, _INV, _LR, _POOL
+    _NC, _INV, _LR, _POOL = args.num_classes, args.inv_steps, args.lr, args.pool
     _FUSED_SGD, _CL = bool(args.fused_sgd), bool(args.channels_last)
     _IMG, _BATCH = args.image, args.batch
     dev = torch.device('cuda')
     torch.manual_seed(0)
-    base = resnet50(num_classes=10)
+    base = resnet50(num_classes=_NC)
+    if not args.graph_safe:
+        unsafe(base)
     if args.sequential:
         sequential(base, dev, args)
         return
@@ -140,7 +163,7 @@ def main() -> None:
         B[2]._graphs = None  # the eager twin never replays precondition graphs
     gen = torch.Generator(device='cpu').manual_seed(1)
     pool = [(torch.randn(_BATCH, 3, _IMG, _IMG, generator=gen),
-             torch.randint(0, 10, (_BATCH,), generator=gen)) for _ in range(4)]
+             torch.randint(0, _NC, (_BATCH,), generator=gen)) for _ in range(_POOL)]
     env = {k: v for k, v in os.environ.items() if k.startswith('KFAC_')}
     for i in range(args.steps):
         kind = A[5].kind() if hasattr(A[5], 'kind') else '-'
@@ -175,7 +198,10 @@ def main() -> None:
             diffs = [float((a.float() - b.float()).abs().max() / b.float().abs().max().clamp_min(1e-30))
                      for a, b in zip(sa[k], sb[k]) if a.shape == b.shape]
             rec[k] = {'nonfinite': bad, 'n': len(sa[k]), 'maxrel': max(diffs) if diffs else None}
-        print(json.dumps(rec), flush=True)
+        bad_now = any(rec[k]['nonfinite'] for k in sa) or any(
+            (rec[k]['maxrel'] or 0.0) > 0.0 for k in ('param', 'grad'))
+        if bad_now or i % args.print_every == 0 or i == args.steps - 1:
+            print(json.dumps(rec), flush=True)
         if any(rec[k]['nonfinite'] for k in sa):
             break
 
@@ -183,7 +209,7 @@ def main() -> None:
 def sequential(base, dev, args) -> None:  # type: ignore[no-untyped-def]
     gen = torch.Generator(device='cpu').manual_seed(1)
     pool = [(torch.randn(_BATCH, 3, _IMG, _IMG, generator=gen),
-             torch.randint(0, 10, (_BATCH,), generator=gen)) for _ in range(4)]
+             torch.randint(0, _NC, (_BATCH,), generator=gen)) for _ in range(_POOL)]
     snaps = []
     for graphs in (True, False):
         m = build(base, dev, graphs, not args.fp32, bool(args.fused_cast), args.warmup,

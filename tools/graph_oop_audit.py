@@ -29,6 +29,7 @@ import os
 import sys
 
 import torch
+from torch import nn
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
@@ -40,6 +41,14 @@ from distributed_kfac_pytorch_amd.ops.cast import enable_fused_weight_cast  # no
 
 _S0 = 7777 * 512  # sentinel allocation sizes marking the capture window
 _S1 = 7779 * 512
+
+
+def unsafe(model: nn.Module) -> None:
+    """Undo ops/conv.py: plain nn.Conv2d strided 1x1 shortcuts."""
+    from distributed_kfac_pytorch_amd.ops.conv import StridedConv1x1
+    for mm in model.modules():
+        if type(mm) is StridedConv1x1:
+            mm.__class__ = nn.Conv2d
 
 
 def _frames(fr: list, n: int = 8) -> list[str]:
@@ -57,6 +66,8 @@ def _frames(fr: list, n: int = 8) -> list[str]:
 def build(args: argparse.Namespace, dev: torch.device):  # type: ignore[no-untyped-def]
     torch.manual_seed(0)
     model = get_model('resnet50').to(dev).to(memory_format=torch.channels_last)
+    if not args.graph_safe:
+        unsafe(model)
     amp = args.bf16
     if amp and args.fused_cast:
         enable_fused_weight_cast(model)
@@ -105,6 +116,8 @@ def main() -> None:
     ap.add_argument('--inv-steps', type=int, default=100)
     ap.add_argument('--steps', type=int, default=4, help='steps before the audit (>= capture)')
     ap.add_argument('--max-report', type=int, default=40)
+    ap.add_argument('--graph-safe', type=int, default=1,
+                    help='0: plain nn.Conv2d for the strided 1x1 shortcuts (reproduces the bug)')
     args = ap.parse_args()
     torch.backends.cudnn.deterministic = True
     torch.backends.cudnn.benchmark = False

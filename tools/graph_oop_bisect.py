@@ -17,12 +17,27 @@ import json
 import os
 import sys
 
+if '--miopen-db' in sys.argv:
+    # the tuned MIOpen database bench.py uses (must be set before MIOpen
+    # initialises)
+    os.environ.setdefault('MIOPEN_USER_DB_PATH', os.path.join(
+        os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'miopen_db'))
+
 import torch
+from torch import nn
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from distributed_kfac_pytorch_amd.models.resnet import get_model  # noqa: E402
 from distributed_kfac_pytorch_amd.ops import _native  # noqa: E402
+
+
+def unsafe(model: nn.Module) -> None:
+    """Undo ops/conv.py: plain nn.Conv2d strided 1x1 shortcuts."""
+    from distributed_kfac_pytorch_amd.ops.conv import StridedConv1x1
+    for mm in model.modules():
+        if type(mm) is StridedConv1x1:
+            mm.__class__ = nn.Conv2d
 
 
 def free_global_blocks() -> list[tuple[int, int]]:
@@ -47,17 +62,23 @@ def main() -> None:
     ap.add_argument('--stages', default='conv1,conv1_bwd,stem,layer1,fwd,loss,fwd_bwd,full')
     ap.add_argument('--eager-steps', type=int, default=1)
     ap.add_argument('--stages-quiet', type=int, default=0, help='print only failing stages')
+    ap.add_argument('--miopen-db', action='store_true', help="use the repo's tuned MIOpen db")
+    ap.add_argument('--deterministic', type=int, default=1)
     ap.add_argument('--fused-bn', type=int, default=1)
+    ap.add_argument('--graph-safe', type=int, default=1,
+                    help='0: plain nn.Conv2d for the strided 1x1 shortcuts (reproduces the bug)')
     args = ap.parse_args()
     if not args.fused_bn:
         os.environ['KFAC_FUSED_BN'] = '0'
-    torch.backends.cudnn.deterministic = True
+    torch.backends.cudnn.deterministic = bool(args.deterministic)
     torch.backends.cudnn.benchmark = False
     dev = torch.device('cuda', 0)
     lib = _native.native()
     assert lib is not None and hasattr(lib, 'memset_raw'), _native.load_error()
     torch.manual_seed(0)
     model = get_model('resnet50').to(dev).to(memory_format=torch.channels_last)
+    if not args.graph_safe:
+        unsafe(model)
     opt = torch.optim.SGD(model.parameters(), lr=0.0125, momentum=0.9, weight_decay=5e-5,
                           fused=True)
     x = torch.randn(args.batch, 3, args.image, args.image, device=dev).contiguous(
@@ -159,9 +180,12 @@ def main() -> None:
 
     # every conv on its own: backward data + weight from a fixed input
     conv_in: dict = {}
-    hooks = [mm.register_forward_hook(
-        lambda mod, inp, out, nm=nm: conv_in.setdefault(nm, tuple(inp[0].shape)))
-        for nm, mm in m.named_modules() if isinstance(mm, torch.nn.Conv2d)]
+    def rec(nm: str):  # type: ignore[no-untyped-def]
+        def hook(mod, inp, out) -> None:  # type: ignore[no-untyped-def]
+            conv_in.setdefault(nm, tuple(inp[0].shape))
+        return hook
+    hooks = [mm.register_forward_hook(rec(nm))
+             for nm, mm in m.named_modules() if isinstance(mm, torch.nn.Conv2d)]
     with torch.no_grad(), ac():
         m(x)
     for h in hooks:
