@@ -23,6 +23,7 @@ ms/step(K-FAC) - ms/step(SGD) is reported alongside.
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -53,6 +54,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import distributed_kfac_pytorch_amd as kfac  # noqa: E402
 from distributed_kfac_pytorch_amd import tracing  # noqa: E402
 from distributed_kfac_pytorch_amd.graphs import GraphedTrainStep  # noqa: E402
+from distributed_kfac_pytorch_amd.graphs import step_stream  # noqa: E402
 from distributed_kfac_pytorch_amd.models.resnet import get_model  # noqa: E402
 from distributed_kfac_pytorch_amd.ops.cast import enable_fused_weight_cast  # noqa: E402
 
@@ -133,6 +135,10 @@ def parse_args() -> argparse.Namespace:
                         'establish the MI355X baseline')
     p.add_argument('--backend', default='nccl',
                    help='torch.distributed backend (nccl = RCCL)')
+    p.add_argument('--ddp', type=int, default=0,
+                   help='1: wrap the model in DistributedDataParallel even at world 1 '
+                        '(launch under torchrun: exercises RCCL init, the DDP reducer and '
+                        'its capture inside the step graphs on a 1-GPU box)')
     p.add_argument('--same-device', action='store_true',
                    help='put every rank on cuda:0 (multi-rank rehearsal on a '
                         '1-GPU box; use with --backend gloo)')
@@ -146,7 +152,7 @@ def setup(args: argparse.Namespace) -> tuple[int, int, torch.device]:
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
     torch.backends.cudnn.benchmark = bool(args.cudnn_benchmark)
-    if world > 1:
+    if world > 1 or args.ddp:
         if args.backend == 'nccl':
             dist.init_process_group('nccl', device_id=dev)
         else:
@@ -187,10 +193,18 @@ def run(args: argparse.Namespace, use_kfac: bool, rank: int, world: int,
         # bf16 weight copies / fp32 weight gradients by multi-tensor launches
         # instead of autocast's per-weight casts (ops/cast.py)
         enable_fused_weight_cast(model)
-    if world > 1:
-        model = torch.nn.parallel.DistributedDataParallel(
-            model, device_ids=[dev.index], gradient_as_bucket_view=True,
-        )
+    use_graphs = bool(args.graphs) and args.impl == 'native' and (
+        world == 1 or os.environ.get('KFAC_STEP_GRAPHS_MULTI', '0') == '1')
+    if amp and not args.graphs_bf16:
+        use_graphs = False
+    if world > 1 or args.ddp:
+        # under graphs DDP is built on the stream the steps run and are
+        # captured on (its reducer holds the AccumulateGrad nodes)
+        ctx = torch.cuda.stream(step_stream(dev)) if use_graphs else contextlib.nullcontext()
+        with ctx:
+            model = torch.nn.parallel.DistributedDataParallel(
+                model, device_ids=[dev.index], gradient_as_bucket_view=True,
+            )
     lr = args.lr * world
     # fused: one-pass SGD kernels (weight decay + momentum + update per
     # element); foreach: PyTorch's multi-pass multi-tensor SGD
@@ -239,16 +253,6 @@ def run(args: argparse.Namespace, use_kfac: bool, rank: int, world: int,
         y.copy_(pool_y[i])
     crit = torch.nn.CrossEntropyLoss(label_smoothing=0.1)
 
-    use_graphs = bool(args.graphs) and args.impl == 'native' and world == 1
-    if amp and not args.graphs_bf16:
-        # bf16 autocast runs eager: whole-step replays of the bf16 K-FAC step
-        # went non-finite 1-13 steps after the step-100 refresh in round-3
-        # bench runs (profiles/graph_replay_r3_investigation.txt: with or
-        # without the fused casts, the fused BN, the factor side stream, a
-        # sync after the refresh), while
-        # eager bf16 and the fp32 replays (bit-exact vs eager in
-        # tests/test_graphs_refresh_gpu.py) stayed finite
-        use_graphs = False
 
     def forward_backward() -> torch.Tensor:
         # no autocast weight cache: it cannot be replayed from a graph
@@ -493,7 +497,7 @@ def main() -> None:
             line[k] = res[k]
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 

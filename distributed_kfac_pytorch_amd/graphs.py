@@ -82,6 +82,27 @@ def _no_gc() -> Iterator[None]:
         if was:
             gc.enable()
 
+_STEP_STREAMS: dict = {}
+
+
+def step_stream(device: torch.device | int | None = None) -> torch.cuda.Stream:
+    """The per-device stream ``GraphedTrainStep`` runs steps and captures on
+    by default.  Construct a ``DistributedDataParallel`` model under it
+    (``with torch.cuda.stream(step_stream()):``) when its steps will be
+    graph-captured."""
+    if device is None:
+        dev = torch.cuda.current_device()
+    elif isinstance(device, int):
+        dev = device
+    else:
+        dev = device.index if device.index is not None else torch.cuda.current_device()
+    s = _STEP_STREAMS.get(dev)
+    if s is None:
+        s = torch.cuda.Stream(device=dev)
+        _STEP_STREAMS[dev] = s
+    return s
+
+
 def _graph_safe(model: torch.nn.Module | None, preconditioner: Any) -> int:
     from distributed_kfac_pytorch_amd.ops.conv import StridedConv1x1
     from distributed_kfac_pytorch_amd.ops.conv import is_strided_1x1
@@ -112,6 +133,16 @@ class GraphedTrainStep:
         model: the trained module; its strided 1x1 convolutions are switched
             to the graph-safe formulation of ``ops.conv`` (same parameters
             and values).  Without it only K-FAC's registered layers are.
+        stream: the HIP stream every step -- eager or replayed -- and every
+            capture runs on (default: a private stream; the caller's stream
+            is joined on entry and exit).  One stream for all of them keeps
+            the autograd engine's AccumulateGrad nodes on the stream that
+            produces the gradients.  A ``DistributedDataParallel`` model must
+            be CONSTRUCTED under it (``with torch.cuda.stream(step.stream)``,
+            or ``step_stream()`` before building the runner): DDP's reducer
+            holds every parameter's AccumulateGrad node from construction
+            on, and nodes bound to another stream make the captured backward
+            synchronise with a stream outside the capture.
     """
 
     def __init__(
@@ -124,6 +155,7 @@ class GraphedTrainStep:
         enabled: bool | None = None,
         kinds: tuple[str, ...] = ('plain',),
         model: torch.nn.Module | None = None,
+        stream: torch.cuda.Stream | None = None,
     ) -> None:
         self.forward_backward = forward_backward
         self.optimizer = optimizer
@@ -135,6 +167,9 @@ class GraphedTrainStep:
                 not multi or os.environ.get('KFAC_STEP_GRAPHS_MULTI', '0') == '1'
             )
         self.enabled = enabled
+        self.stream = stream
+        if enabled and self.stream is None:
+            self.stream = step_stream()
         if enabled:
             # strided 1x1 convolutions through the graph-safe formulation
             # (MIOpen's own backward-data of them reads memory outside the
@@ -250,8 +285,9 @@ class GraphedTrainStep:
                 return
             p._steps = at
         g = torch.cuda.CUDAGraph()
-        side = torch.cuda.Stream()
-        side.wait_stream(torch.cuda.current_stream())
+        side = self.stream if self.stream is not None else torch.cuda.Stream()
+        if side != torch.cuda.current_stream():
+            side.wait_stream(torch.cuda.current_stream())
         # Gradients are dropped before the capture, so the captured backward
         # writes them directly (autograd hands over its buffer, no
         # zero + accumulate kernels: ~160 fewer launches and 0.8 ms per
@@ -272,7 +308,8 @@ class GraphedTrainStep:
                 if p is not None:
                     p.step()
                 self.optimizer.step()
-        torch.cuda.current_stream().wait_stream(side)
+        if side != torch.cuda.current_stream():
+            torch.cuda.current_stream().wait_stream(side)
         # descriptor tables built during the capture: one eager upload now
         _native.flush_table_uploads()
         if p is not None:
@@ -301,6 +338,18 @@ class GraphedTrainStep:
 
     # --------------------------------------------------------------- step
     def __call__(self) -> torch.Tensor:
+        if not self.enabled or self.stream is None:
+            return self._call()
+        caller = torch.cuda.current_stream()
+        if caller == self.stream:
+            return self._call()
+        self.stream.wait_stream(caller)
+        with torch.cuda.stream(self.stream):
+            out = self._call()
+        caller.wait_stream(self.stream)
+        return out
+
+    def _call(self) -> torch.Tensor:
         kind = self.kind()
         if not self.enabled or kind == 'inverse':
             loss = self._eager()

@@ -249,8 +249,11 @@ class KFACPreconditioner(BaseKFACPreconditioner):
         if cost_model not in ('auto', 'flops', 'measured'):
             raise ValueError(f'unknown cost_model {cost_model!r}')
         if cost_model == 'auto':
-            on_gpu = any(p.is_cuda for p in model.parameters())
-            cost_model = 'measured' if (on_gpu and compute_method == ComputeMethod.EIGEN) else 'flops'
+            # the reference's n^3 placement (kfac/preconditioner.py:266-281);
+            # the latency model of parallel/costmodel.py stays opt-in
+            # ('measured') until its table is regenerated on the GPU with the
+            # current solver tiers (profiles/solver_table_mi355x.json)
+            cost_model = 'flops'
         self.cost_model = cost_model
         if assignment_strategy == AssignmentStrategy.COMPUTE and cost_model == 'measured':
             from distributed_kfac_pytorch_amd.parallel.costmodel import solver_ms as cost

@@ -1,25 +1,23 @@
-"""Whole-step HIP graphs across eigen refreshes at production shape.
+"""Whole-step HIP graphs at the bench configuration, interleaved with a
+foreign model's eager steps, across eigen refreshes.
 
-Round 2 found that ``GraphedTrainStep`` replays after an eager second-order
-refresh produced NaN in every K-FAC layer on the ResNet-50 bench config
-(profiles/graph_replay_nonfinite_r2.txt), while the toy-model parity test
-(tests/test_graphs.py) passed.  The cause: the runner kept the captured
-loss -- and through its autograd graph every parameter's AccumulateGrad
-node, bound to the capture's side stream -- alive, so the eager refresh
-step accumulated its gradients on that foreign stream from buffers the
-producing stream had already recycled.
+Rounds 2-3 saw ``GraphedTrainStep`` replays go wrong as soon as other eager
+work ran between them: a second model's steps (fp32 and bf16, with or
+without K-FAC) or the K-FAC refresh step (bf16 bench runs went non-finite a
+few steps after the step-100 refresh;
+profiles/graph_replay_r3_investigation.txt).  The cause was MIOpen's
+backward-data of the strided 1x1 projection convolutions, whose graph reads
+free memory of the caching allocator's global pool (ops/conv.py,
+profiles/graph_oop_r4.md); ``GraphedTrainStep`` now runs those convolutions
+through the graph-safe ``StridedConv1x1``.
 
-This test runs the configuration that failed: ResNet-50 (every eigensolver
-tier: n <= 128 Jacobi, mid sizes, 2304 / 4608 large-n factors), fused BN,
-bf16 autocast, channels_last, fused weight casts and the factor side stream,
-with three refreshes inside the replay window.  The graph run goes first
-(parameters checked for finiteness after every step, snapshots after each
-refresh), then an eager twin from the same weights and data; with
-deterministic MIOpen the two agree to the bit (round 3).  The twin runs
-AFTER the graph run: interleaving a second model's eager steps between
-replays perturbed the replays (profiles/graph_replay_r3_investigation.txt),
-while runs with no foreign work between replays -- eager factor / refresh
-steps of the same model included -- matched exactly.
+This test is the failing pattern itself: the graphed model and an eager
+twin from the same weights are stepped ALTERNATELY in one process (each
+one's eager work lands between the other's replays), at the bench shape
+(ResNet-50, 224x224, batch 32, fused SGD, channels_last, fused BN, fused
+weight casts in bf16), with refreshes inside the replay window.  With
+deterministic MIOpen every replayed step must equal the eager twin's to the
+bit, and parameters must stay finite.
 """
 from __future__ import annotations
 
@@ -36,77 +34,78 @@ from distributed_kfac_pytorch_amd.ops.cast import enable_fused_weight_cast
 pytestmark = pytest.mark.gpu
 
 
-def _build(base: torch.nn.Module, cuda: torch.device, graphs: bool, kinds=('plain',)):
+def _build(base: torch.nn.Module, cuda: torch.device, graphs: bool, amp: bool,
+           use_kfac: bool, kinds=('plain',)):
     model = copy.deepcopy(base).to(cuda).to(memory_format=torch.channels_last)
-    enable_fused_weight_cast(model)
-    opt = torch.optim.SGD(model.parameters(), lr=0.01, momentum=0.9, weight_decay=5e-5)
+    if amp:
+        enable_fused_weight_cast(model)
+    opt = torch.optim.SGD(model.parameters(), lr=0.0125, momentum=0.9, weight_decay=5e-5,
+                          fused=True)
     pre = kfac.KFACPreconditioner(
         model, factor_update_steps=2, inv_update_steps=8, damping=0.001,
         kl_clip=0.001, lr=lambda s: opt.param_groups[0]['lr'],
         grad_worker_fraction=0.5,
-    )
-    x = torch.empty(8, 3, 64, 64, device=cuda).contiguous(memory_format=torch.channels_last)
-    y = torch.empty(8, dtype=torch.long, device=cuda)
+    ) if use_kfac else None
+    x = torch.empty(32, 3, 224, 224, device=cuda).contiguous(memory_format=torch.channels_last)
+    y = torch.empty(32, dtype=torch.long, device=cuda)
     crit = torch.nn.CrossEntropyLoss(label_smoothing=0.1)
 
     def fb() -> torch.Tensor:
-        with torch.autocast('cuda', dtype=torch.bfloat16, cache_enabled=not graphs):
+        with torch.autocast('cuda', dtype=torch.bfloat16, enabled=amp, cache_enabled=False):
             loss = crit(model(x), y)
         loss.backward()
         return loss
 
     if graphs:
-        runner = GraphedTrainStep(fb, opt, pre, warmup=1, enabled=True, kinds=kinds)
+        runner = GraphedTrainStep(fb, opt, pre, warmup=1, enabled=True, kinds=kinds, model=model)
     else:
         def runner() -> torch.Tensor:
             opt.zero_grad(set_to_none=False)
             loss = fb()
-            pre.step()
+            if pre is not None:
+                pre.step()
             opt.step()
             return loss.detach()
     return model, pre, x, y, runner
 
 
-@pytest.mark.parametrize('kinds', [('plain',), ('plain', 'factor')])
-def test_graph_replay_matches_eager_across_refreshes(cuda, kinds) -> None:
+@pytest.mark.parametrize('amp,use_kfac,kinds', [
+    (True, True, ('plain',)),
+    (False, True, ('plain', 'factor')),
+    (False, False, ('plain',)),
+])
+def test_graph_replay_interleaved_with_eager_twin(cuda, amp, use_kfac, kinds) -> None:
     det = torch.backends.cudnn.deterministic
     torch.backends.cudnn.deterministic = True
     try:
         torch.manual_seed(0)
-        base = resnet50(num_classes=10)
+        base = resnet50()
         gen = torch.Generator(device='cpu').manual_seed(1)
-        pool = [(torch.randn(8, 3, 64, 64, generator=gen),
-                 torch.randint(0, 10, (8,), generator=gen)) for _ in range(4)]
-        steps = 26  # refreshes at steps 0, 8, 16, 24
-        marks = (1, 9, 17, 25)  # the step after each refresh
-        snaps: list[dict] = []
-        for graphs in (True, False):
-            m, pre, xs, ys, run = _build(base, cuda, graphs, kinds)
-            got: dict = {}
-            for i in range(steps):
-                x, y = pool[i % len(pool)]
-                xs.copy_(x)
-                ys.copy_(y)
-                run()
-                if graphs:
-                    torch.cuda.synchronize()
-                    fin = all(bool(torch.isfinite(p).all()) for p in m.parameters())
-                    assert fin, f'non-finite parameters after step {i} (graph replay)'
-                if i in marks:
-                    got[i] = [p.detach().float().cpu() for p in m.parameters()]
-            assert pre.steps == steps
-            if graphs:
-                assert isinstance(run, GraphedTrainStep)
-                assert run.captures == len(kinds), run.captures
-                assert run.replays >= (18 if 'factor' in kinds else 12), run.replays
-                # the captured autograd graphs must not outlive their capture
-                assert all(o.grad_fn is None for o in run.outputs.values())
-            snaps.append(got)
-            del m, pre, run
+        pool = [(torch.randn(32, 3, 224, 224, generator=gen),
+                 torch.randint(0, 1000, (32,), generator=gen)) for _ in range(4)]
+        steps = 18  # K-FAC refreshes at steps 0, 8, 16
+        A = _build(base, cuda, True, amp, use_kfac, kinds)
+        B = _build(base, cuda, False, amp, use_kfac)
+        for i in range(steps):
+            x, y = pool[i % len(pool)]
+            for m in (A, B):
+                m[2].copy_(x)
+                m[3].copy_(y)
+            A[4]()
+            B[4]()  # eager work of another model between A's replays
             torch.cuda.synchronize()
-        for i in marks:
-            num = max(float((a - b).abs().max()) for a, b in zip(snaps[0][i], snaps[1][i]))
-            den = max(float(b.abs().max()) for b in snaps[1][i])
-            assert num <= 1e-3 * den, (i, num / den)
+            pa, pb = list(A[0].parameters()), list(B[0].parameters())
+            assert all(bool(torch.isfinite(p).all()) for p in pa), f'non-finite params at step {i}'
+            bad = [n for (n, _), p, q in zip(A[0].named_parameters(), pa, pb)
+                   if not torch.equal(p, q) or not torch.equal(p.grad, q.grad)]
+            assert not bad, (i, len(bad), bad[:3])
+        run = A[4]
+        assert isinstance(run, GraphedTrainStep)
+        assert run.captures == (len(kinds) if use_kfac else 1), run.captures
+        assert run.replays >= (6 if use_kfac else steps - 2), run.replays
+        if use_kfac:
+            assert A[1].steps == steps
+        # the captured autograd graphs must not outlive their capture
+        assert all(o.grad_fn is None for o in run.outputs.values())
     finally:
         torch.backends.cudnn.deterministic = det

@@ -256,10 +256,20 @@ def main() -> None:
         p = [o.detach().float().cpu() for o in outs if o is not None]
         bad = sum(int(not torch.equal(a, b)) for a, b in zip(c1, p))
         first = next((i for i, (a, b) in enumerate(zip(c1, p)) if not torch.equal(a, b)), None)
-        if args.stages_quiet and not bad and not det:
+
+        def rel(a: torch.Tensor, b: torch.Tensor) -> float:
+            if not bool(torch.isfinite(b).all()):
+                return float('inf')
+            return float((a - b).abs().max() / a.abs().max().clamp_min(1e-30))
+        # atomics-based (non-deterministic) kernels differ run to run at the
+        # 1e-6 level; a read of poisoned (0xFF) memory is far larger
+        noise = max([rel(a, b) for a, b in zip(c1, c2)] or [0.0])
+        gross = [i for i, (a, b) in enumerate(zip(c1, p)) if rel(a, b) > max(1e-3, 100 * noise)]
+        if args.stages_quiet and not gross:
             del g, outs
             continue
         print(json.dumps({'stage': name, 'outputs': len(c1), 'nondet': det,
+                          'noise_rel': noise, 'gross_outputs': gross,
                           'poisoned_differs': bad, 'first_bad_output': first,
                           'free_blocks': len(blocks),
                           'free_mb': round(sum(b[1] for b in blocks) / 2**20, 1)}), flush=True)
