@@ -750,7 +750,10 @@ class SplitGroupedPrecondition(GroupedPrecondition):
                     [s[0] for s in split], [s[1] for s in split], [s[2] for s in split], slots[0])
                 tables.append(('split', stab, len(split), sblocks, shost))
                 for (name, amc, bmc, osplit), slot in zip(flags, slots[1:]):
-                    rows = t[name]
+                    # longest tiles first: a tile's time is its K loop, and
+                    # blocks start in table order, so the K = 4608 / 2304
+                    # layers' tiles no longer form the launch's tail
+                    rows = sorted(t[name], key=lambda r: (-r[4][2], -r[4][0] * r[4][1]))
                     if not rows:
                         continue
                     meta: list[int] = []

@@ -41,6 +41,53 @@ def _to_device(data: torch.Tensor, target: torch.Tensor, args: argparse.Namespac
     return data, target
 
 
+class _GraphedSteps:
+    """Whole-step HIP-graph runner for ``train`` (``--graphs``): static input
+    buffers, the loss and accuracy produced inside the captured step
+    (``distributed_kfac_pytorch_amd.graphs.GraphedTrainStep``; graph-safe
+    strided convolutions, one step stream).  Batches of another shape (the
+    last partial batch) take the eager path."""
+
+    def __init__(self, model: torch.nn.Module, optimizer: torch.optim.Optimizer,
+                 preconditioner: Any, loss_func: torch.nn.Module,
+                 data: torch.Tensor, target: torch.Tensor, args: argparse.Namespace) -> None:
+        from distributed_kfac_pytorch_amd.graphs import GraphedTrainStep
+
+        self.x = torch.empty_like(data)
+        self.y = torch.empty_like(target)
+        self.acc = torch.zeros((), device=data.device)
+        # captured with the autocast weight cache off (it cannot be replayed)
+        amp = getattr(args, 'amp_dtype', None)
+
+        def fb() -> torch.Tensor:
+            with torch.autocast(data.device.type, dtype=amp or torch.float32,
+                                enabled=amp is not None, cache_enabled=False):
+                output = model(self.x)
+                loss = loss_func(output, self.y)
+            with torch.no_grad():
+                self.acc.copy_(accuracy(output, self.y))
+            loss.backward()
+            return loss
+
+        self.runner = GraphedTrainStep(fb, optimizer, preconditioner, model=model)
+
+    def fits(self, data: torch.Tensor, target: torch.Tensor) -> bool:
+        return data.shape == self.x.shape and data.stride() == self.x.stride() and \
+            target.shape == self.y.shape
+
+    def __call__(self, data: torch.Tensor, target: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+        self.x.copy_(data)
+        self.y.copy_(target)
+        loss = self.runner()
+        return loss.float(), self.acc
+
+
+def _graphs_usable(args: argparse.Namespace) -> bool:
+    return (bool(getattr(args, 'graphs', False)) and args.device.type == 'cuda'
+            and max(1, args.batches_per_allreduce) == 1
+            and getattr(args, 'grad_scaler', None) is None)
+
+
 def train(
     epoch: int,
     model: torch.nn.Module,
@@ -72,6 +119,26 @@ def train(
               desc=f'Epoch {epoch:3d}/{args.epochs:3d}', disable=not args.verbose) as t:
         for batch_idx, (data, target) in enumerate(train_loader):
             data, target = _to_device(data, target, args)
+            if _graphs_usable(args):
+                graphed = getattr(args, '_graphed_steps', None)
+                if graphed is None:
+                    graphed = _GraphedSteps(model, optimizer, preconditioner, loss_func,
+                                            data, target, args)
+                    args._graphed_steps = graphed
+                if graphed.fits(data, target):
+                    loss_v, acc_v = graphed(data, target)
+                    train_loss.update(loss_v)
+                    train_accuracy.update(acc_v)
+                    steps += 1
+                    t.update(1)
+                    if steps % log_interval == 0 or steps == total:
+                        t.set_postfix_str(
+                            f'loss: {train_loss.avg:.4f}, acc: {100 * train_accuracy.avg:.2f}%, '
+                            f'lr: {optimizer.param_groups[0]["lr"]:.4f}',
+                        )
+                    if max_steps and steps >= max_steps:
+                        break
+                    continue
             mini_step += 1
             last = mini_step % accum == 0 or batch_idx + 1 == n_batches
             sync_ctx = (
@@ -118,6 +185,9 @@ def train(
                 break
     out = {'train/loss': train_loss.avg, 'train/accuracy': train_accuracy.avg,
            'train/lr': optimizer.param_groups[0]['lr']}
+    graphed = getattr(args, '_graphed_steps', None)
+    if graphed is not None:
+        out['train/graph_replays'] = float(graphed.runner.replays)
     writer = getattr(args, 'log_writer', None)
     if writer is not None:
         for k, v in out.items():

@@ -10,6 +10,7 @@ checkpoint every ``--checkpoint-freq`` epochs).
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import time
@@ -55,6 +56,11 @@ def add_common_args(p: argparse.ArgumentParser, *, batch_size: int, epochs: int,
     p.add_argument('--max-steps-per-epoch', type=int, default=None,
                    help='truncate epochs (smoke runs)')
     p.add_argument('--log-interval', type=int, default=10)
+    p.add_argument('--graphs', type=int, default=0,
+                   help='1: replay training steps from whole-step HIP graphs '
+                        '(distributed_kfac_pytorch_amd.graphs.GraphedTrainStep; single-rank '
+                        'jobs, or KFAC_STEP_GRAPHS_MULTI=1; no gradient accumulation, no fp16 '
+                        'GradScaler); K-FAC second-order updates stay eager')
     p.add_argument('--no-resume', dest='resume', action='store_false', default=True)
 
 
@@ -75,13 +81,20 @@ def run(args: argparse.Namespace,
     if args.channels_last and args.cuda:
         model = model.to(memory_format=torch.channels_last)
     if args.world_size > 1:
-        model = torch.nn.parallel.DistributedDataParallel(
-            model,
-            device_ids=[args.local_rank] if args.cuda else None,
-            bucket_cap_mb=args.ddp_bucket_mb,
-            gradient_as_bucket_view=True,
-            static_graph=args.ddp_static_graph and args.batches_per_allreduce == 1,
-        )
+        ctx = contextlib.nullcontext()
+        if getattr(args, 'graphs', 0) and args.cuda:
+            # the reducer holds the AccumulateGrad nodes: build it on the
+            # stream the graphed steps run on
+            from distributed_kfac_pytorch_amd.graphs import step_stream
+            ctx = torch.cuda.stream(step_stream(args.device))
+        with ctx:
+            model = torch.nn.parallel.DistributedDataParallel(
+                model,
+                device_ids=[args.local_rank] if args.cuda else None,
+                bucket_cap_mb=args.ddp_bucket_mb,
+                gradient_as_bucket_view=True,
+                static_graph=args.ddp_static_graph and args.batches_per_allreduce == 1,
+            )
     optimizer, preconditioner, (lr_scheduler, kfac_scheduler) = optimizers.get_optimizer(
         model, args,
     )
