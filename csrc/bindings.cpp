@@ -106,19 +106,10 @@ std::vector<at::Tensor> rocsolver_eigh(at::Tensor A, int64_t algo,
                                        int64_t max_sweeps, double tol);
 int64_t sytrd_panel();
 int64_t sytrd_max_n();
-int64_t spd_lds_max_n();
-// eigh_block_host.cpp
-std::vector<at::Tensor> block_jacobi_eigh(at::Tensor A, c10::optional<at::Tensor> Q0,
-                                          int64_t max_sweeps, double tol,
-                                          int64_t inner_sweeps, double noise, bool refine);
-at::Tensor spd_inverse(at::Tensor F, double damping);
 std::vector<at::Tensor> spd_inverse_blocked(at::Tensor F, double damping);
 std::vector<at::Tensor> sytrd_reduce(std::vector<at::Tensor> stacks);
-std::vector<at::Tensor> tridiag_stedc(at::Tensor d, at::Tensor e);
 std::vector<at::Tensor> sytrd_begin(std::vector<at::Tensor> stacks);
 void sytrd_advance(at::Tensor descs, std::vector<int64_t> sizes, int64_t k0, int64_t k1);
-std::vector<at::Tensor> tridiag_eigvecs(at::Tensor A, at::Tensor d, at::Tensor e,
-                                        at::Tensor tau);
 
 namespace {
 
@@ -1182,12 +1173,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_act_forward", &bn_act_forward);
   m.def("bn_act_backward", &bn_act_backward);
   m.def("bn_act", &bn_act);
-  m.def("spd_lds_max_n", &spd_lds_max_n);
-  m.def("spd_inverse", &spd_inverse, py::call_guard<py::gil_scoped_release>());
   m.def("spd_inverse_blocked", &spd_inverse_blocked, py::call_guard<py::gil_scoped_release>());
   m.def("sytrd_reduce", &sytrd_reduce, py::call_guard<py::gil_scoped_release>());
-  m.def("tridiag_eigvecs", &tridiag_eigvecs, py::call_guard<py::gil_scoped_release>());
-  m.def("tridiag_stedc", &tridiag_stedc, py::call_guard<py::gil_scoped_release>());
   m.def("sytrd_begin", &sytrd_begin, py::call_guard<py::gil_scoped_release>());
   m.def("sytrd_advance", &sytrd_advance, py::call_guard<py::gil_scoped_release>());
   m.def("rocsolver_eigh", &rocsolver_eigh, py::call_guard<py::gil_scoped_release>(),
@@ -1209,10 +1196,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cast_multi", &cast_multi);
   // GIL released: one host thread per eigensolver lane (the sweep loop reads
   // its convergence flags back once per sweep)
-  m.def("block_jacobi_eigh", &block_jacobi_eigh, py::call_guard<py::gil_scoped_release>(),
-        py::arg("A"), py::arg("Q0") = py::none(), py::arg("max_sweeps") = 12,
-        py::arg("tol") = 1e-6, py::arg("inner_sweeps") = 2, py::arg("noise") = 4e-6,
-        py::arg("refine") = true);
   m.def("tridiag_eigh_dc", &tridiag_eigh_dc, py::call_guard<py::gil_scoped_release>());
   m.def("tridiag_dc_plan", &tridiag_dc_plan);
   m.def("eigh_twostage", &eigh_twostage, py::call_guard<py::gil_scoped_release>(),

@@ -1,5 +1,5 @@
-// 64x64x64 fp32 MFMA tile product on LDS operands, shared by the block
-// eigensolver (eigh_block.hip) and the blocked SPD inverse (spdinv_blocked.hip).
+// 64x64x64 fp32 MFMA tile product on LDS operands, used by the blocked SPD
+// inverse (spdinv_chol.hip).
 //
 // A 256-thread block = 4 waves; wave w computes the 32x32 quadrant
 // (wi, wj) = (w >> 1, w & 1) of  C = A^T * Bt  with both operands stored

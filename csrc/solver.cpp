@@ -231,115 +231,6 @@ void sytrd_advance(at::Tensor descs, std::vector<int64_t> sizes, int64_t k0, int
                             ns.data(), (int)ns.size(), (int)k0, (int)k1, s);
 }
 
-// A: [cnt, n, n] reduced by sytrd_reduce (reflectors); d, e, tau from it.
-// Returns (evals [cnt, n] ascending, evecs [cnt, n, n], eigenvectors in
-// columns).
-std::vector<at::Tensor> tridiag_eigvecs(at::Tensor A, at::Tensor d, at::Tensor e,
-                                        at::Tensor tau) {
-  TORCH_CHECK(A.is_cuda() && A.dim() == 3 && A.is_contiguous());
-  const int64_t cnt = A.size(0), n = A.size(1);
-  c10::hip::HIPGuardMasqueradingAsCUDA g(A.device());
-  hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
-  auto Z = at::empty({cnt, n, n}, A.options());
-  auto info = at::empty({std::max<int64_t>(cnt, 1)}, A.options().dtype(at::kInt));
-  if (cnt == 0 || n == 0) return {d, Z.transpose(1, 2)};
-  HandleState& st = handle_for(s);
-  auto run = [&](int64_t b) -> rocblas_status {
-    float* Ab = A.data_ptr<float>() + b * n * n;
-    float* Zb = Z.data_ptr<float>() + b * n * n;
-    rocblas_status r = rocsolver_sstedc(st.handle, rocblas_evect_tridiagonal, (int)n,
-                                        d.data_ptr<float>() + b * n,
-                                        e.data_ptr<float>() + b * n, Zb, (int)n,
-                                        info.data_ptr<int>() + b);
-    if (r != rocblas_status_success && r != rocblas_status_size_unchanged &&
-        r != rocblas_status_size_increased)
-      return r;
-    rocblas_status r2 = rocsolver_sormtr(st.handle, rocblas_side_left, rocblas_fill_lower,
-                                         rocblas_operation_none, (int)n, (int)n, Ab,
-                                         (int)n, tau.data_ptr<float>() + b * n, Zb,
-                                         (int)n);
-    return r2;
-  };
-  size_t need = 0;
-  ROCBLAS_OK(rocblas_start_device_memory_size_query(st.handle));
-  run(0);
-  ROCBLAS_OK(rocblas_stop_device_memory_size_query(st.handle, &need));
-  if (!st.workspace.defined() || (size_t)st.workspace.numel() < need) {
-    st.workspace = at::empty({(int64_t)std::max<size_t>(need, 1)},
-                             A.options().dtype(at::kByte));
-    ROCBLAS_OK(rocblas_set_workspace(st.handle, st.workspace.data_ptr(),
-                                     (size_t)st.workspace.numel()));
-  }
-  for (int64_t b = 0; b < cnt; ++b) ROCBLAS_OK(run(b));
-  return {d, Z.transpose(1, 2)};
-}
-
-// Eigenvectors of the tridiagonal matrices alone (rocSOLVER stedc, divide
-// and conquer): d, e [cnt, n] (d overwritten with the ascending eigenvalues,
-// e destroyed).  Returns (evals [cnt, n], Z [cnt, n, n] with the eigenvectors
-// of T in columns); the caller applies Q (ops/linalg.py apply_q_blocked: the
-// reflectors grouped into 256-wide UT blocks on fp32 GEMMs, replacing
-// rocSOLVER ormtr's 32-wide panel loop).
-std::vector<at::Tensor> tridiag_stedc(at::Tensor d, at::Tensor e) {
-  TORCH_CHECK(d.is_cuda() && d.dim() == 2 && d.is_contiguous() && e.is_contiguous() &&
-              d.scalar_type() == at::kFloat && e.sizes() == d.sizes());
-  const int64_t cnt = d.size(0), n = d.size(1);
-  c10::hip::HIPGuardMasqueradingAsCUDA g(d.device());
-  hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
-  auto Z = at::empty({cnt, n, n}, d.options());
-  auto info = at::empty({std::max<int64_t>(cnt, 1)}, d.options().dtype(at::kInt));
-  if (cnt == 0 || n == 0) return {d, Z.transpose(1, 2)};
-  HandleState& st = handle_for(s);
-  auto run = [&](int64_t b) -> rocblas_status {
-    return rocsolver_sstedc(st.handle, rocblas_evect_tridiagonal, (int)n,
-                            d.data_ptr<float>() + b * n, e.data_ptr<float>() + b * n,
-                            Z.data_ptr<float>() + b * n * n, (int)n,
-                            info.data_ptr<int>() + b);
-  };
-  size_t need = 0;
-  ROCBLAS_OK(rocblas_start_device_memory_size_query(st.handle));
-  run(0);
-  ROCBLAS_OK(rocblas_stop_device_memory_size_query(st.handle, &need));
-  if (!st.workspace.defined() || (size_t)st.workspace.numel() < need) {
-    st.workspace = at::empty({(int64_t)std::max<size_t>(need, 1)},
-                             d.options().dtype(at::kByte));
-    ROCBLAS_OK(rocblas_set_workspace(st.handle, st.workspace.data_ptr(),
-                                     (size_t)st.workspace.numel()));
-  }
-  for (int64_t b = 0; b < cnt; ++b) ROCBLAS_OK(run(b));
-  return {d, Z.transpose(1, 2)};
-}
-
-// ---------------------------------------------------------------------------
-// K-HIP-5 batched damped SPD inverse (csrc/spdinv.hip): F [cnt, n, n] fp32
-// symmetric -> (F + damping I)^-1, exactly symmetric, no host sync; one
-// workgroup per matrix, Gauss-Jordan in LDS (n <= spd_lds_max_n()).  Larger
-// factors are inverted one at a time by the caller (ops/linalg.py): the
-// strided-batched rocSOLVER potrf + potri path returned sporadic NaN rows on
-// MI355X (ROCm 7.2), so it is not offered here.
-namespace kfac {
-int spd_lds_max_n();
-void spd_inverse_lds(const float* F, float* X, int n, int batch, int64_t strideF,
-                     int64_t strideX, float damping, hipStream_t s);
-}  // namespace kfac
-
-int64_t spd_lds_max_n() { return kfac::spd_lds_max_n(); }
-
-at::Tensor spd_inverse(at::Tensor F, double damping) {
-  TORCH_CHECK(F.is_cuda() && F.scalar_type() == at::kFloat && F.dim() == 3 &&
-              F.size(1) == F.size(2) && F.is_contiguous());
-  const int64_t cnt = F.size(0), n = F.size(1);
-  TORCH_CHECK(n <= kfac::spd_lds_max_n(), "spd_inverse supports n <= ",
-              kfac::spd_lds_max_n());
-  c10::hip::HIPGuardMasqueradingAsCUDA g(F.device());
-  hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
-  auto X = at::empty_like(F);
-  if (cnt == 0 || n == 0) return X;
-  kfac::spd_inverse_lds(F.data_ptr<float>(), X.data_ptr<float>(), (int)n, (int)cnt,
-                        n * n, n * n, (float)damping, s);
-  return X;
-}
-
 // ---------------------------------------------------------------------------
 // K-HIP-5 blocked tier (csrc/spdinv_chol.hip): blocked Cholesky + triangular
 // inverse + W^T W on fp32 MFMA tiles, any n.  Returns (X [cnt, n, n] exactly

@@ -13,9 +13,9 @@ every rank).  MI355X-first differences:
   accumulate + EMA is a single fused SYRK.
 * Second order.  All factors this rank owns are decomposed together
   (``ops.linalg.eigh_many``: one-workgroup LDS Jacobi for n <= 128, the
-  native block-Jacobi solver warm-started from each factor's previous
-  eigenbasis above that), then broadcasts are issued in the reference's
-  (reversed layer, A then G) order.
+  native Householder tridiagonalisation chains + divide and conquer above
+  that, the two-stage solver for large same-size buckets), then broadcasts
+  are issued in the reference's (reversed layer, A then G) order.
 * No host syncs in ``step()``.  The KL-clip scale is reduced on the device
   (fp64 accumulator) and applied by the gradient-write kernel; the
   reference performs two ``.item()`` syncs per layer per step.
@@ -49,7 +49,6 @@ from distributed_kfac_pytorch_amd.parallel.comm import (
 
 logger = logging.getLogger(__name__)
 # diagnostics only: compute P but leave the raw gradients in place
-_DEBUG_NO_APPLY = os.environ.get('KFAC_DEBUG_NO_APPLY') == '1'
 
 
 class StepGraphs:
@@ -178,12 +177,11 @@ class StepGraphs:
         if inverse_step or not ordered or _native.native() is None:
             self.pending_key = None
             if inverse_step and self.graph is not None:
-                # a refresh: capture again afterwards.  Whole-step graphs
-                # (graphs.GraphedTrainStep) captured before a refresh produced
-                # non-finite gradients in every K-FAC layer after it on
-                # ResNet-50 while eager steps and re-captured graphs stayed
-                # finite (profiles/graph_replay_nonfinite_r2.txt); the cause
-                # is not pinned down, so no precondition graph outlives one
+                # a refresh: capture again afterwards (the refresh may have
+                # re-split the bases into new images; a fresh capture costs
+                # one eager step per refresh).  The post-refresh corruption of
+                # rounds 2-3 was MIOpen's strided 1x1 backward-data reading
+                # outside the graph (ops/conv.py), not this phase.
                 self.graph = None
                 self.key = None
                 self._release()
@@ -566,11 +564,7 @@ class BaseKFACPreconditioner:
             if l.g_factor is None:
                 raise RuntimeError('Cannot eigendecompose G before G has been computed')
             mats.append(l.g_factor)
-        # warm starts: each factor's previous eigenbasis (factors drift
-        # slowly between second-order updates; ops.linalg block Jacobi)
-        warm = [self._warm_basis(l.qa, m) for (_, l), m in zip(eig_a, mats[: len(eig_a)])]
-        warm += [self._warm_basis(l.qg, m) for (_, l), m in zip(eig_g, mats[len(eig_a):])]
-        results = linalg.eigh_many(mats, warm) if mats else []
+        results = linalg.eigh_many(mats) if mats else []
         for (_, l), (d, q) in zip(eig_a, results[: len(eig_a)]):
             assert isinstance(l, KFACEigenLayer)
             l.set_a_eig(d, q)
@@ -605,19 +599,6 @@ class BaseKFACPreconditioner:
     @staticmethod
     def _bcast_inv(fn: Callable[..., None], src: int, group: Any) -> None:
         fn(src=src, group=group, bucketed=True)
-
-    @staticmethod
-    def _warm_basis(q: Any, factor: torch.Tensor) -> torch.Tensor | None:
-        if (
-            os.environ.get('KFAC_EIGH_WARM', '1') == '0'
-            or not isinstance(q, torch.Tensor)
-            or q.shape != factor.shape
-            or q.dtype != torch.float32
-            or q.device != factor.device
-            or not q.is_cuda
-        ):
-            return None
-        return q
 
     @torch.no_grad()
     def step(self) -> None:
@@ -812,7 +793,7 @@ class BaseKFACPreconditioner:
         GPU fast path: three multi-tensor launches for the whole model
         (``ops.precondition.MultiLayerApply``); otherwise per layer.
         """
-        if not ordered or _DEBUG_NO_APPLY:
+        if not ordered:
             return
         if self._multi_apply is None:
             self._multi_apply = pops.MultiLayerApply()

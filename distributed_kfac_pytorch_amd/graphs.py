@@ -14,7 +14,8 @@ optimizer step`` and captures one graph per K-FAC step *kind*:
 * ``factor``: additionally the factor SYRK/EMA launches of the forward and
   backward hooks (``steps % factor_update_steps == 0``);
 * ``inverse`` steps (``steps % inv_update_steps == 0``) always run eagerly:
-  rocSOLVER's syevd cannot be stream-captured.
+  the refresh runs on its own lanes and host threads (ops.linalg) and its
+  finiteness check reads one flag back to the host.
 
 Graphs are captured once ``warmup`` eager steps have run and (with K-FAC)
 a second-order update step has run eagerly -- that step exercises every code
@@ -35,6 +36,16 @@ run later.  Replays advance the host-side
 K-FAC state (``steps``) exactly as an eager step would.  Values baked into a
 graph -- K-FAC hyperparameters, the optimizer's learning rates -- form a
 signature; when it changes the affected graphs are dropped and re-captured.
+
+Correctness: a captured graph may only read memory that its private pool
+or a live tensor owns.  MIOpen's backward-data of strided 1x1 convolutions
+did not (it read free global-pool blocks, so replays broke as soon as other
+eager work -- an eval pass, a second model, the refresh -- reused them:
+profiles/graph_oop_r4.md); the runner therefore switches those convolutions
+to the graph-safe ``ops.conv.StridedConv1x1`` (``model=``), and
+``tools/graph_oop_audit.py`` checks any new model the same way (poisons the
+free global pool between replays).  Every step -- eager or replayed -- runs
+on one persistent stream (``step_stream()``).
 
 Multi-rank jobs run every step eagerly by default (the K-FAC precondition
 phase is still replayed from ``StepGraphs``).  The K-FAC collectives
@@ -297,13 +308,8 @@ class GraphedTrainStep:
         # no Python GC while capturing: collecting an unreachable cycle that
         # holds an old CUDAGraph would destroy that graph mid-capture, which
         # HIP forbids (hipErrorStreamCaptureUnsupported -> abort)
-        pool = None
-        if os.environ.get('KFAC_GRAPH_SHARED_POOL') == '1':  # diagnostics
-            if getattr(self, '_pool', None) is None:
-                self._pool = torch.cuda.graph_pool_handle()
-            pool = self._pool
         with _no_gc(), torch.cuda.stream(side):
-            with torch.cuda.graph(g, pool=pool, stream=side):
+            with torch.cuda.graph(g, stream=side):
                 loss = self.forward_backward()
                 if p is not None:
                     p.step()
@@ -328,10 +334,7 @@ class GraphedTrainStep:
         # step folds garbage into the gradients / factors and the replays
         # after it diverge (profiles/graph_replay_nonfinite_r2.txt; torch
         # warns "The AccumulateGrad node's stream does not match ...").
-        if os.environ.get('KFAC_GRAPH_KEEP_AUTOGRAD') == '1':  # A/B diagnostic only
-            self.outputs[kind] = loss
-        else:
-            self.outputs[kind] = loss.detach()
+        self.outputs[kind] = loss.detach()
         del loss
         self.grads[kind] = [q.grad for q in self._params()]
         self.captures += 1
@@ -356,11 +359,6 @@ class GraphedTrainStep:
             self.seen += 1
             if kind == 'inverse':
                 self._inverse_done = True
-                if os.environ.get('KFAC_GRAPH_SYNC_AFTER_REFRESH') == '1':
-                    # diagnostic for the non-finite replays after a refresh
-                    # (profiles/graph_replay_nonfinite_r2.txt): rules a race
-                    # with the refresh's side-lane work in or out
-                    torch.cuda.synchronize()
             return loss
         sig = self._signature()
         if sig != self.signature:
@@ -402,8 +400,6 @@ class GraphedTrainStep:
                 return self._eager()
         with tracing.phase(f'step(graph:{kind})'):
             self.graphs[kind].replay()
-        if os.environ.get('KFAC_GRAPH_SYNC') == '1':  # diagnostics
-            torch.cuda.synchronize()
         # expose this graph's gradients as .grad (each kind has its own)
         for q, gr in zip(self._params(), self.grads[kind]):
             q.grad = gr

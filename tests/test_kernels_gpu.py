@@ -218,7 +218,7 @@ def test_eigh_many_mixed_sizes(cuda):
 
 
 def test_eigh_many_rocsolver_sizes(cuda):
-    """Mixed mid-size factors through the threaded rocSOLVER lanes: the
+    """Mixed mid-size factors through the threaded chain lanes: the
     eigenpairs must match a float64 reference."""
     torch.manual_seed(3)
     mats = []
@@ -280,15 +280,14 @@ def test_sytrd_reduce_reconstructs(cuda):
             assert err < 1e-5 * a0[b].abs().max().item(), (n, b, err)
 
 
-@pytest.mark.parametrize('back', ['blocked', 'rocsolver'])
-@pytest.mark.parametrize('sizes', [(65, 96, 97, 130, 257), (513, 1000, 64, 700, 2049)])
-def test_eigh_many_sytrd_tier(cuda, monkeypatch, sizes, back):
-    """eigh_many through the native sytrd tier (segmented chain; stedc, then
-    the blocked UT back-transform or rocSOLVER ormtr), including
-    rank-deficient K-FAC-like factors, vs a float64 reference."""
-    monkeypatch.setenv('KFAC_EIGH', 'sytrd')
-    monkeypatch.setenv('KFAC_SYTRD_MIN_N', '65')
-    monkeypatch.setenv('KFAC_EIGH_ORMTR', back)
+@pytest.mark.parametrize('graphs', ['0', '1'])
+@pytest.mark.parametrize('sizes', [(129, 130, 257, 300), (513, 1000, 64, 700, 2049)])
+def test_eigh_many_sytrd_tier(cuda, monkeypatch, sizes, graphs):
+    """eigh_many through the native sytrd tier (segmented chains, native
+    divide and conquer, blocked UT back-transform), including rank-deficient
+    K-FAC-like factors, vs a float64 reference; chain segments launched
+    eagerly or replayed from captured HIP graphs."""
+    monkeypatch.setenv('KFAC_SYTRD_GRAPHS', graphs)
     torch.manual_seed(7)
     # twice with the same sizes: the second refresh replays the chain's
     # captured HIP graphs on new matrices
@@ -305,37 +304,10 @@ def test_eigh_many_sytrd_tier(cuda, monkeypatch, sizes, back):
             _check_eigpairs(m, d, q)
 
 
-def test_eigh_many_sytrd_warm_acceptance(cuda, monkeypatch):
-    """Default large tier with warm bases: a factor its previous basis still
-    diagonalises is settled by the acceptance test (no solve); chain
-    members are never candidates (fixed chain signature); every result
-    matches float64."""
-    monkeypatch.setenv('KFAC_EIGH_LARGE', 'sytrd')
-    monkeypatch.setenv('KFAC_SYTRD_MIN_N', '250')  # 300: chain; 130, 200: syevd
-    monkeypatch.setattr(linalg, 'WARM_ACCEPT_MAX_N', 2048)  # opt-in since round 3
-    torch.manual_seed(11)
-    mats, warm = [], []
-    for j, n in enumerate((200, 200, 300, 130)):
-        x = torch.randn(n, 2 * n, device=cuda)
-        m = x @ x.t() / (2 * n) + 1e-3 * torch.eye(n, device=cuda)
-        mats.append(m)
-        if j == 0:
-            warm.append(torch.linalg.eigh(m.double())[1].float())  # exact basis
-        else:
-            warm.append(torch.linalg.eigh(m + 0.1 * torch.eye(n, device=cuda)
-                                          + 0.05 * torch.randn(n, n, device=cuda).mT
-                                          @ torch.randn(n, n, device=cuda) / n)[1])
-    linalg.last_stats.clear()
-    res = linalg.eigh_many(mats, warm)
-    assert linalg.last_stats.get('accepted', []).count(200) >= 1
-    for m, (d, q) in zip(mats, res):
-        _check_eigpairs(m, d, q)
-
-
 @pytest.mark.parametrize('n', [1, 7, 64, 129, 176, 177, 300, 577, 640, 2049])
 def test_spd_inverse(cuda, n):
-    """K-HIP-5: LDS Gauss-Jordan (n <= 176) and blocked MFMA Gauss-Jordan
-    (larger n) damped inverses vs a float64 reference; exactly symmetric."""
+    """K-HIP-5: blocked Cholesky damped inverses on fp32 MFMA tiles vs a
+    float64 reference; exactly symmetric."""
     torch.manual_seed(n)
     b, damping = (3 if n < 1000 else 2), 1e-2
     x = torch.randn(b, n, 2 * n, device=cuda)
@@ -418,65 +390,18 @@ def _kfac_like(n: int, seed: int, cuda, drift: float = 0.02):
     return old.float().to(cuda), a.float().to(cuda)
 
 
-@pytest.mark.parametrize('n', [129, 300, 640, 1025])
-def test_block_jacobi_cold_and_warm(cuda, n):
-    """K-HIP-3 large tier: cold start and warm start from the previous
-    eigenbasis both match a float64 reference to 1e-5 relative (eigenvalues
-    and reconstruction) with orthonormal vectors; the warm start needs
-    fewer sweeps."""
-    lib = _native.native()
-    old, new = _kfac_like(n, n, cuda)
-    _, q0 = torch.linalg.eigh(old.double())
-    q0 = q0.float().unsqueeze(0).contiguous()
-    sweeps = {}
-    for mode, warm in (('cold', None), ('warm', q0)):
-        d, q, sw, _ = lib.block_jacobi_eigh(new.unsqueeze(0).contiguous(), warm, 20, 1e-6, 1,
-                                             4e-6, True)
-        assert int(sw[0]) > 0, (mode, 'not converged')
-        sweeps[mode] = int(sw[0])
-        _check_eigpairs(new, d[0], q[0], tol=1e-5)
-        eye = torch.eye(n, device=cuda, dtype=torch.float64)
-        assert (q[0].double().t() @ q[0].double() - eye).abs().max().item() < 1e-5
-        assert bool((d[0][1:] >= d[0][:-1]).all())
-    assert sweeps['warm'] < sweeps['cold'], sweeps
-
-
-def test_eigh_many_warm_accept(cuda, monkeypatch):
-    """A factor its previous basis still diagonalises keeps that basis (one
-    GEMM, no solve); the others of the bucket are solved; all exact."""
-    monkeypatch.setattr(linalg, 'WARM_ACCEPT_MAX_N', 2048)  # opt-in since round 3
-    mats, warms = [], []
-    for j, n in enumerate((200, 200, 200, 333)):
-        old, new = _kfac_like(n, 200 + j, cuda)
-        if j == 0:
-            new = old.clone()  # unchanged factor
+def test_eigh_many_above_native_limit_falls_back(cuda, monkeypatch):
+    """Factors above the native chain limit go to rocSOLVER's syevd (no
+    host synchronisation), still exact."""
+    monkeypatch.setattr(linalg, '_use_sytrd', lambda n: False)
+    monkeypatch.setattr(linalg.twostage, 'max_n', lambda: 0)
+    mats = []
+    for j, n in enumerate((200, 333)):
+        _, new = _kfac_like(n, 100 + j, cuda)
         mats.append(new)
-        warms.append(torch.linalg.eigh(old.double())[1].float().contiguous())
     linalg.last_stats.clear()
-    res = linalg.eigh_many(mats, warms)
-    for m, (d, q) in zip(mats, res):
-        _check_eigpairs(m, d, q)
-    assert linalg.last_stats.get('accepted') == [200], linalg.last_stats
-
-
-def test_eigh_many_block_jacobi_and_fallback(cuda, monkeypatch):
-    """KFAC_EIGH_LARGE=block routes the large factors through the native
-    block Jacobi (warm where a previous basis is given); a factor that does
-    not converge within the sweep budget falls back to syevd, still exact."""
-    monkeypatch.setenv('KFAC_EIGH_LARGE', 'block')
-    mats, warms = [], []
-    for j, n in enumerate((200, 200, 333, 96)):
-        old, new = _kfac_like(n, 100 + j, cuda)
-        mats.append(new)
-        warms.append(torch.linalg.eigh(old.double())[1].float() if j != 1 else None)
-    linalg.last_stats.clear()
-    res = linalg.eigh_many(mats, warms)
-    for m, (d, q) in zip(mats, res):
-        _check_eigpairs(m, d, q)
-    assert linalg.last_stats['sweeps'], linalg.last_stats
-    monkeypatch.setattr(linalg, 'BJ_MAX_SWEEPS_WARM', 1)
-    monkeypatch.setattr(linalg, 'BJ_MAX_SWEEPS_COLD', 1)
-    res = linalg.eigh_many(mats, warms)
+    res = linalg.eigh_many(mats)
+    assert {t[0] for t in linalg.last_stats['tiers']} == {'syevd'}, linalg.last_stats
     for m, (d, q) in zip(mats, res):
         _check_eigpairs(m, d, q)
 

@@ -18,3 +18,7 @@ mkdir -p $O
 b() { name=$1; shift; env "$@" timeout -k 10 300 python3 -u bench.py --steps 100 --warmup 10 --baseline 1 --secondary-bf16 0 > $O/$name.json 2> $O/$name.err || { echo "$name rc=$?"; tail -3 $O/$name.err; return 1; }
   python3 -c "import json;d=json.load(open('$O/$name.json'));print('$name', d['value'], d['kind_ms'], d.get('sgd_ms_per_step'), d['params_finite'])"; }
 b base A=1 && b nogtcwrw MIOPEN_DEBUG_CONV_IMPLICIT_GEMM_ASM_WRW_GTC_XDLOPS_NHWC=0 && b base2 A=1 && b nogtcwrw2 MIOPEN_DEBUG_CONV_IMPLICIT_GEMM_ASM_WRW_GTC_XDLOPS_NHWC=0
+KFAC_SYTRD_GRAPHS=1 timeout -k 10 200 python -u tools/eigh_probe.py --sizes 4608 --count 1 --no-acc > gpurun_out/r4h/eig/e4608_graphs.jsonl 2>> gpurun_out/r4h/eig/e.err && \
+KFAC_SYTRD_GRAPHS=1 timeout -k 10 200 python -u tools/eigh_probe.py --sizes 4608 --count 3 --no-acc >> gpurun_out/r4h/eig/e4608_graphs.jsonl 2>> gpurun_out/r4h/eig/e.err && \
+KFAC_SYTRD_GRAPHS=1 timeout -k 10 300 python -u tools/eigh_probe.py --mix resnet50 --no-acc >> gpurun_out/r4h/eig/e4608_graphs.jsonl 2>> gpurun_out/r4h/eig/e.err && \
+KFAC_SYTRD_GRAPHS=1 timeout -k 10 200 rocprofv3 --kernel-trace -d gpurun_out/r4h/eig/prof2 -o p2 -- python3 tools/eigh_probe.py --sizes 4608 --count 1 --reps 1 --no-acc > /dev/null 2>> gpurun_out/r4h/eig/e.err
