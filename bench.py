@@ -309,10 +309,15 @@ def run(args: argparse.Namespace, use_kfac: bool, rank: int, world: int,
         marker()
     t0 = time.perf_counter()
     nan_probe = os.environ.get('KFAC_BENCH_NANSTEP') == '1'  # diagnostics only
+    host_ms: list[float] = []
     for i in range(args.steps):
         kinds.append(kind())
         ev[i].record()
+        h0 = time.perf_counter()
         step()
+        # host time to issue the step (no sync): equal to the GPU time when
+        # the step is host-bound
+        host_ms.append((time.perf_counter() - h0) * 1e3)
         if nan_probe:
             bad = [n for n, p_ in model.named_parameters() if not torch.isfinite(p_).all()]
             gbad = [n for n, p_ in model.named_parameters()
@@ -339,7 +344,13 @@ def run(args: argparse.Namespace, use_kfac: bool, rank: int, world: int,
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t[0].item())
     by_kind = {'plain': float(t[1]), 'factor': float(t[2]), 'inverse': float(t[3])}
+    host_by_kind = {}
+    for k in ('plain', 'factor', 'inverse'):
+        v = sorted(t for t, kk in zip(host_ms, kinds) if kk == k)
+        if v:
+            host_by_kind[k] = round(v[len(v) // 2], 3)  # median
     out = {'seconds': elapsed, 'ms_per_step': elapsed / args.steps * 1e3,
+           'host_issue_ms': host_by_kind,
            'kind_ms': {k: round(v, 3) for k, v in by_kind.items() if v > 0.0},
            'kind_counts': {k: kinds.count(k) for k in ('plain', 'factor', 'inverse')},
            'inverse_ms_each': [round(t, 1) for t, kk in zip(per_step, kinds) if kk == 'inverse'],
@@ -488,8 +499,12 @@ def main() -> None:
             'vs_baseline': round(v2 / (REFERENCE_IMG_S_PER_GPU['bf16'] * world), 4),
             'kind_ms': sec['kind_ms'], 'params_finite': sec['params_finite'],
             'eigen_refresh_ms': round(sec.get('refresh_ms', 0.0), 3),
+            'host_issue_ms': sec['host_issue_ms'],
             'graphs': 'step_graphs' in sec,
         }
+    line['host_issue_ms'] = res['host_issue_ms']
+    if base is not None:
+        line['sgd_host_issue_ms'] = base['host_issue_ms']
     for k in ('phase_ms_per_step', 'phase_counts', 'kfac_layers', 'step_graphs',
               'kfac_memory_mb', 'kfac_steps_end', 'align_steps', 'inverse_ms_each',
               'refresh_ms_per_rank', 'params_finite'):
