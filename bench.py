@@ -153,6 +153,10 @@ def setup(args: argparse.Namespace) -> tuple[int, int, torch.device]:
     dev = torch.device('cuda', local)
     torch.backends.cudnn.benchmark = bool(args.cudnn_benchmark)
     if world > 1 or args.ddp:
+        if args.graphs and (world == 1 or os.environ.get('KFAC_STEP_GRAPHS_MULTI') == '1'):
+            # captured RCCL collectives: the watchdog must not poll (and
+            # abort on) events recorded inside a capture
+            os.environ.setdefault('TORCH_NCCL_ASYNC_ERROR_HANDLING', '0')
         if args.backend == 'nccl':
             dist.init_process_group('nccl', device_id=dev)
         else:

@@ -88,6 +88,13 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 
 // col step for column k of panel p (i = k - p).  fin_only: only finalise
 // column k-1 (panel end).  grid (chunks, batch).
+//
+// Latency-bound (a few microseconds of work per column, n of them in a
+// chain): every global load of a thread is issued first; the scalars shared
+// by the block (the w.v reduction of the previous symv, the panel entries
+// of column k) are formed by EVERY wave on its own -- wave reductions and
+// lane broadcasts, no LDS round trip -- so the kernel has one block
+// barrier, before the final cross-wave sums.
 __global__ void __launch_bounds__(SY_T) sytrd_col_kernel(
     const SytrdDesc* __restrict__ descs, int k, int p, int fin_only) {
   const GView D = gview(descs[blockIdx.y]);
@@ -98,8 +105,7 @@ __global__ void __launch_bounds__(SY_T) sytrd_col_kernel(
   const int i = k - p;
   const int r = r0 + threadIdx.x;
   const bool act = r < n;
-  __shared__ float red[SY_T / 64];
-  __shared__ float cW[SY_NB], cV[SY_NB];
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   __shared__ float wred[SY_T / 64][SY_P1];
   const bool fin = i > 0;  // column k-1 to finalise
 
@@ -108,17 +114,17 @@ __global__ void __launch_bounds__(SY_T) sytrd_col_kernel(
   // panel's current width are masked after the load, never multiplied in)
   float s2 = 0.f;
   if (fin) {
-    // partial w.v of column k-1: rows k..n-1 in blocks of SY_ROWS
+    // partial w.v of column k-1 (one per symv row block), summed per wave
     const int cnt = (int)ceil_div(n - k, SY_ROWS);
-    for (int t = threadIdx.x; t < cnt; t += SY_T) s2 += D.part2[t];
+    for (int t = l; t < cnt; t += 64) s2 += D.part2[t];
   }
   const float tp = fin ? D.sc[0] : 0.f;
   const float sprev = fin ? D.sc[1] : 0.f;
-  const int j0 = threadIdx.x;
+  // lane j < i of every wave: W[k, j] and V_j[k] of the panel
   float cw_raw = 0.f, cv_raw = 0.f;
-  if (j0 < i && !fin_only) {
-    cw_raw = D.Wt[(int64_t)j0 * n + k];
-    cv_raw = j0 == i - 1 ? 1.f : D.A[(int64_t)(p + j0) * n + k];  // V_{i-1}[k] = 1
+  if (l < i && !fin_only) {
+    cw_raw = D.Wt[(int64_t)l * n + k];
+    cv_raw = l == i - 1 ? 1.f : D.A[(int64_t)(p + l) * n + k];  // V_{i-1}[k] = 1
   }
   float vraw = 0.f, wraw = 0.f;
   if (act && fin) {
@@ -143,45 +149,45 @@ __global__ void __launch_bounds__(SY_T) sytrd_col_kernel(
   }
 
   float alpha2 = 0.f;
-  if (fin) alpha2 = -0.5f * tp * block_sum(s2, red);
-  if (j0 < SY_NB && !fin_only) {
-    // finalised W[k, i-1] gets the -tau/2 (w.v) v correction
-    cW[j0] = j0 < i ? cw_raw + (j0 == i - 1 ? alpha2 : 0.f) : 0.f;
-    cV[j0] = j0 < i ? cv_raw : 0.f;
-  }
-  __syncthreads();
+  if (fin) alpha2 = -0.5f * tp * wave_sum_uniform(s2);
+  // finalised W[k, i-1] gets the -tau/2 (w.v) v correction
+  const float cw = l < i ? cw_raw + (l == i - 1 ? alpha2 : 0.f) : 0.f;
+  const float cv = l < i ? cv_raw : 0.f;
 
   float vprev = 0.f, wprev = 0.f;
   if (act && fin) {
     vprev = r == k ? 1.f : vraw * sprev;
     if (r > k) D.A[(int64_t)(k - 1) * n + r] = vprev;
     wprev = wraw + alpha2 * vprev;
-    // W[k, i-1] is finalised by every block on its own (cW above) and not
+    // W[k, i-1] is finalised by every block on its own (cw above) and not
     // read again by later col / symv steps: writing it here would race with
     // those reads.  The panel-end trailing update does read it (r = q).
     if (r > k || fin_only) D.Wt[(int64_t)(i - 1) * n + r] = wprev;
   }
   if (fin_only) return;
 
-  if (act) {
+  const int cwi = __builtin_bit_cast(int, cw), cvi = __builtin_bit_cast(int, cv);
 #pragma unroll
-    for (int j = 0; j < SY_NB; ++j) {
-      if (j == i - 1) {
-        vj[j] = vprev;
-        wj[j] = wprev;
-      } else if (j >= i) {
-        vj[j] = 0.f;
-        wj[j] = 0.f;
-      }
-      a -= vj[j] * cW[j] + wj[j] * cV[j];
+  for (int j = 0; j < SY_NB; ++j) {
+    if (j == i - 1) {
+      vj[j] = vprev;
+      wj[j] = wprev;
+    } else if (j >= i) {
+      vj[j] = 0.f;
+      wj[j] = 0.f;
     }
+    // lane j's panel entries, broadcast (zero for j >= i)
+    const float cWj = __builtin_bit_cast(float, __builtin_amdgcn_readlane(cwi, j));
+    const float cVj = __builtin_bit_cast(float, __builtin_amdgcn_readlane(cvi, j));
+    a -= vj[j] * cWj + wj[j] * cVj;
+  }
+  if (act) {
     D.A[(int64_t)k * n + r] = a;
     if (r == k) D.d[k] = a;
   }
   if (k == n - 1) return;  // last diagonal entry: no reflector
   // partial sums over the reflector tail x = a[k+2:n]
   const float x = (act && r >= k + 2) ? a : 0.f;
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   float s0 = wave_sum_uniform(x * x);
   if (l == 0) wred[w][0] = s0;
 #pragma unroll
@@ -207,6 +213,12 @@ __global__ void __launch_bounds__(SY_T) sytrd_col_kernel(
 }
 
 // symv step for column k (k <= n-2).  grid (row blocks, batch).
+//
+// The matrix stream does not depend on the reflector scalars (v is staged
+// raw; the scale is applied to each row's sum), so the first block of this
+// wave's rows is loaded before the prologue, the prologue's loads land
+// under it, and after ONE block barrier (staged v and partials visible)
+// each wave forms the scalars and its panel correction terms on its own.
 __global__ void __launch_bounds__(SY_T) sytrd_symv_kernel(
     const SytrdDesc* __restrict__ descs, int k, int p) {
   const GView D = gview(descs[blockIdx.y]);
@@ -217,35 +229,48 @@ __global__ void __launch_bounds__(SY_T) sytrd_symv_kernel(
   const int i = k - p;
   __shared__ __attribute__((aligned(16))) float sv[SY_MAXN];
   __shared__ float ptmp[SY_MAXCH * SY_P1];
-  __shared__ float tot[SY_P1];
-  __shared__ float t1[SY_NB], t2[SY_NB], wk1[SY_NB], ak1[SY_NB];
   __shared__ float red[SY_T / 64];
-  __shared__ float scal[3];
 
-  // ---- every global load except the matrix rows first, in flight together:
-  // the col-step partials of column k, the pivot, the panel entries of
-  // column k+1, the raw reflector row (scaled later: v = [1, scale * a]),
-  // and this wave's rows' panel entries for the V t1 + W t2 correction
-  const int nch = (int)ceil_div(n - k, SY_T);
-  for (int t = threadIdx.x; t < nch * SY_P1; t += SY_T) ptmp[t] = D.part1[t];
-  const float alpha = D.A[(int64_t)k * n + k + 1];
-  if ((int)threadIdx.x < i) {
-    const int j = threadIdx.x;
-    wk1[j] = D.Wt[(int64_t)j * n + k + 1];
-    ak1[j] = D.A[(int64_t)(p + j) * n + k + 1];
-  }
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int rw = row0 + wv * SY_RPW;
   // v staged 16-B aligned: column col at sv[col - base], base = (k+1)
   // rounded down to 4; columns <= k+1 hold 0 (column k+1, v = 1, is added
   // per row from A[r][k+1] below)
   const int base = (k + 1) & ~3;
   const int span = n - base;
+  const bool vec = (n & 3) == 0;  // rows 16-B aligned
+  const int nq = span >> 2;
+  // rows past the end read row n-1 (valid memory) and are dropped below,
+  // so the streaming loop has no per-row branch
+  const GLOBAL float* rp[SY_RPW];
+#pragma unroll
+  for (int h = 0; h < SY_RPW; ++h)
+    rp[h] = D.A + (int64_t)(rw + h < n ? rw + h : n - 1) * n + base;
+  // ---- (1) this wave's first SY_SU x SY_RPW matrix block (16-B per lane)
+  f4 a4[SY_SU][SY_RPW];
+  const bool first = vec && l + (SY_SU - 1) * 64 < nq;
+  if (first) {
+#pragma unroll
+    for (int u = 0; u < SY_SU; ++u)
+#pragma unroll
+      for (int h = 0; h < SY_RPW; ++h) a4[u][h] = *(const GLOBAL f4*)(rp[h] + 4 * (l + 64 * u));
+  }
+  // ---- (2) prologue: the col step's partials of column k, the raw
+  // reflector row, this lane's panel entry of column k+1, the pivot, and
+  // this wave's rows' panel entries for the V t1 + W t2 correction
+  const int nch = (int)ceil_div(n - k, SY_T);
+  for (int t = threadIdx.x; t < nch * SY_P1; t += SY_T) ptmp[t] = D.part1[t];
   const GLOBAL float* arow = D.A + (int64_t)k * n;
   for (int c = threadIdx.x; c < span; c += SY_T) {
     const int col = base + c;
     sv[c] = col <= k + 1 ? 0.f : arow[col];
   }
-  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
-  const int rw = row0 + wv * SY_RPW;
+  // lane l < i: W[k+1, l]; lane 32 <= l < 32 + i: V_{l-32}[k+1]
+  float wa = 0.f;
+  if (l < i) wa = D.Wt[(int64_t)l * n + k + 1];
+  else if (l >= 32 && l - 32 < i) wa = D.A[(int64_t)(p + l - 32) * n + k + 1];
+  const float alpha = D.A[(int64_t)k * n + k + 1];
   float pv[SY_RPW], pk1[SY_RPW];
 #pragma unroll
   for (int h = 0; h < SY_RPW; ++h) {
@@ -257,63 +282,26 @@ __global__ void __launch_bounds__(SY_T) sytrd_symv_kernel(
   }
   __syncthreads();
 
-  // reduce the partials, then the reflector scalars
-  for (int t = threadIdx.x; t < SY_P1; t += SY_T) {
-    float s = 0.f;
-    for (int c = 0; c < nch; ++c) s += ptmp[c * SY_P1 + t];
-    tot[t] = s;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const float xn2 = tot[0];
-    float tau_k, beta, scale;
-    if (xn2 == 0.f) {
-      tau_k = 0.f;
-      beta = alpha;
-      scale = 0.f;
-    } else {
-      beta = -copysignf(sqrtf(alpha * alpha + xn2), alpha);
-      tau_k = (beta - alpha) / beta;
-      scale = 1.f / (alpha - beta);
-    }
-    scal[0] = tau_k;
-    scal[1] = scale;
-    if (blockIdx.x == 0) {
-      D.e[k] = beta;
-      D.tau[k] = tau_k;
-      D.sc[0] = tau_k;
-      D.sc[1] = scale;
-    }
-  }
-  __syncthreads();
-  const float tau_k = scal[0], scale = scal[1];
-  if ((int)threadIdx.x < i) {
-    const int j = threadIdx.x;
-    t1[j] = wk1[j] + scale * tot[1 + j];
-    t2[j] = ak1[j] + scale * tot[1 + SY_NB + j];
-  }
-  __syncthreads();
-
-  // SY_RPW rows per wave, all in flight together: one 16-B load per lane
-  // per row per 256 columns (rows are 16-B aligned when n % 4 == 0)
+  // ---- (3) y_raw = A22 a_raw for this wave's rows
   float acc[SY_RPW];
 #pragma unroll
   for (int h = 0; h < SY_RPW; ++h) acc[h] = 0.f;
-  if ((n & 3) == 0) {
-    typedef float f4 __attribute__((ext_vector_type(4)));
-    const int nq = span >> 2;
-    // rows past the end read row n-1 (valid memory) and are dropped below,
-    // so the streaming loop has no per-row branch
-    const GLOBAL float* rp[SY_RPW];
-#pragma unroll
-    for (int h = 0; h < SY_RPW; ++h)
-      rp[h] = D.A + (int64_t)(rw + h < n ? rw + h : n - 1) * n + base;
-    // SY_SU column blocks per row in flight together: SY_RPW * SY_SU 16-B
-    // loads per lane before the first FMA (the 1-deep loop kept 4 loads in
-    // flight and streamed the trailing matrix at ~2.5 TB/s)
+  if (vec) {
     int q = l;
+    if (first) {
+#pragma unroll
+      for (int u = 0; u < SY_SU; ++u) {
+        const f4 vv = *reinterpret_cast<const f4*>(sv + 4 * (q + 64 * u));
+#pragma unroll
+        for (int h = 0; h < SY_RPW; ++h)
+          acc[h] += (a4[u][h].x * vv.x + a4[u][h].y * vv.y) +
+                    (a4[u][h].z * vv.z + a4[u][h].w * vv.w);
+      }
+      q += SY_SU * 64;
+    }
+    // SY_SU column blocks per row in flight together: SY_RPW * SY_SU 16-B
+    // loads per lane before the first FMA
     for (; q + (SY_SU - 1) * 64 < nq; q += SY_SU * 64) {
-      f4 a4[SY_SU][SY_RPW];
 #pragma unroll
       for (int u = 0; u < SY_SU; ++u)
 #pragma unroll
@@ -344,6 +332,35 @@ __global__ void __launch_bounds__(SY_T) sytrd_symv_kernel(
         if (rw + h < n) acc[h] += D.A[(int64_t)(rw + h) * n + base + c] * vc;
     }
   }
+
+  // ---- (4) reflector scalars, per wave: ||x||^2 and this lane's
+  // V^T x / W^T x partial totals (lane l needs entry 1 + l either way)
+  float xn2 = 0.f, xl = 0.f;
+  for (int c = 0; c < nch; ++c) {
+    xn2 += ptmp[c * SY_P1];
+    if (l + 1 < SY_P1) xl += ptmp[c * SY_P1 + 1 + l];
+  }
+  float tau_k, beta, scale;
+  if (xn2 == 0.f) {
+    tau_k = 0.f;
+    beta = alpha;
+    scale = 0.f;
+  } else {
+    beta = -copysignf(sqrtf(alpha * alpha + xn2), alpha);
+    tau_k = (beta - alpha) / beta;
+    scale = 1.f / (alpha - beta);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    D.e[k] = beta;
+    D.tau[k] = tau_k;
+    D.sc[0] = tau_k;
+    D.sc[1] = scale;
+  }
+  // t1 = W^T v (lanes < i), t2 = V^T v (lanes 32 .. 32 + i)
+  const bool tlive = l < i || (l >= 32 && l - 32 < i);
+  const float tl = tlive ? wa + scale * xl : 0.f;
+
+  // ---- (5) w = tau (A22 v - V t1 - W t2) for this wave's rows
   float pd = 0.f;
 #pragma unroll
   for (int h = 0; h < SY_RPW; ++h) {
@@ -351,10 +368,7 @@ __global__ void __launch_bounds__(SY_T) sytrd_symv_kernel(
     if (r >= n) break;
     // y = A22 v with v = [1, scale * a]
     const float y = pk1[h] + scale * wave_sum_uniform(acc[h]);
-    float cp = 0.f;
-    if (l < i) cp = pv[h] * t1[l];
-    else if (l >= 32 && l - 32 < i) cp = pv[h] * t2[l - 32];
-    const float corr = wave_sum_uniform(cp);
+    const float corr = wave_sum_uniform(pv[h] * tl);
     const float wr = tau_k * (y - corr);
     if (l == 0) {
       D.Wt[(int64_t)i * n + r] = wr;

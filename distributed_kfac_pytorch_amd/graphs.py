@@ -171,6 +171,10 @@ class GraphedTrainStep:
         self.forward_backward = forward_backward
         self.optimizer = optimizer
         self.preconditioner = preconditioner
+        if isinstance(model, torch.nn.parallel.DistributedDataParallel):
+            # DDP records runtime statistics (event timings, host syncs) in
+            # its first 10 iterations: a capture must come after them
+            warmup = max(warmup, 11)
         self.warmup = warmup
         if enabled is None:
             multi = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
@@ -390,12 +394,15 @@ class GraphedTrainStep:
                         if self.preconditioner is not None:
                             self.preconditioner._steps = self._steps_before_capture
                         self.enabled = False
+                        # a stream whose capture was invalidated is not reused
+                        self.stream = torch.cuda.Stream()
                         self.graphs.clear()
                         self.outputs.clear()
                         self.grads.clear()
                         _native.flush_table_uploads()
                         gc.collect()
-                        return self._eager()
+                        with torch.cuda.stream(self.stream):
+                            return self._eager()
             if kind not in self.graphs:
                 return self._eager()
         with tracing.phase(f'step(graph:{kind})'):

@@ -208,8 +208,8 @@ def main() -> None:
               'conv1': st_conv1, 'conv1_bwd': st_conv1_bwd, 'stem': st_stem,
               'layer1': st_layer1, 'fwd': st_fwd, 'loss': st_loss, 'fwd_bwd': st_fwd_bwd,
               'full': st_full, **conv_stages}
-    if args.stages == 'convs':
-        args.stages = ','.join(conv_stages)
+    args.stages = ','.join(','.join(conv_stages) if t == 'convs' else t
+                           for t in args.stages.split(','))
     state = list(m.parameters()) + list(m.buffers()) + [
         opt.state[p]['momentum_buffer'] for p in m.parameters()
         if opt.state.get(p, {}).get('momentum_buffer') is not None]
