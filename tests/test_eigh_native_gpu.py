@@ -61,3 +61,33 @@ def test_mixed_refresh_two_rounds(cuda) -> None:
     torch.cuda.synchronize()
     for a64, (d, q) in zip(mats64, res2):
         _check(a64, d, q)
+
+
+_COLD = r'''
+import sys, torch
+sys.path.insert(0, {root!r})
+from tests.test_eigh_native_gpu import _factor, _check
+from distributed_kfac_pytorch_amd.ops import linalg
+mats64 = [_factor(n, 31 + i) for i, n in enumerate((1000, 2049, 1000))]
+res = linalg.eigh_many([m.float().cuda() for m in mats64])
+torch.cuda.synchronize()
+for a64, (d, q) in zip(mats64, res):
+    _check(a64, d, q)
+print('ok', sorted({{t[0] for t in linalg.last_stats['tiers']}}))
+'''
+
+
+def test_cold_process_chain_1000_2049() -> None:
+    """Round 2 saw one fault of a chain holding n = 1000 and 2049 in a COLD
+    bench process (first refresh, fresh allocator and streams); those sizes
+    run through the chains on every ResNet-50 refresh since round 3.  Here:
+    a fresh process whose first GPU work is exactly that bucket mix."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, '-c', _COLD.format(root=root)], cwd=root,
+                       capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
+    assert 'ok' in p.stdout and 'sytrd+dc' in p.stdout, p.stdout
