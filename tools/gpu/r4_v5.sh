@@ -13,3 +13,5 @@ python3 tools/trace_gaps.py $(ls /tmp/p3/*.db /tmp/p3/*/*.db 2>/dev/null | head 
 b() { name=$1; shift; env "$@" timeout -k 10 300 python3 -u bench.py --steps 100 --warmup 10 --baseline 1 --secondary-bf16 0 > $O/mw_$name.json 2> $O/mw_$name.err || { echo "$name rc=$?"; return 1; }; }
 b base A=1 && b nogtcwrw MIOPEN_DEBUG_CONV_IMPLICIT_GEMM_ASM_WRW_GTC_XDLOPS_NHWC=0 && b base2 A=1 && b nogtcwrw2 MIOPEN_DEBUG_CONV_IMPLICIT_GEMM_ASM_WRW_GTC_XDLOPS_NHWC=0
 du -sh gpurun_out
+timeout -k 10 300 python -u tools/conv1x1_probe.py > $O/conv1x1_fp32.jsonl 2> $O/conv1x1.err
+timeout -k 10 300 python -u tools/conv1x1_probe.py --bf16 > $O/conv1x1_bf16.jsonl 2>> $O/conv1x1.err
