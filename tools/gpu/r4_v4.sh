@@ -14,3 +14,4 @@ python3 tools/trace_gaps.py $(ls /tmp/p1/*.db /tmp/p1/*/*.db 2>/dev/null | head 
 timeout -k 10 400 python -u tools/graph_oop_bisect.py --stages convs,fwd_bwd,full --miopen-db --deterministic 0 --stages-quiet 1 --bf16 > $O/bisect_bf16_db.jsonl 2> $O/bisect.err
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29511 bench.py --ddp 1 --steps 30 --warmup 15 --baseline 0 --secondary-bf16 0 > $O/bench_ddp1.json 2> $O/bench_ddp1.err
 du -sh gpurun_out
+timeout -k 10 300 python -u tools/graph_oop_audit.py --bf16 --steps 3 --miopen-db --deterministic 0 > $O/audit_bf16_db.jsonl 2> $O/audit.err

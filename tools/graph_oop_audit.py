@@ -28,6 +28,11 @@ import json
 import os
 import sys
 
+if '--miopen-db' in sys.argv:
+    # the tuned MIOpen database bench.py uses (before MIOpen initialises)
+    os.environ.setdefault('MIOPEN_USER_DB_PATH', os.path.join(
+        os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'miopen_db'))
+
 import torch
 from torch import nn
 
@@ -116,10 +121,12 @@ def main() -> None:
     ap.add_argument('--inv-steps', type=int, default=100)
     ap.add_argument('--steps', type=int, default=4, help='steps before the audit (>= capture)')
     ap.add_argument('--max-report', type=int, default=40)
+    ap.add_argument('--miopen-db', action='store_true', help="use the repo's tuned MIOpen db")
+    ap.add_argument('--deterministic', type=int, default=1)
     ap.add_argument('--graph-safe', type=int, default=1,
                     help='0: plain nn.Conv2d for the strided 1x1 shortcuts (reproduces the bug)')
     args = ap.parse_args()
-    torch.backends.cudnn.deterministic = True
+    torch.backends.cudnn.deterministic = bool(args.deterministic)
     torch.backends.cudnn.benchmark = False
     dev = torch.device('cuda', 0)
     lib = _native.native()
@@ -217,13 +224,25 @@ def main() -> None:
         return [t.detach().float().cpu() for t in list(model.parameters())] + \
             [t.detach().float().cpu() for t in grads if t is not None]
 
+    def rel(x: torch.Tensor, y: torch.Tensor) -> float:
+        if not bool(torch.isfinite(y).all()):
+            return float('inf')
+        return float((x - y).abs().max() / x.abs().max().clamp_min(1e-30))
+
+    noise = [0.0]
+
     def differs(a: list, b: list) -> int:
-        return sum(int(not torch.equal(x, y)) for x, y in zip(a, b))
+        # exact with deterministic kernels; otherwise only differences far
+        # above the run-to-run noise of atomics-based kernels count
+        if args.deterministic:
+            return sum(int(not torch.equal(x, y)) for x, y in zip(a, b))
+        return sum(int(rel(x, y) > max(1e-3, 100 * noise[0])) for x, y in zip(a, b))
 
     restore()
     clean = outcome()
     restore()
     clean2 = outcome()
+    noise[0] = max([rel(x, y) for x, y in zip(clean, clean2)] or [0.0])
     det = differs(clean, clean2)
     free_blocks = []
     snap2 = torch.cuda.memory._snapshot()
@@ -236,7 +255,7 @@ def main() -> None:
             if b['state'] == 'inactive':
                 free_blocks.append((ba, b['size']))
             addr = ba + b['size']
-    pres = {'kind': kind, 'nondeterministic_tensors': det,
+    pres = {'kind': kind, 'nondeterministic_tensors': det, 'noise_rel': noise[0],
             'free_global_blocks': len(free_blocks),
             'free_global_mb': round(sum(b[1] for b in free_blocks) / 2**20, 1)}
 
