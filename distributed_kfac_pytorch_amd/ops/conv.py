@@ -30,7 +30,7 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
-__all__ = ['StridedConv1x1', 'make_graph_safe', 'is_strided_1x1']
+__all__ = ['StridedConv1x1', 'GemmConv1x1', 'make_graph_safe', 'is_strided_1x1', 'use_gemm_conv1x1']
 
 
 def is_strided_1x1(m: nn.Module) -> bool:
@@ -69,5 +69,45 @@ def make_graph_safe(model: nn.Module) -> int:
     for m in model.modules():
         if type(m) is nn.Conv2d and is_strided_1x1(m):
             m.__class__ = StridedConv1x1
+            n += 1
+    return n
+
+
+class GemmConv1x1(StridedConv1x1):
+    """``nn.Conv2d`` (1x1, unpadded, undilated, ungrouped, any stride) on
+    channels_last activations evaluated as one GEMM:
+    ``Y[NHW, Cout] = X[NHW, Cin] W[Cout, Cin]^T`` on the NHWC activation
+    matrix (a strided conv first subsamples, as ``StridedConv1x1``).  The
+    backward is two GEMMs (``dX = dY W``, ``dW = dY^T X``) through
+    hipBLASLt.  Same module, parameters and state-dict keys; other layouts
+    or groups fall back to the convolution."""
+
+    def _conv_forward(  # type: ignore[override]
+        self,
+        input: torch.Tensor,
+        weight: torch.Tensor,
+        bias: torch.Tensor | None,
+    ) -> torch.Tensor:
+        if self.groups != 1 or not input.is_contiguous(memory_format=torch.channels_last):
+            return super()._conv_forward(input, weight, bias)
+        sh, sw = self.stride
+        x = input
+        if (sh, sw) != (1, 1):
+            x = input[:, :, ::sh, ::sw].contiguous(memory_format=torch.channels_last)
+        n, c, h, w = x.shape
+        y = F.linear(x.permute(0, 2, 3, 1).reshape(n * h * w, c),
+                     weight.view(weight.shape[0], c), bias)
+        return y.view(n, h, w, -1).permute(0, 3, 1, 2)
+
+
+def use_gemm_conv1x1(model: nn.Module) -> int:
+    """Switch every 1x1 ``nn.Conv2d`` / ``StridedConv1x1`` of ``model`` (in
+    place) to ``GemmConv1x1``.  Returns the number switched."""
+    n = 0
+    for m in model.modules():
+        if (type(m) in (nn.Conv2d, StridedConv1x1) and tuple(m.kernel_size) == (1, 1)
+                and m.padding in (0, (0, 0)) and tuple(m.dilation) == (1, 1)
+                and m.groups == 1 and m.padding_mode == 'zeros'):
+            m.__class__ = GemmConv1x1
             n += 1
     return n

@@ -1,0 +1,59 @@
+"""Graph-safe / GEMM 1x1 convolution modules (ops/conv.py) against
+``F.conv2d``: identical forward values and gradients (CPU, float64)."""
+from __future__ import annotations
+
+import copy
+
+import pytest
+import torch
+from torch import nn
+
+from distributed_kfac_pytorch_amd.models.resnet import resnet50
+from distributed_kfac_pytorch_amd.ops.conv import GemmConv1x1
+from distributed_kfac_pytorch_amd.ops.conv import StridedConv1x1
+from distributed_kfac_pytorch_amd.ops.conv import make_graph_safe
+from distributed_kfac_pytorch_amd.ops.conv import use_gemm_conv1x1
+
+
+@pytest.mark.parametrize('cls', [StridedConv1x1, GemmConv1x1])
+@pytest.mark.parametrize('stride', [1, 2])
+@pytest.mark.parametrize('bias', [False, True])
+@pytest.mark.parametrize('channels_last', [False, True])
+def test_conv1x1_matches_conv2d(cls, stride, bias, channels_last) -> None:
+    torch.manual_seed(stride + 2 * bias)
+    ref = nn.Conv2d(6, 5, 1, stride=stride, bias=bias).double()
+    mod = copy.deepcopy(ref)
+    mod.__class__ = cls
+    x = torch.randn(3, 6, 9, 8, dtype=torch.float64)
+    if channels_last:
+        x = x.contiguous(memory_format=torch.channels_last)
+    xa, xb = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    ya, yb = ref(xa), mod(xb)
+    assert ya.shape == yb.shape
+    torch.testing.assert_close(yb, ya, rtol=1e-12, atol=1e-12)
+    g = torch.randn_like(ya)
+    ga = torch.autograd.grad(ya, [xa] + list(ref.parameters()), g)
+    gb = torch.autograd.grad(yb, [xb] + list(mod.parameters()), g)
+    for a, b in zip(ga, gb):
+        torch.testing.assert_close(b, a, rtol=1e-12, atol=1e-12)
+
+
+def test_resnet50_projections_are_graph_safe() -> None:
+    m = resnet50()
+    strided = [n for n, mm in m.named_modules() if isinstance(mm, StridedConv1x1)]
+    assert strided == ['layer2.0.downsample.0', 'layer3.0.downsample.0',
+                       'layer4.0.downsample.0']
+    # same state dict keys as torchvision's layout
+    assert 'layer2.0.downsample.0.weight' in m.state_dict()
+    plain = nn.Sequential(nn.Conv2d(4, 8, 1, stride=2), nn.Conv2d(8, 8, 1), nn.Conv2d(8, 8, 3))
+    assert make_graph_safe(plain) == 1
+    assert type(plain[0]) is StridedConv1x1 and type(plain[1]) is nn.Conv2d
+
+
+def test_use_gemm_conv1x1_switches_every_1x1() -> None:
+    m = resnet50()
+    n1 = sum(1 for mm in m.modules() if isinstance(mm, nn.Conv2d) and mm.kernel_size == (1, 1))
+    assert use_gemm_conv1x1(m) == n1
+    x = torch.randn(2, 3, 32, 32).contiguous(memory_format=torch.channels_last)
+    m = m.to(memory_format=torch.channels_last)
+    assert torch.isfinite(m(x)).all()
