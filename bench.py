@@ -57,6 +57,7 @@ from distributed_kfac_pytorch_amd.graphs import GraphedTrainStep  # noqa: E402
 from distributed_kfac_pytorch_amd.graphs import step_stream  # noqa: E402
 from distributed_kfac_pytorch_amd.models.resnet import get_model  # noqa: E402
 from distributed_kfac_pytorch_amd.ops.cast import enable_fused_weight_cast  # noqa: E402
+from distributed_kfac_pytorch_amd.ops.conv import use_gemm_conv1x1  # noqa: E402
 
 # The reference publishes no number.  Measured on MI355X: the
 # upstream kfac_pytorch package, same config and harness (shipped MIOpen
@@ -126,6 +127,9 @@ def parse_args() -> argparse.Namespace:
                         'with the shipped tuning db (miopen_db/)')
     p.add_argument('--profile-mark', action='store_true',
                    help='bracket the timed steps with marker kernels (rocprof windows)')
+    p.add_argument('--conv1x1', default='miopen', choices=['miopen', 'gemm'],
+                   help='1x1 convolutions: MIOpen, or one GEMM on the NHWC activation '
+                        'matrix (ops/conv.py GemmConv1x1; same values)')
     p.add_argument('--lr', type=float, default=0.0125)
     p.add_argument('--data-pool', type=int, default=8,
                    help='distinct synthetic batches cycled through the input buffer')
@@ -190,6 +194,8 @@ def run(args: argparse.Namespace, use_kfac: bool, rank: int, world: int,
         dev: torch.device, amp: bool) -> dict:
     torch.manual_seed(1234 + rank)
     model = get_model(args.model).to(dev)
+    if args.conv1x1 == 'gemm' and args.impl == 'native':
+        use_gemm_conv1x1(model)
     cl = not args.no_channels_last
     if cl:
         model = model.to(memory_format=torch.channels_last)
@@ -468,6 +474,7 @@ def main() -> None:
             'channels_last': not args.no_channels_last,
             'fused_weight_cast': bool(args.fused_weight_cast) and amp,
             'sgd_impl': args.sgd_impl,
+            'conv1x1': args.conv1x1,
             'graphs': 'step_graphs' in res,
         },
         'timing': (

@@ -15,3 +15,4 @@ b base A=1 && b nogtcwrw MIOPEN_DEBUG_CONV_IMPLICIT_GEMM_ASM_WRW_GTC_XDLOPS_NHWC
 du -sh gpurun_out
 timeout -k 10 300 python -u tools/conv1x1_probe.py > $O/conv1x1_fp32.jsonl 2> $O/conv1x1.err
 timeout -k 10 300 python -u tools/conv1x1_probe.py --bf16 > $O/conv1x1_bf16.jsonl 2>> $O/conv1x1.err
+timeout -k 10 400 python -u bench.py --steps 100 --warmup 10 --conv1x1 gemm > $O/bench_fp32_gemm1x1.json 2> $O/bench_gemm1x1.err
