@@ -297,7 +297,7 @@ __global__ void __launch_bounds__(S2_T) sb2st_kernel(float* __restrict__ ABall, 
       __hip_atomic_store(&prog[w], rho * S2_RS + (S2_RS - 1), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_WORKGROUP);
   }
-  if (abort && l == 0) atomicOr(err, 1);
+  if (abort && l == 0) atomicOr(err + b, 1);  // this matrix only
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   for (int c = threadIdx.x; c < n; c += S2_T) {

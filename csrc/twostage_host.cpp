@@ -118,7 +118,7 @@ void apply_q1(const at::Tensor& A, const at::Tensor& tau1, int64_t n, int64_t nr
 int64_t eigh_twostage_max_n() { return kfac::twostage_max_n(); }
 
 // A [b, n, n] fp32 symmetric on the GPU -> (w [b, n] ascending, X [b, n, n]
-// eigenvectors in columns, err [1] int32: nonzero if the bulge-chasing
+// eigenvectors in columns, err [batch] int32: nonzero if the bulge-chasing
 // pipeline timed out -- then w is NaN).  `times` (optional, host fp32 [5]):
 // per-stage milliseconds (synchronises; diagnostics only).
 std::vector<at::Tensor> eigh_twostage(const at::Tensor& A_in, bool timed) {
@@ -198,12 +198,15 @@ std::vector<at::Tensor> eigh_twostage(const at::Tensor& A_in, bool timed) {
   auto tau2 = at::zeros({b, nslot}, fopt);
   auto d = at::empty({b, n}, fopt);
   auto e = at::empty({b, n - 1}, fopt);
-  auto err = at::zeros({1}, A_in.options().dtype(at::kInt));
+  // one timeout flag per matrix: a timed-out pipeline poisons only its own
+  // eigenvalues (and so only its own repair in ops.linalg)
+  auto err = at::zeros({b}, A_in.options().dtype(at::kInt));
   kfac::sb2st(AB.data_ptr<float>(), ncols * 2 * B, (int)n, (int)b, V2.data_ptr<float>(),
               tau2.data_ptr<float>(), nslot, kmax, d.data_ptr<float>(), e.data_ptr<float>(),
               err.data_ptr<int>(), s);
   // a timed-out pipeline must never be installed: poison its eigenvalues
-  d = at::where(err.ne(0), at::full({}, std::numeric_limits<float>::quiet_NaN(), fopt), d);
+  d = at::where(err.ne(0).unsqueeze(1), at::full({}, std::numeric_limits<float>::quiet_NaN(), fopt),
+                d);
   mark();
   // ---- tridiagonal eigenpairs
   auto wz = tridiag_eigh_dc(d, e);

@@ -39,7 +39,7 @@ def _check(a: torch.Tensor, w: torch.Tensor, x: torch.Tensor, tol: float = 2e-5)
 def test_twostage_matches_float64(cuda, n: int) -> None:
     a = _factor(n, 1, n, cuda)
     w, x, err, _ = twostage.eigh_twostage(a)
-    assert int(err.item()) == 0
+    assert int(err.max().item()) == 0
     _check(a, w, x)
 
 
@@ -50,7 +50,7 @@ def test_twostage_batch_mixed_spectra(cuda) -> None:
     a[0].zero_()
     a[1] = torch.diag(torch.linspace(0.0, 1.0, n, device=cuda))
     w, x, err, _ = twostage.eigh_twostage(a)
-    assert int(err.item()) == 0
+    assert int(err.max().item()) == 0
     assert torch.isfinite(w).all() and torch.isfinite(x).all()
     _check(a[2:], w[2:], x[2:])
     assert float(w[0].abs().max()) == 0.0

@@ -58,7 +58,7 @@ def main() -> None:
         eye = torch.eye(n, dtype=torch.float64, device=dev)
         orth = torch.linalg.matrix_norm(xd.transpose(1, 2) @ xd - eye)
         rec = {
-            'n': n, 'batch': args.batch, 'err': int(err.item()),
+            'n': n, 'batch': args.batch, 'err': int(err.max().item()),
             'finite': bool(torch.isfinite(x).all() and torch.isfinite(w).all()),
             'eig_maxrel': float(((wd - w64).abs().amax(1) / w64.abs().amax(1)).max()),
             'resid_rel': float(res.max()), 'orth': float(orth.max()),
