@@ -114,8 +114,9 @@ __global__ void __launch_bounds__(SY_T) sytrd_col_kernel(
   // panel's current width are masked after the load, never multiplied in)
   float s2 = 0.f;
   if (fin) {
-    // partial w.v of column k-1 (one per symv row block), summed per wave
-    const int cnt = (int)ceil_div(n - k, SY_ROWS);
+    // partial w.v of column k-1 (one per symv block; the symv recorded its
+    // block count in sc[2]), summed per wave
+    const int cnt = (int)D.sc[2];
     for (int t = l; t < cnt; t += 64) s2 += D.part2[t];
   }
   const float tp = fin ? D.sc[0] : 0.f;
@@ -212,53 +213,54 @@ __global__ void __launch_bounds__(SY_T) sytrd_col_kernel(
   }
 }
 
-// symv step for column k (k <= n-2).  grid (row blocks, batch).
+// symv step for column k (k <= n-2).  grid (G, batch), G = sytrd_symv_blocks().
 //
-// The matrix stream does not depend on the reflector scalars (v is staged
-// raw; the scale is applied to each row's sum), so the first block of this
-// wave's rows is loaded before the prologue, the prologue's loads land
-// under it, and after ONE block barrier (staged v and partials visible)
-// each wave forms the scalars and its panel correction terms on its own.
+// Rows are dealt to WAVES, not blocks: global wave g = 4 b + w of the
+// member's G blocks takes rows k+1+g, k+1+g+4G, ... two at a time, so every
+// wave of a launch streams the same number of rows (+-1) whatever n - k is
+// -- with 16-row blocks, 288 blocks for one 4608 factor at column 0 put two
+// blocks on 32 of the 256 CUs.  The matrix stream does not depend on the
+// reflector scalars (v is staged raw; the scale is applied to each row's
+// sum), so each wave's first two rows are loaded before the prologue, and
+// after ONE block barrier (staged v and partials visible) each wave forms
+// the scalars and its panel correction terms on its own.  Every block
+// writes its partial w.v (0 without rows) to part2[b]; block 0 records G in
+// sc[2] for the next col step.
 __global__ void __launch_bounds__(SY_T) sytrd_symv_kernel(
     const SytrdDesc* __restrict__ descs, int k, int p) {
   const GView D = gview(descs[blockIdx.y]);
   const int n = D.n;
-  if (k >= n - 1) return;
-  const int row0 = k + 1 + blockIdx.x * SY_ROWS;
-  if (row0 >= n) return;
+  if (k >= n - 1) return;  // this member is done (its col steps stop too)
   const int i = k - p;
+  const int G = gridDim.x;
   __shared__ __attribute__((aligned(16))) float sv[SY_MAXN];
   __shared__ float ptmp[SY_MAXCH * SY_P1];
   __shared__ float red[SY_T / 64];
 
   typedef float f4 __attribute__((ext_vector_type(4)));
   const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
-  const int rw = row0 + wv * SY_RPW;
-  // v staged 16-B aligned: column col at sv[col - base], base = (k+1)
-  // rounded down to 4; columns <= k+1 hold 0 (column k+1, v = 1, is added
-  // per row from A[r][k+1] below)
+  const int W = 4 * G;                                  // waves of this member
+  const int r_first = k + 1 + (int)blockIdx.x * 4 + wv;  // this wave's first row
   const int base = (k + 1) & ~3;
   const int span = n - base;
   const bool vec = (n & 3) == 0;  // rows 16-B aligned
   const int nq = span >> 2;
-  // rows past the end read row n-1 (valid memory) and are dropped below,
-  // so the streaming loop has no per-row branch
-  const GLOBAL float* rp[SY_RPW];
-#pragma unroll
-  for (int h = 0; h < SY_RPW; ++h)
-    rp[h] = D.A + (int64_t)(rw + h < n ? rw + h : n - 1) * n + base;
-  // ---- (1) this wave's first SY_SU x SY_RPW matrix block (16-B per lane)
-  f4 a4[SY_SU][SY_RPW];
-  const bool first = vec && l + (SY_SU - 1) * 64 < nq;
+  // ---- (1) this wave's first two rows, first SY_SU column blocks
+  f4 a4[2][SY_SU];
+  const bool first = vec && r_first < n;
   if (first) {
+    const int rb = r_first + W < n ? r_first + W : r_first;
+    const GLOBAL float* p0 = D.A + (int64_t)r_first * n + base;
+    const GLOBAL float* p1 = D.A + (int64_t)rb * n + base;
 #pragma unroll
-    for (int u = 0; u < SY_SU; ++u)
-#pragma unroll
-      for (int h = 0; h < SY_RPW; ++h) a4[u][h] = *(const GLOBAL f4*)(rp[h] + 4 * (l + 64 * u));
+    for (int u = 0; u < SY_SU; ++u) {
+      const int q = l + 64 * u < nq ? l + 64 * u : 0;
+      a4[0][u] = *(const GLOBAL f4*)(p0 + 4 * q);
+      a4[1][u] = *(const GLOBAL f4*)(p1 + 4 * q);
+    }
   }
   // ---- (2) prologue: the col step's partials of column k, the raw
-  // reflector row, this lane's panel entry of column k+1, the pivot, and
-  // this wave's rows' panel entries for the V t1 + W t2 correction
+  // reflector row, this lane's panel entry of column k+1, the pivot
   const int nch = (int)ceil_div(n - k, SY_T);
   for (int t = threadIdx.x; t < nch * SY_P1; t += SY_T) ptmp[t] = D.part1[t];
   const GLOBAL float* arow = D.A + (int64_t)k * n;
@@ -271,74 +273,14 @@ __global__ void __launch_bounds__(SY_T) sytrd_symv_kernel(
   if (l < i) wa = D.Wt[(int64_t)l * n + k + 1];
   else if (l >= 32 && l - 32 < i) wa = D.A[(int64_t)(p + l - 32) * n + k + 1];
   const float alpha = D.A[(int64_t)k * n + k + 1];
-  float pv[SY_RPW], pk1[SY_RPW];
-#pragma unroll
-  for (int h = 0; h < SY_RPW; ++h) {
-    const int r = rw + h < n ? rw + h : n - 1;
-    pv[h] = 0.f;
-    if (l < i) pv[h] = D.A[(int64_t)(p + l) * n + r];
-    else if (l >= 32 && l - 32 < i) pv[h] = D.Wt[(int64_t)(l - 32) * n + r];
-    pk1[h] = D.A[(int64_t)r * n + k + 1];
-  }
   __syncthreads();
 
-  // ---- (3) y_raw = A22 a_raw for this wave's rows
-  float acc[SY_RPW];
-#pragma unroll
-  for (int h = 0; h < SY_RPW; ++h) acc[h] = 0.f;
-  if (vec) {
-    int q = l;
-    if (first) {
-#pragma unroll
-      for (int u = 0; u < SY_SU; ++u) {
-        const f4 vv = *reinterpret_cast<const f4*>(sv + 4 * (q + 64 * u));
-#pragma unroll
-        for (int h = 0; h < SY_RPW; ++h)
-          acc[h] += (a4[u][h].x * vv.x + a4[u][h].y * vv.y) +
-                    (a4[u][h].z * vv.z + a4[u][h].w * vv.w);
-      }
-      q += SY_SU * 64;
-    }
-    // SY_SU column blocks per row in flight together: SY_RPW * SY_SU 16-B
-    // loads per lane before the first FMA
-    for (; q + (SY_SU - 1) * 64 < nq; q += SY_SU * 64) {
-#pragma unroll
-      for (int u = 0; u < SY_SU; ++u)
-#pragma unroll
-        for (int h = 0; h < SY_RPW; ++h)
-          a4[u][h] = *(const GLOBAL f4*)(rp[h] + 4 * (q + 64 * u));
-#pragma unroll
-      for (int u = 0; u < SY_SU; ++u) {
-        const f4 vv = *reinterpret_cast<const f4*>(sv + 4 * (q + 64 * u));
-#pragma unroll
-        for (int h = 0; h < SY_RPW; ++h)
-          acc[h] += (a4[u][h].x * vv.x + a4[u][h].y * vv.y) +
-                    (a4[u][h].z * vv.z + a4[u][h].w * vv.w);
-      }
-    }
-    for (; q < nq; q += 64) {
-      const f4 vv = *reinterpret_cast<const f4*>(sv + 4 * q);
-#pragma unroll
-      for (int h = 0; h < SY_RPW; ++h) {
-        const f4 a = *(const GLOBAL f4*)(rp[h] + 4 * q);
-        acc[h] += (a.x * vv.x + a.y * vv.y) + (a.z * vv.z + a.w * vv.w);
-      }
-    }
-  } else {
-    for (int c = l; c < span; c += 64) {
-      const float vc = sv[c];
-#pragma unroll
-      for (int h = 0; h < SY_RPW; ++h)
-        if (rw + h < n) acc[h] += D.A[(int64_t)(rw + h) * n + base + c] * vc;
-    }
-  }
-
-  // ---- (4) reflector scalars, per wave: ||x||^2 and this lane's
+  // ---- (3) reflector scalars, per wave: ||x||^2 and this lane's
   // V^T x / W^T x partial totals (lane l needs entry 1 + l either way)
   float xn2 = 0.f, xl = 0.f;
   for (int c = 0; c < nch; ++c) {
     xn2 += ptmp[c * SY_P1];
-    if (l + 1 < SY_P1) xl += ptmp[c * SY_P1 + 1 + l];
+    xl += ptmp[c * SY_P1 + 1 + l];
   }
   float tau_k, beta, scale;
   if (xn2 == 0.f) {
@@ -355,24 +297,79 @@ __global__ void __launch_bounds__(SY_T) sytrd_symv_kernel(
     D.tau[k] = tau_k;
     D.sc[0] = tau_k;
     D.sc[1] = scale;
+    D.sc[2] = (float)G;
   }
   // t1 = W^T v (lanes < i), t2 = V^T v (lanes 32 .. 32 + i)
   const bool tlive = l < i || (l >= 32 && l - 32 < i);
   const float tl = tlive ? wa + scale * xl : 0.f;
 
-  // ---- (5) w = tau (A22 v - V t1 - W t2) for this wave's rows
+  // ---- (4) rows: y_raw = A22 a_raw, then w = tau (A22 v - V t1 - W t2)
   float pd = 0.f;
+  bool pre = first;
+  for (int r0 = r_first; r0 < n; r0 += 2 * W) {
+    const int r1 = r0 + W;
+    const bool two = r1 < n;
+    const int r1c = two ? r1 : r0;
+    // this pair's panel entries (lanes < i: V rows, 32.. : W rows) and
+    // column k+1 entries
+    float pv0 = 0.f, pv1 = 0.f;
+    if (l < i) {
+      pv0 = D.A[(int64_t)(p + l) * n + r0];
+      pv1 = D.A[(int64_t)(p + l) * n + r1c];
+    } else if (l >= 32 && l - 32 < i) {
+      pv0 = D.Wt[(int64_t)(l - 32) * n + r0];
+      pv1 = D.Wt[(int64_t)(l - 32) * n + r1c];
+    }
+    const float pk0 = D.A[(int64_t)r0 * n + k + 1];
+    const float pk1 = D.A[(int64_t)r1c * n + k + 1];
+    float acc0 = 0.f, acc1 = 0.f;
+    if (vec) {
+      const GLOBAL float* p0 = D.A + (int64_t)r0 * n + base;
+      const GLOBAL float* p1 = D.A + (int64_t)r1c * n + base;
+      int q = l;
+      for (; q < nq; q += 64 * SY_SU) {
+        if (!pre) {
 #pragma unroll
-  for (int h = 0; h < SY_RPW; ++h) {
-    const int r = rw + h;
-    if (r >= n) break;
+          for (int u = 0; u < SY_SU; ++u) {
+            const int qq = q + 64 * u < nq ? q + 64 * u : 0;
+            a4[0][u] = *(const GLOBAL f4*)(p0 + 4 * qq);
+            a4[1][u] = *(const GLOBAL f4*)(p1 + 4 * qq);
+          }
+        }
+        pre = false;
+#pragma unroll
+        for (int u = 0; u < SY_SU; ++u) {
+          if (q + 64 * u < nq) {
+            const f4 vv = *reinterpret_cast<const f4*>(sv + 4 * (q + 64 * u));
+            acc0 += (a4[0][u].x * vv.x + a4[0][u].y * vv.y) +
+                    (a4[0][u].z * vv.z + a4[0][u].w * vv.w);
+            acc1 += (a4[1][u].x * vv.x + a4[1][u].y * vv.y) +
+                    (a4[1][u].z * vv.z + a4[1][u].w * vv.w);
+          }
+        }
+      }
+      pre = false;  // (lanes past nq never entered the loop)
+    } else {
+      for (int c = l; c < span; c += 64) {
+        const float vc = sv[c];
+        acc0 += D.A[(int64_t)r0 * n + base + c] * vc;
+        acc1 += D.A[(int64_t)r1c * n + base + c] * vc;
+      }
+    }
     // y = A22 v with v = [1, scale * a]
-    const float y = pk1[h] + scale * wave_sum_uniform(acc[h]);
-    const float corr = wave_sum_uniform(pv[h] * tl);
-    const float wr = tau_k * (y - corr);
+    const float y0 = pk0 + scale * wave_sum_uniform(acc0);
+    const float c0 = wave_sum_uniform(pv0 * tl);
+    const float w0 = tau_k * (y0 - c0);
+    const float y1 = pk1 + scale * wave_sum_uniform(acc1);
+    const float c1 = wave_sum_uniform(pv1 * tl);
+    const float w1 = tau_k * (y1 - c1);
     if (l == 0) {
-      D.Wt[(int64_t)i * n + r] = wr;
-      pd += wr * (r == k + 1 ? 1.f : scale * sv[r - base]);
+      D.Wt[(int64_t)i * n + r0] = w0;
+      pd += w0 * (r0 == k + 1 ? 1.f : scale * sv[r0 - base]);
+      if (two) {
+        D.Wt[(int64_t)i * n + r1] = w1;
+        pd += w1 * (r1 == k + 1 ? 1.f : scale * sv[r1 - base]);
+      }
     }
   }
   pd = block_sum(pd, red);
@@ -440,6 +437,19 @@ __global__ void __launch_bounds__(SY_T) sytrd_syr2k_kernel(
 
 }  // namespace
 
+// symv blocks per member for `rows` rows of the largest member: the whole
+// launch (blocks x batch) is sized to ~3 resident 256-thread blocks on each
+// of the 256 CUs (41 KB of LDS each), with every wave streaming the same
+// number of rows
+int sytrd_symv_blocks(int rows, int batch) {
+  if (rows <= 0) return 1;
+  const int waves = 3 * 256 * 4;
+  const int per = (int)ceil_div((int64_t)rows * batch, (int64_t)waves);  // rows per wave
+  int g = (int)ceil_div((int64_t)rows, (int64_t)4 * per);
+  if (g > SY_MAXROWBLK) g = SY_MAXROWBLK;
+  return g < 1 ? 1 : g;
+}
+
 // Host driver: descs is a device table of `batch` descriptors, ns the host
 // copy of their sizes.  Issues 2 launches per column of the largest matrix
 // plus 2 per panel, all on `stream`, no host sync.
@@ -458,7 +468,7 @@ void sytrd_batched_range(const SytrdDesc* descs_dev, const int* ns, int batch,
                          dim3(SY_T), 0, stream, descs_dev, k, p, 0);
       if (k < maxn - 1) {
         hipLaunchKernelGGL(sytrd_symv_kernel,
-                           dim3((unsigned)ceil_div(rem - 1, SY_ROWS), batch),
+                           dim3((unsigned)sytrd_symv_blocks(rem - 1, batch), batch),
                            dim3(SY_T), 0, stream, descs_dev, k, p);
       }
     }

@@ -63,14 +63,15 @@ class StridedConv1x1(nn.Conv2d):
 
 
 def make_graph_safe(model: nn.Module) -> int:
-    """Switch every strided 1x1 ``nn.Conv2d`` of ``model`` (in place, same
-    parameters) to ``StridedConv1x1``.  Returns the number switched."""
-    n = 0
-    for m in model.modules():
-        if type(m) is nn.Conv2d and is_strided_1x1(m):
-            m.__class__ = StridedConv1x1
-            n += 1
-    return n
+    """Switch every 1x1 convolution of ``model`` (in place, same parameters)
+    to ``GemmConv1x1``: on channels_last activations its forward and both
+    backward products are hipBLASLt GEMMs, so no MIOpen 1x1 solver runs in a
+    captured step.  Besides the strided backward-data above, the tuned MIOpen
+    database's bf16 backward-weights solver of some stride-1 1x1 shapes
+    (``layer2.0.conv1``, ``layer2.2.conv3``) also read free global memory
+    from a graph (profiles/graph_oop_r4/bisect_convs_bf16_tuned_db.jsonl).
+    Returns the number switched."""
+    return use_gemm_conv1x1(model)
 
 
 class GemmConv1x1(StridedConv1x1):

@@ -45,9 +45,11 @@ def test_resnet50_projections_are_graph_safe() -> None:
                        'layer4.0.downsample.0']
     # same state dict keys as torchvision's layout
     assert 'layer2.0.downsample.0.weight' in m.state_dict()
+    # graph-safe: every 1x1 conv becomes a GEMM conv, other kernels stay
     plain = nn.Sequential(nn.Conv2d(4, 8, 1, stride=2), nn.Conv2d(8, 8, 1), nn.Conv2d(8, 8, 3))
-    assert make_graph_safe(plain) == 1
-    assert type(plain[0]) is StridedConv1x1 and type(plain[1]) is nn.Conv2d
+    assert make_graph_safe(plain) == 2
+    assert type(plain[0]) is GemmConv1x1 and type(plain[1]) is GemmConv1x1
+    assert type(plain[2]) is nn.Conv2d
 
 
 def test_use_gemm_conv1x1_switches_every_1x1() -> None:
