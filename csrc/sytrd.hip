@@ -74,6 +74,14 @@ __device__ __forceinline__ GView gview(const SytrdDesc& s) {
           (GLOBAL float*)s.part2, (GLOBAL float*)s.sc,    s.n};
 }
 
+// Pins every descriptor field in SGPRs at the call site.  Without it the
+// compiler loads n first, branches on it, and only then loads the pointers:
+// two dependent scalar round trips at the head of every chain kernel.
+__device__ __forceinline__ void pin_desc(const GView& D) {
+  asm volatile("" ::"s"(D.A), "s"(D.Wt), "s"(D.d), "s"(D.e), "s"(D.tau), "s"(D.part1),
+               "s"(D.part2), "s"(D.sc), "s"(D.n));
+}
+
 __device__ __forceinline__ float block_sum(float v, float* red) {
   v = wave_sum_uniform(v);
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
@@ -96,8 +104,9 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 // lane broadcasts, no LDS round trip -- so the kernel has one block
 // barrier, before the final cross-wave sums.
 __global__ void __launch_bounds__(SY_T) sytrd_col_kernel(
-    const SytrdDesc* __restrict__ descs, int k, int p, int fin_only) {
+    const SytrdDesc* __restrict__ descs, int k, int p, int fin_only, int cnt) {
   const GView D = gview(descs[blockIdx.y]);
+  pin_desc(D);
   const int n = D.n;
   if (k >= n) return;
   const int r0 = k + blockIdx.x * SY_T;
@@ -109,29 +118,11 @@ __global__ void __launch_bounds__(SY_T) sytrd_col_kernel(
   __shared__ float wred[SY_T / 64][SY_P1];
   const bool fin = i > 0;  // column k-1 to finalise
 
-  // ---- every global load of this thread first, all in flight together
-  // (rows p + j < n and Wt rows j < NB are always in bounds; values past the
-  // panel's current width are masked after the load, never multiplied in)
-  float s2 = 0.f;
-  if (fin) {
-    // partial w.v of column k-1 (one per symv block; the symv recorded its
-    // block count in sc[2]), summed per wave
-    const int cnt = (int)D.sc[2];
-    for (int t = l; t < cnt; t += 64) s2 += D.part2[t];
-  }
-  const float tp = fin ? D.sc[0] : 0.f;
-  const float sprev = fin ? D.sc[1] : 0.f;
-  // lane j < i of every wave: W[k, j] and V_j[k] of the panel
-  float cw_raw = 0.f, cv_raw = 0.f;
-  if (l < i && !fin_only) {
-    cw_raw = D.Wt[(int64_t)l * n + k];
-    cv_raw = l == i - 1 ? 1.f : D.A[(int64_t)(p + l) * n + k];  // V_{i-1}[k] = 1
-  }
-  float vraw = 0.f, wraw = 0.f;
-  if (act && fin) {
-    vraw = r == k ? 1.f : D.A[(int64_t)(k - 1) * n + r];
-    wraw = D.Wt[(int64_t)(i - 1) * n + r];
-  }
+  // ---- every global load of this thread first, all in flight together:
+  // nothing but the descriptor is loaded before them (cnt, the previous
+  // symv's block count, is a kernel argument; rows p + j < n and Wt rows
+  // j < NB are always in bounds; values past the panel's current width are
+  // masked after the load, never multiplied in)
   float vj[SY_NB], wj[SY_NB];
   float a = 0.f;
 #pragma unroll
@@ -147,6 +138,31 @@ __global__ void __launch_bounds__(SY_T) sytrd_col_kernel(
       vj[j] = D.A[(int64_t)pj * n + r];
       wj[j] = D.Wt[(int64_t)j * n + r];
     }
+  }
+  float s2 = 0.f;
+  if (fin) {
+    // partial w.v of column k-1 (one per symv block), summed per wave
+    // (G <= SY_MAXROWBLK: a fixed unrolled count, clamped loads, no
+    // memory wait per trip)
+#pragma unroll
+    for (int u = 0; u < SY_MAXROWBLK / 64; ++u) {
+      const int t = l + 64 * u;
+      const float v = D.part2[t < cnt ? t : cnt - 1];
+      s2 += t < cnt ? v : 0.f;
+    }
+  }
+  const float tp = fin ? D.sc[0] : 0.f;
+  const float sprev = fin ? D.sc[1] : 0.f;
+  // lane j < i of every wave: W[k, j] and V_j[k] of the panel
+  float cw_raw = 0.f, cv_raw = 0.f;
+  if (l < i && !fin_only) {
+    cw_raw = D.Wt[(int64_t)l * n + k];
+    cv_raw = l == i - 1 ? 1.f : D.A[(int64_t)(p + l) * n + k];  // V_{i-1}[k] = 1
+  }
+  float vraw = 0.f, wraw = 0.f;
+  if (act && fin) {
+    vraw = r == k ? 1.f : D.A[(int64_t)(k - 1) * n + r];
+    wraw = D.Wt[(int64_t)(i - 1) * n + r];
   }
 
   float alpha2 = 0.f;
@@ -193,12 +209,15 @@ __global__ void __launch_bounds__(SY_T) sytrd_col_kernel(
   if (l == 0) wred[w][0] = s0;
 #pragma unroll
   for (int j = 0; j < SY_NB; ++j) {
-    // independent reductions (j >= i contribute zeros and are not stored)
-    const float sw = wave_sum_uniform(wj[j] * x);
-    const float sv = wave_sum_uniform(vj[j] * x);
-    if (l == 0 && j < i) {
-      wred[w][1 + j] = sw;
-      wred[w][1 + SY_NB + j] = sv;
+    // independent reductions; panel columns j >= i are zero and skipped
+    // (i is uniform: a scalar branch)
+    if (j < i) {
+      const float sw = wave_sum_uniform(wj[j] * x);
+      const float sv = wave_sum_uniform(vj[j] * x);
+      if (l == 0) {
+        wred[w][1 + j] = sw;
+        wred[w][1 + SY_NB + j] = sv;
+      }
     }
   }
   __syncthreads();
@@ -224,11 +243,12 @@ __global__ void __launch_bounds__(SY_T) sytrd_col_kernel(
 // sum), so each wave's first two rows are loaded before the prologue, and
 // after ONE block barrier (staged v and partials visible) each wave forms
 // the scalars and its panel correction terms on its own.  Every block
-// writes its partial w.v (0 without rows) to part2[b]; block 0 records G in
-// sc[2] for the next col step.
+// writes its partial w.v (0 without rows) to part2[b]; the next col step
+// gets G as an argument.
 __global__ void __launch_bounds__(SY_T) sytrd_symv_kernel(
     const SytrdDesc* __restrict__ descs, int k, int p) {
   const GView D = gview(descs[blockIdx.y]);
+  pin_desc(D);
   const int n = D.n;
   if (k >= n - 1) return;  // this member is done (its col steps stop too)
   const int i = k - p;
@@ -261,18 +281,41 @@ __global__ void __launch_bounds__(SY_T) sytrd_symv_kernel(
   }
   // ---- (2) prologue: the col step's partials of column k, the raw
   // reflector row, this lane's panel entry of column k+1, the pivot
-  const int nch = (int)ceil_div(n - k, SY_T);
-  for (int t = threadIdx.x; t < nch * SY_P1; t += SY_T) ptmp[t] = D.part1[t];
-  const GLOBAL float* arow = D.A + (int64_t)k * n;
-  for (int c = threadIdx.x; c < span; c += SY_T) {
-    const int col = base + c;
-    sv[c] = col <= k + 1 ? 0.f : arow[col];
-  }
+  // (fixed-count unrolled loads: a plain strided loop is vectorised 8 wide
+  // with a full memory wait per trip -- 3-4 dependent round trips at n=4608)
   // lane l < i: W[k+1, l]; lane 32 <= l < 32 + i: V_{l-32}[k+1]
   float wa = 0.f;
   if (l < i) wa = D.Wt[(int64_t)l * n + k + 1];
   else if (l >= 32 && l - 32 < i) wa = D.A[(int64_t)(p + l - 32) * n + k + 1];
   const float alpha = D.A[(int64_t)k * n + k + 1];
+  const int nch = (int)ceil_div(n - k, SY_T);
+  const int np1 = nch * SY_P1;
+  constexpr int PT = (SY_MAXCH * SY_P1 + SY_T - 1) / SY_T;
+  float pst[PT];
+#pragma unroll
+  for (int u = 0; u < PT; ++u) {
+    const int t = threadIdx.x + SY_T * u;
+    pst[u] = D.part1[t < np1 ? t : np1 - 1];  // clamped: no branch per load
+  }
+  const GLOBAL float* arow = D.A + (int64_t)k * n;
+  constexpr int VT = SY_MAXN / SY_T;
+  float vst[VT];
+#pragma unroll
+  for (int u = 0; u < VT; ++u) {
+    const int c = threadIdx.x + SY_T * u;
+    const float v = arow[c < span ? base + c : n - 1];
+    vst[u] = base + c > k + 1 ? v : 0.f;
+  }
+#pragma unroll
+  for (int u = 0; u < PT; ++u) {
+    const int t = threadIdx.x + SY_T * u;
+    if (t < np1) ptmp[t] = pst[u];
+  }
+#pragma unroll
+  for (int u = 0; u < VT; ++u) {
+    const int c = threadIdx.x + SY_T * u;
+    if (c < span) sv[c] = vst[u];
+  }
   __syncthreads();
 
   // ---- (3) reflector scalars, per wave: ||x||^2 and this lane's
@@ -297,7 +340,6 @@ __global__ void __launch_bounds__(SY_T) sytrd_symv_kernel(
     D.tau[k] = tau_k;
     D.sc[0] = tau_k;
     D.sc[1] = scale;
-    D.sc[2] = (float)G;
   }
   // t1 = W^T v (lanes < i), t2 = V^T v (lanes 32 .. 32 + i)
   const bool tlive = l < i || (l >= 32 && l - 32 < i);
@@ -381,6 +423,7 @@ __global__ void __launch_bounds__(SY_T) sytrd_symv_kernel(
 __global__ void __launch_bounds__(SY_T) sytrd_syr2k_kernel(
     const SytrdDesc* __restrict__ descs, int q, int p) {
   const GView D = gview(descs[blockIdx.z]);
+  pin_desc(D);
   const int n = D.n;
   if (q >= n) return;
   const int r0 = q + blockIdx.y * 64, c0 = q + blockIdx.x * 64;
@@ -464,8 +507,10 @@ void sytrd_batched_range(const SytrdDesc* descs_dev, const int* ns, int batch,
     const int q = (p + SY_NB < maxn) ? p + SY_NB : maxn;
     for (int k = p; k < q; ++k) {
       const int rem = maxn - k;
+      // the previous column's symv had maxn - k rows in the largest member
       hipLaunchKernelGGL(sytrd_col_kernel, dim3((unsigned)ceil_div(rem, SY_T), batch),
-                         dim3(SY_T), 0, stream, descs_dev, k, p, 0);
+                         dim3(SY_T), 0, stream, descs_dev, k, p, 0,
+                         sytrd_symv_blocks(maxn - k, batch));
       if (k < maxn - 1) {
         hipLaunchKernelGGL(sytrd_symv_kernel,
                            dim3((unsigned)sytrd_symv_blocks(rem - 1, batch), batch),
@@ -475,7 +520,8 @@ void sytrd_batched_range(const SytrdDesc* descs_dev, const int* ns, int batch,
     if (q < maxn) {
       const int rem = maxn - q;
       hipLaunchKernelGGL(sytrd_col_kernel, dim3((unsigned)ceil_div(rem, SY_T), batch),
-                         dim3(SY_T), 0, stream, descs_dev, q, p, 1);
+                         dim3(SY_T), 0, stream, descs_dev, q, p, 1,
+                         sytrd_symv_blocks(maxn - q, batch));
       const unsigned tiles = (unsigned)ceil_div(rem, 64);
       hipLaunchKernelGGL(sytrd_syr2k_kernel, dim3(tiles, tiles, batch), dim3(SY_T), 0,
                          stream, descs_dev, q, p);

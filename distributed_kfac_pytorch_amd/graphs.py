@@ -116,16 +116,12 @@ def step_stream(device: torch.device | int | None = None) -> torch.cuda.Stream:
 
 def _graph_safe(model: torch.nn.Module | None, preconditioner: Any) -> int:
     from distributed_kfac_pytorch_amd.ops.conv import StridedConv1x1
-    from distributed_kfac_pytorch_amd.ops.conv import is_strided_1x1
     from distributed_kfac_pytorch_amd.ops.conv import make_graph_safe
 
     n = make_graph_safe(model) if model is not None else 0
     for module in list(getattr(preconditioner, '_layers', None) or {}):
         if type(module) in (torch.nn.Conv2d, StridedConv1x1) and module.kernel_size == (1, 1):
             n += make_graph_safe(module)
-        elif type(module) is torch.nn.Conv2d and is_strided_1x1(module):
-            module.__class__ = StridedConv1x1
-            n += 1
     return n
 
 

@@ -26,11 +26,14 @@ input and the module's stride) and checkpoints are unchanged.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 from torch import nn
 
-__all__ = ['StridedConv1x1', 'GemmConv1x1', 'make_graph_safe', 'is_strided_1x1', 'use_gemm_conv1x1']
+__all__ = ['StridedConv1x1', 'GemmConv1x1', 'make_graph_safe', 'is_strided_1x1', 'use_gemm_conv1x1',
+           'disable_unsafe_miopen_solvers']
 
 
 def is_strided_1x1(m: nn.Module) -> bool:
@@ -62,16 +65,50 @@ class StridedConv1x1(nn.Conv2d):
         return F.conv2d(sub, weight, bias, 1, 0, 1, self.groups)
 
 
-def make_graph_safe(model: nn.Module) -> int:
-    """Switch every 1x1 convolution of ``model`` (in place, same parameters)
-    to ``GemmConv1x1``: on channels_last activations its forward and both
-    backward products are hipBLASLt GEMMs, so no MIOpen 1x1 solver runs in a
-    captured step.  Besides the strided backward-data above, the tuned MIOpen
-    database's bf16 backward-weights solver of some stride-1 1x1 shapes
-    (``layer2.0.conv1``, ``layer2.2.conv3``) also read free global memory
-    from a graph (profiles/graph_oop_r4/bisect_convs_bf16_tuned_db.jsonl).
-    Returns the number switched."""
-    return use_gemm_conv1x1(model)
+def make_graph_safe(model: nn.Module, mode: str | None = None) -> int:
+    """Make the 1x1 convolutions of ``model`` safe to capture (in place, same
+    parameters).  Returns the number switched.
+
+    ``mode`` (default ``KFAC_GRAPH_SAFE_CONV``, else ``strided``):
+
+    * ``strided``: strided 1x1 convolutions become ``StridedConv1x1``; the
+      stride-1 ones stay on MIOpen.  Besides the strided backward-data above,
+      the tuned database's bf16 backward-weights solver of some stride-1 1x1
+      shapes (``layer2.0.conv1``, ``layer2.2.conv3``: the assembly
+      ``ConvAsmImplicitGemmGTCDynamicWrwXdlopsNHWC``, with a workspace) also
+      read free global memory from a graph
+      (profiles/graph_oop_r4/bisect_convs_bf16_tuned_db.jsonl);
+      ``disable_unsafe_miopen_solvers()`` takes that solver out.
+    * ``gemm``: every 1x1 convolution becomes ``GemmConv1x1`` (hipBLASLt
+      GEMMs, no MIOpen 1x1 solver in the graph at all) -- slower than MIOpen
+      at the 56x56 stages (profiles/conv1x1_probe_r4.jsonl).
+    """
+    mode = mode or os.environ.get('KFAC_GRAPH_SAFE_CONV', 'strided')
+    if mode == 'gemm':
+        return use_gemm_conv1x1(model)
+    if mode != 'strided':
+        raise ValueError(f'KFAC_GRAPH_SAFE_CONV={mode!r}: expected strided or gemm')
+    n = 0
+    for m in model.modules():
+        if type(m) is nn.Conv2d and is_strided_1x1(m):
+            m.__class__ = StridedConv1x1
+            n += 1
+    return n
+
+
+# MIOpen solvers that read memory outside a captured graph (see
+# make_graph_safe); MIOpen reads these switches once, at its first use of
+# the solver, so they are set when the package is imported.
+UNSAFE_MIOPEN_SOLVERS = ('MIOPEN_DEBUG_CONV_IMPLICIT_GEMM_ASM_WRW_GTC_XDLOPS_NHWC',)
+
+
+def disable_unsafe_miopen_solvers() -> None:
+    """Turn the solvers in ``UNSAFE_MIOPEN_SOLVERS`` off unless the user set
+    them (``KFAC_MIOPEN_SAFE=0`` leaves MIOpen untouched)."""
+    if os.environ.get('KFAC_MIOPEN_SAFE', '1') == '0':
+        return
+    for var in UNSAFE_MIOPEN_SOLVERS:
+        os.environ.setdefault(var, '0')
 
 
 class GemmConv1x1(StridedConv1x1):

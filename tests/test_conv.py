@@ -45,11 +45,27 @@ def test_resnet50_projections_are_graph_safe() -> None:
                        'layer4.0.downsample.0']
     # same state dict keys as torchvision's layout
     assert 'layer2.0.downsample.0.weight' in m.state_dict()
-    # graph-safe: every 1x1 conv becomes a GEMM conv, other kernels stay
+    # graph-safe (default 'strided'): only the strided 1x1 conv is switched
     plain = nn.Sequential(nn.Conv2d(4, 8, 1, stride=2), nn.Conv2d(8, 8, 1), nn.Conv2d(8, 8, 3))
-    assert make_graph_safe(plain) == 2
+    assert make_graph_safe(plain, 'strided') == 1
+    assert type(plain[0]) is StridedConv1x1 and type(plain[1]) is nn.Conv2d
+    assert type(plain[2]) is nn.Conv2d
+    # 'gemm': every 1x1 conv becomes a GEMM conv, other kernels stay
+    plain = nn.Sequential(nn.Conv2d(4, 8, 1, stride=2), nn.Conv2d(8, 8, 1), nn.Conv2d(8, 8, 3))
+    assert make_graph_safe(plain, 'gemm') == 2
     assert type(plain[0]) is GemmConv1x1 and type(plain[1]) is GemmConv1x1
     assert type(plain[2]) is nn.Conv2d
+    with pytest.raises(ValueError):
+        make_graph_safe(plain, 'nope')
+
+
+def test_unsafe_miopen_solvers_disabled_on_import() -> None:
+    import os
+
+    import distributed_kfac_pytorch_amd  # noqa: F401
+    from distributed_kfac_pytorch_amd.ops.conv import UNSAFE_MIOPEN_SOLVERS
+    for var in UNSAFE_MIOPEN_SOLVERS:
+        assert os.environ.get(var) is not None
 
 
 def test_use_gemm_conv1x1_switches_every_1x1() -> None:
