@@ -115,8 +115,6 @@ def parse_args() -> argparse.Namespace:
                         '(distributed_kfac_pytorch_amd.graphs.GraphedTrainStep; '
                         'single-rank jobs only, second-order update steps stay '
                         'eager); 0: every step eager')
-    p.add_argument('--graphs-bf16', type=int, default=0,
-                   help='1: also replay bf16 autocast steps from graphs (off: see run())')
     p.add_argument('--sgd-impl', default='fused', choices=['fused', 'foreach'],
                    help='torch.optim.SGD implementation (same math)')
     p.add_argument('--fused-weight-cast', type=int, default=1,
@@ -205,8 +203,6 @@ def run(args: argparse.Namespace, use_kfac: bool, rank: int, world: int,
         enable_fused_weight_cast(model)
     use_graphs = bool(args.graphs) and args.impl == 'native' and (
         world == 1 or os.environ.get('KFAC_STEP_GRAPHS_MULTI', '0') == '1')
-    if amp and not args.graphs_bf16:
-        use_graphs = False
     if world > 1 or args.ddp:
         # under graphs DDP is built on the stream the steps run and are
         # captured on (its reducer holds the AccumulateGrad nodes)
@@ -274,7 +270,10 @@ def run(args: argparse.Namespace, use_kfac: bool, rank: int, world: int,
 
     runner = None
     if use_graphs:
-        runner = GraphedTrainStep(forward_backward, opt, precond, model=model)
+        # bf16: every 1x1 conv as GEMMs inside the graphs (the tuned MIOpen
+        # bf16 backward-weights solvers read outside it: ops/conv.py)
+        runner = GraphedTrainStep(forward_backward, opt, precond, model=model,
+                                  conv_mode='gemm' if amp else None)
 
     def step() -> None:
         next_batch()

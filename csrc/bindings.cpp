@@ -109,7 +109,8 @@ int64_t sytrd_max_n();
 std::vector<at::Tensor> spd_inverse_blocked(at::Tensor F, double damping);
 std::vector<at::Tensor> sytrd_reduce(std::vector<at::Tensor> stacks);
 std::vector<at::Tensor> sytrd_begin(std::vector<at::Tensor> stacks);
-void sytrd_advance(at::Tensor descs, std::vector<int64_t> sizes, int64_t k0, int64_t k1);
+void sytrd_advance(at::Tensor descs, std::vector<int64_t> sizes, int64_t k0, int64_t k1,
+                   int64_t waves);
 
 namespace {
 
@@ -1176,7 +1177,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("spd_inverse_blocked", &spd_inverse_blocked, py::call_guard<py::gil_scoped_release>());
   m.def("sytrd_reduce", &sytrd_reduce, py::call_guard<py::gil_scoped_release>());
   m.def("sytrd_begin", &sytrd_begin, py::call_guard<py::gil_scoped_release>());
-  m.def("sytrd_advance", &sytrd_advance, py::call_guard<py::gil_scoped_release>());
+  m.def("sytrd_advance", &sytrd_advance, py::arg("descs"), py::arg("sizes"), py::arg("k0"),
+        py::arg("k1"), py::arg("waves") = 0, py::call_guard<py::gil_scoped_release>());
   m.def("rocsolver_eigh", &rocsolver_eigh, py::call_guard<py::gil_scoped_release>(),
         py::arg("A"), py::arg("algo") = 0,
         py::arg("max_sweeps") = 100, py::arg("tol") = 1e-7);

@@ -133,7 +133,7 @@ int sytrd_maxrowblk();
 void sytrd_batched(const SytrdDesc* descs_dev, const int* ns, int batch,
                    hipStream_t stream);
 void sytrd_batched_range(const SytrdDesc* descs_dev, const int* ns, int batch,
-                         int k_begin, int k_end, hipStream_t stream);
+                         int k_begin, int k_end, hipStream_t stream, int waves);
 }  // namespace kfac
 
 int64_t sytrd_max_n() { return kfac::sytrd_max_n(); }
@@ -214,21 +214,23 @@ std::vector<at::Tensor> sytrd_reduce(std::vector<at::Tensor> stacks) {
 // in the returned tensors: [descs, work, d0, e0, tau0, ...]); each
 // sytrd_advance(state, sizes, k0, k1) issues the panels covering columns
 // [k0, k1) (k0 a multiple of the panel width) on the current stream.  After
-// advancing past n, every matrix of size <= n is fully reduced.
+// advancing past n, every matrix of size <= n is fully reduced.  `waves`
+// sizes each symv launch (0: the whole chip, see sytrd_symv_blocks).
 std::vector<at::Tensor> sytrd_begin(std::vector<at::Tensor> stacks) {
   c10::hip::HIPGuardMasqueradingAsCUDA g(stacks.at(0).device());
   std::vector<int> ns;
   return sytrd_setup(stacks, ns);
 }
 
-void sytrd_advance(at::Tensor descs, std::vector<int64_t> sizes, int64_t k0, int64_t k1) {
+void sytrd_advance(at::Tensor descs, std::vector<int64_t> sizes, int64_t k0, int64_t k1,
+                   int64_t waves) {
   TORCH_CHECK(k0 % kfac::sytrd_nb() == 0, "segments start on panel boundaries");
   c10::hip::HIPGuardMasqueradingAsCUDA g(descs.device());
   hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
   std::vector<int> ns(sizes.begin(), sizes.end());
   TORCH_CHECK((int64_t)ns.size() * (int64_t)sizeof(kfac::SytrdDesc) == descs.numel());
   kfac::sytrd_batched_range(reinterpret_cast<const kfac::SytrdDesc*>(descs.data_ptr()),
-                            ns.data(), (int)ns.size(), (int)k0, (int)k1, s);
+                            ns.data(), (int)ns.size(), (int)k0, (int)k1, s, (int)waves);
 }
 
 // ---------------------------------------------------------------------------

@@ -481,12 +481,13 @@ __global__ void __launch_bounds__(SY_T) sytrd_syr2k_kernel(
 }  // namespace
 
 // symv blocks per member for `rows` rows of the largest member: the whole
-// launch (blocks x batch) is sized to ~3 resident 256-thread blocks on each
-// of the 256 CUs (41 KB of LDS each), with every wave streaming the same
-// number of rows
-int sytrd_symv_blocks(int rows, int batch) {
+// launch (blocks x batch) is sized to `waves` waves (default ~3 resident
+// 256-thread blocks on each of the 256 CUs), with every wave streaming the
+// same number of rows.  Chains that run concurrently on other lanes get a
+// smaller budget (ops/linalg.py, KFAC_SYTRD_WAVES).
+int sytrd_symv_blocks(int rows, int batch, int waves) {
   if (rows <= 0) return 1;
-  const int waves = 3 * 256 * 4;
+  if (waves <= 0) waves = 3 * 256 * 4;
   const int per = (int)ceil_div((int64_t)rows * batch, (int64_t)waves);  // rows per wave
   int g = (int)ceil_div((int64_t)rows, (int64_t)4 * per);
   if (g > SY_MAXROWBLK) g = SY_MAXROWBLK;
@@ -497,7 +498,7 @@ int sytrd_symv_blocks(int rows, int batch) {
 // copy of their sizes.  Issues 2 launches per column of the largest matrix
 // plus 2 per panel, all on `stream`, no host sync.
 void sytrd_batched_range(const SytrdDesc* descs_dev, const int* ns, int batch,
-                         int k_begin, int k_end, hipStream_t stream) {
+                         int k_begin, int k_end, hipStream_t stream, int waves) {
   int maxn = 0;
   for (int b = 0; b < batch; ++b) maxn = ns[b] > maxn ? ns[b] : maxn;
   if (maxn <= 0) return;
@@ -510,10 +511,10 @@ void sytrd_batched_range(const SytrdDesc* descs_dev, const int* ns, int batch,
       // the previous column's symv had maxn - k rows in the largest member
       hipLaunchKernelGGL(sytrd_col_kernel, dim3((unsigned)ceil_div(rem, SY_T), batch),
                          dim3(SY_T), 0, stream, descs_dev, k, p, 0,
-                         sytrd_symv_blocks(maxn - k, batch));
+                         sytrd_symv_blocks(maxn - k, batch, waves));
       if (k < maxn - 1) {
         hipLaunchKernelGGL(sytrd_symv_kernel,
-                           dim3((unsigned)sytrd_symv_blocks(rem - 1, batch), batch),
+                           dim3((unsigned)sytrd_symv_blocks(rem - 1, batch, waves), batch),
                            dim3(SY_T), 0, stream, descs_dev, k, p);
       }
     }
@@ -521,7 +522,7 @@ void sytrd_batched_range(const SytrdDesc* descs_dev, const int* ns, int batch,
       const int rem = maxn - q;
       hipLaunchKernelGGL(sytrd_col_kernel, dim3((unsigned)ceil_div(rem, SY_T), batch),
                          dim3(SY_T), 0, stream, descs_dev, q, p, 1,
-                         sytrd_symv_blocks(maxn - q, batch));
+                         sytrd_symv_blocks(maxn - q, batch, waves));
       const unsigned tiles = (unsigned)ceil_div(rem, 64);
       hipLaunchKernelGGL(sytrd_syr2k_kernel, dim3(tiles, tiles, batch), dim3(SY_T), 0,
                          stream, descs_dev, q, p);
@@ -535,7 +536,7 @@ void sytrd_batched_range(const SytrdDesc* descs_dev, const int* ns, int batch,
 // caller split the chain into segments and finish small matrices early.
 void sytrd_batched(const SytrdDesc* descs_dev, const int* ns, int batch,
                    hipStream_t stream) {
-  sytrd_batched_range(descs_dev, ns, batch, 0, 1 << 30, stream);
+  sytrd_batched_range(descs_dev, ns, batch, 0, 1 << 30, stream, 0);
 }
 
 }  // namespace kfac

@@ -30,10 +30,6 @@ from distributed_kfac_pytorch_amd.enums import ComputeMethod
 from distributed_kfac_pytorch_amd.enums import DistributedStrategy
 from distributed_kfac_pytorch_amd.preconditioner import KFACPreconditioner
 from distributed_kfac_pytorch_amd.scheduler import LambdaParamScheduler
-from distributed_kfac_pytorch_amd.ops.conv import disable_unsafe_miopen_solvers
-
-# before any MIOpen use: take MIOpen's graph-unsafe solvers out (ops/conv.py)
-disable_unsafe_miopen_solvers()
 
 __version__ = '0.4.1+mi355x.1'
 

@@ -114,14 +114,15 @@ def step_stream(device: torch.device | int | None = None) -> torch.cuda.Stream:
     return s
 
 
-def _graph_safe(model: torch.nn.Module | None, preconditioner: Any) -> int:
+def _graph_safe(model: torch.nn.Module | None, preconditioner: Any,
+                mode: str | None = None) -> int:
     from distributed_kfac_pytorch_amd.ops.conv import StridedConv1x1
     from distributed_kfac_pytorch_amd.ops.conv import make_graph_safe
 
-    n = make_graph_safe(model) if model is not None else 0
+    n = make_graph_safe(model, mode) if model is not None else 0
     for module in list(getattr(preconditioner, '_layers', None) or {}):
         if type(module) in (torch.nn.Conv2d, StridedConv1x1) and module.kernel_size == (1, 1):
-            n += make_graph_safe(module)
+            n += make_graph_safe(module, mode)
     return n
 
 
@@ -139,9 +140,15 @@ class GraphedTrainStep:
             before the graphs are captured.
         enabled: force graphs on / off (default: on when CUDA is available
             and the job has a single rank).
-        model: the trained module; its strided 1x1 convolutions are switched
-            to the graph-safe formulation of ``ops.conv`` (same parameters
-            and values).  Without it only K-FAC's registered layers are.
+        model: the trained module; its 1x1 convolutions are switched to the
+            graph-safe formulation of ``ops.conv`` (same parameters and
+            values).  Without it only K-FAC's registered layers are.
+        conv_mode: ``ops.conv.make_graph_safe`` mode: ``'strided'`` (fp32
+            default: strided 1x1 convolutions only) or ``'gemm'`` (every 1x1
+            convolution as hipBLASLt GEMMs; REQUIRED when the step runs under
+            bf16 autocast, whose tuned MIOpen backward-weights solvers read
+            memory outside the graph: profiles/graph_oop_r4.md).  Default:
+            ``KFAC_GRAPH_SAFE_CONV``, else ``'strided'``.
         stream: the HIP stream every step -- eager or replayed -- and every
             capture runs on (default: a private stream; the caller's stream
             is joined on entry and exit).  One stream for all of them keeps
@@ -165,6 +172,7 @@ class GraphedTrainStep:
         kinds: tuple[str, ...] = ('plain',),
         model: torch.nn.Module | None = None,
         stream: torch.cuda.Stream | None = None,
+        conv_mode: str | None = None,
     ) -> None:
         self.forward_backward = forward_backward
         self.optimizer = optimizer
@@ -184,10 +192,10 @@ class GraphedTrainStep:
         if enabled and self.stream is None:
             self.stream = step_stream()
         if enabled:
-            # strided 1x1 convolutions through the graph-safe formulation
-            # (MIOpen's own backward-data of them reads memory outside the
-            # graph: ops/conv.py); the model's, or at least K-FAC's layers'
-            _graph_safe(model, preconditioner)
+            # 1x1 convolutions through the graph-safe formulations (some
+            # MIOpen solvers read memory outside the graph: ops/conv.py); the
+            # model's, or at least K-FAC's layers'
+            _graph_safe(model, preconditioner, conv_mode)
         # Step kinds replayed from graphs.  Factor-update steps stay eager by
         # default: their SYRKs run on the factor side stream concurrently with
         # backward, and a replayed graph executes its nodes in one queue, so

@@ -32,8 +32,7 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
-__all__ = ['StridedConv1x1', 'GemmConv1x1', 'make_graph_safe', 'is_strided_1x1', 'use_gemm_conv1x1',
-           'disable_unsafe_miopen_solvers']
+__all__ = ['StridedConv1x1', 'GemmConv1x1', 'make_graph_safe', 'is_strided_1x1', 'use_gemm_conv1x1']
 
 
 def is_strided_1x1(m: nn.Module) -> bool:
@@ -77,8 +76,13 @@ def make_graph_safe(model: nn.Module, mode: str | None = None) -> int:
       shapes (``layer2.0.conv1``, ``layer2.2.conv3``: the assembly
       ``ConvAsmImplicitGemmGTCDynamicWrwXdlopsNHWC``, with a workspace) also
       read free global memory from a graph
-      (profiles/graph_oop_r4/bisect_convs_bf16_tuned_db.jsonl);
-      ``disable_unsafe_miopen_solvers()`` takes that solver out.
+      (profiles/graph_oop_r4/bisect_convs_bf16_tuned_db.jsonl).  Turning
+      that solver off (``MIOPEN_DEBUG_CONV_IMPLICIT_GEMM_ASM_WRW_GTC_XDLOPS_NHWC=0``)
+      is no cure: MIOpen then falls back to its naive direct kernels (fp32
+      step 13x slower) and bf16's stem convolution is flagged instead
+      (profiles/graph_oop_r4/bisect_convs_*_gtc_off.jsonl).  This mode is
+      for fp32, whose replays match an eager twin bit for bit
+      (tests/test_graphs_refresh_gpu.py).
     * ``gemm``: every 1x1 convolution becomes ``GemmConv1x1`` (hipBLASLt
       GEMMs, no MIOpen 1x1 solver in the graph at all) -- slower than MIOpen
       at the 56x56 stages (profiles/conv1x1_probe_r4.jsonl).
@@ -96,19 +100,6 @@ def make_graph_safe(model: nn.Module, mode: str | None = None) -> int:
     return n
 
 
-# MIOpen solvers that read memory outside a captured graph (see
-# make_graph_safe); MIOpen reads these switches once, at its first use of
-# the solver, so they are set when the package is imported.
-UNSAFE_MIOPEN_SOLVERS = ('MIOPEN_DEBUG_CONV_IMPLICIT_GEMM_ASM_WRW_GTC_XDLOPS_NHWC',)
-
-
-def disable_unsafe_miopen_solvers() -> None:
-    """Turn the solvers in ``UNSAFE_MIOPEN_SOLVERS`` off unless the user set
-    them (``KFAC_MIOPEN_SAFE=0`` leaves MIOpen untouched)."""
-    if os.environ.get('KFAC_MIOPEN_SAFE', '1') == '0':
-        return
-    for var in UNSAFE_MIOPEN_SOLVERS:
-        os.environ.setdefault(var, '0')
 
 
 class GemmConv1x1(StridedConv1x1):

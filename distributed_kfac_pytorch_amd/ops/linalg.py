@@ -318,6 +318,14 @@ def _chain_groups(keys: list) -> list[list]:
     return [g for g in groups if g]
 
 
+def _chain_waves(group: int) -> int:
+    """Waves each symv launch of chain ``group`` (0 = the largest) is sized
+    to: ``KFAC_SYTRD_WAVES``, comma-separated per group, the last entry
+    repeating; 0 = the whole chip (3 blocks per CU)."""
+    vals = [int(v) for v in os.environ.get('KFAC_SYTRD_WAVES', '0').split(',') if v]
+    return vals[min(group, len(vals) - 1)] if vals else 0
+
+
 _chain_cache: dict[tuple, dict] = {}
 _hi: list[torch.cuda.Stream] = []
 
@@ -345,7 +353,7 @@ def _chain_graphs_enabled(group: int = 0) -> bool:
     return mode == '1' or (mode == 'first' and group == 0)
 
 
-def _chain_entry(sig: tuple, keys: list, stacks: dict) -> dict:
+def _chain_entry(sig: tuple, keys: list, stacks: dict, waves: int = 0) -> dict:
     """Persistent operands + one captured HIP graph per segment for a chain
     signature (the sizes and counts of its buckets), built on first use.
 
@@ -372,7 +380,7 @@ def _chain_entry(sig: tuple, keys: list, stacks: dict) -> dict:
             # no torch.cuda.graph(): its entry synchronises the device and
             # empties the cache while the other lanes are running
             g.capture_begin(capture_error_mode='thread_local')
-            lib.sytrd_advance(state[0], sizes, k0, k1)
+            lib.sytrd_advance(state[0], sizes, k0, k1, waves)
             g.capture_end()
             k0 = k1
         graphs.append(g)
@@ -391,10 +399,11 @@ def _run_chain(stream: torch.cuda.Stream, keys: list, stacks: dict,
     nb = int(lib.sytrd_nb())
     keys = sorted(keys, key=lambda k: k[0])
     out = []
+    waves = _chain_waves(group)
     with torch.cuda.stream(stream):
         if _chain_graphs_enabled(group):
             sig = (str(stream.device), tuple((k[0], stacks[k].shape[0]) for k in keys))
-            ent = _chain_entry(sig, keys, stacks)
+            ent = _chain_entry(sig + (waves,), keys, stacks, waves)
             for buf, k in zip(ent['bufs'], keys):
                 buf.copy_(stacks[k])
             state, reds, graphs = ent['state'], ent['bufs'], ent['graphs']
@@ -412,7 +421,7 @@ def _run_chain(stream: torch.cuda.Stream, keys: list, stacks: dict,
             else:
                 k1 = -(-key[0] // nb) * nb
                 if k1 > k0:
-                    lib.sytrd_advance(descs, sizes, k0, k1)
+                    lib.sytrd_advance(descs, sizes, k0, k1, waves)
                     k0 = k1
             ev = torch.cuda.Event()
             ev.record(stream)

@@ -21,7 +21,9 @@ refresh for a model at any world size without a GPU.
 from __future__ import annotations
 
 import bisect
+import json
 import math
+import os
 from typing import Any
 
 # single-factor refresh on one MI355X, ms (tools/solver_table.py).  Sizes
@@ -49,6 +51,103 @@ def solver_ms(n: int, table: dict[int, float] | None = None) -> float:
     lo, hi = keys[i - 1], keys[i]
     f = (math.log(n) - math.log(lo)) / (math.log(hi) - math.log(lo))
     return math.exp(math.log(t[lo]) + f * (math.log(t[hi]) - math.log(t[lo])))
+
+
+# ---------------------------------------------------------------------------
+# Refresh-time model of a whole factor SET (what one rank decomposes per
+# refresh), mirroring ops.linalg.eigh_many's schedule instead of summing
+# single factors:
+#
+# * n <= 128: one LDS Jacobi launch per size bucket, on a side lane
+#   (overlaps the chains: only its own time when nothing else runs);
+# * two-stage buckets (ops.linalg.twostage_sizes): per bucket
+#   ts_a * count * n^3 / 1e9 + ts_b * n;
+# * the rest: one-stage Householder chains, split at KFAC_SYTRD_SPLIT.  A
+#   chain advances all its members one column per launch pair, so it costs
+#   L per column of its LARGEST member plus the bytes its symv steps stream
+#   (4 * sum over members and columns of the trailing square (n - k - 1)^2)
+#   at bandwidth BW.  Each symv launch is sized to fill the chip, so
+#   concurrent chains time-share it: their column latencies ADD, and all
+#   chains' bytes share one BW;
+# * the tail of the largest bucket (divide and conquer + blocked
+#   back-transform), tail_a * count * n^2 / 1e6 + tail_b * count * n^3 / 1e9,
+#   is exposed after the chains (smaller buckets' tails overlap them).
+#
+# T = sum_chains L * N_c + bytes / BW + tail(largest) (+ two-stage buckets,
+# + Jacobi when it is all there is).  Parameters are fitted to measured
+# refreshes by tools/fit_costmodel.py and stored with the measurements in
+# profiles/solver_table_mi355x.json ("fit"); the defaults below are that fit.
+# ---------------------------------------------------------------------------
+
+REFRESH_PARAMS: dict[str, float] = {
+    'L_us': 13.9, 'bw_tbs': 5.9, 'tail_a': 0.25, 'tail_b': 0.06,
+    'jacobi_ms': 1.3, 'ts_a': 1.0, 'ts_b': 0.02,
+}
+
+_TABLE = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
+                      'profiles', 'solver_table_mi355x.json')
+
+
+def load_params(path: str | None = None) -> dict[str, float]:
+    """The fitted refresh-model parameters (``fit`` of the measured table),
+    or ``REFRESH_PARAMS`` when the table is absent."""
+    try:
+        with open(path or _TABLE) as f:
+            fit = json.load(f).get('fit')
+        if fit:
+            return {**REFRESH_PARAMS, **{k: float(v) for k, v in fit.items() if k in REFRESH_PARAMS}}
+    except (OSError, ValueError):
+        pass
+    return dict(REFRESH_PARAMS)
+
+
+def _split_cuts() -> list[int]:
+    return sorted((int(c) for c in os.environ.get('KFAC_SYTRD_SPLIT', '4000,1000').split(',')
+                   if c), reverse=True)
+
+
+def refresh_terms(sizes: list[int], params: dict[str, float] | None = None) -> dict[str, float]:
+    """Per-term predicted milliseconds of one eigen refresh of ``sizes``
+    (see the model above)."""
+    from distributed_kfac_pytorch_amd.ops.linalg import JACOBI_MAX_N
+    from distributed_kfac_pytorch_amd.ops.linalg import twostage_sizes
+
+    p = params or load_params()
+    counts: dict[int, int] = {}
+    for n in sizes:
+        counts[int(n)] = counts.get(int(n), 0) + 1
+    ts = twostage_sizes({n: c for n, c in counts.items() if n > JACOBI_MAX_N})
+    jac = [n for n in counts if n <= JACOBI_MAX_N]
+    chain_sizes = {n: c for n, c in counts.items() if n > JACOBI_MAX_N and n not in ts}
+    groups: list[dict[int, int]] = []
+    left = dict(chain_sizes)
+    for cut in _split_cuts():
+        groups.append({n: c for n, c in left.items() if n >= cut})
+        left = {n: c for n, c in left.items() if n < cut}
+    groups.append(left)
+    groups = [g for g in groups if g]
+    lat = sum(p['L_us'] * 1e-3 * (max(g) - 1) for g in groups)
+    byts = 0.0
+    for n, c in chain_sizes.items():
+        m = n - 1  # trailing squares (n-1)^2 ... 1^2
+        byts += 4.0 * c * m * (m + 1) * (2 * m + 1) / 6.0
+    bw = byts / (p['bw_tbs'] * 1e12) * 1e3
+    tail = 0.0
+    if chain_sizes:
+        n = max(chain_sizes)
+        c = chain_sizes[n]
+        tail = p['tail_a'] * c * n * n / 1e6 + p['tail_b'] * c * n ** 3 / 1e9
+    two = sum(p['ts_a'] * counts[n] * n ** 3 / 1e9 + p['ts_b'] * n for n in ts)
+    jacobi = p['jacobi_ms'] * len(jac)
+    return {'latency': lat, 'bandwidth': bw, 'tail': tail, 'twostage': two, 'jacobi': jacobi}
+
+
+def refresh_ms(sizes: list[int], params: dict[str, float] | None = None) -> float:
+    """Predicted milliseconds of one eigen refresh of the factor set
+    ``sizes`` on one MI355X (ops.linalg.eigh_many)."""
+    t = refresh_terms(sizes, params)
+    main = t['latency'] + t['bandwidth'] + t['tail'] + t['twostage']
+    return max(main, t['jacobi']) if main > 0 else t['jacobi']
 
 
 def flops_cost(n: int) -> float:
@@ -106,6 +205,8 @@ def plan(sizes: list[tuple[str, int, int]], world: int, grad_worker_fraction: fl
     for name in asg.get_layers():
         for f in asg.get_factors(name):
             per[asg.inv_worker(name, f)].append(dims[name][f])
-    pred = [sum(solver_ms(n) for n in ns) for ns in per]
+    # each rank's refresh is one eigh_many over its set: the set model, not
+    # a sum of single factors
+    pred = [refresh_ms(ns) if ns else 0.0 for ns in per]
     return {'world': world, 'cost': cost, 'factors_per_rank': per,
             'predicted_ms': pred, 'max_ms': max(pred) if pred else 0.0}

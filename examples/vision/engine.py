@@ -69,7 +69,10 @@ class _GraphedSteps:
             loss.backward()
             return loss
 
-        self.runner = GraphedTrainStep(fb, optimizer, preconditioner, model=model)
+        # under bf16 autocast every 1x1 conv runs as GEMMs in the graphs
+        # (MIOpen's tuned bf16 backward-weights solvers read outside them)
+        self.runner = GraphedTrainStep(fb, optimizer, preconditioner, model=model,
+                                       conv_mode='gemm' if amp is not None else None)
 
     def fits(self, data: torch.Tensor, target: torch.Tensor) -> bool:
         return data.shape == self.x.shape and data.stride() == self.x.stride() and \

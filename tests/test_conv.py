@@ -59,15 +59,6 @@ def test_resnet50_projections_are_graph_safe() -> None:
         make_graph_safe(plain, 'nope')
 
 
-def test_unsafe_miopen_solvers_disabled_on_import() -> None:
-    import os
-
-    import distributed_kfac_pytorch_amd  # noqa: F401
-    from distributed_kfac_pytorch_amd.ops.conv import UNSAFE_MIOPEN_SOLVERS
-    for var in UNSAFE_MIOPEN_SOLVERS:
-        assert os.environ.get(var) is not None
-
-
 def test_use_gemm_conv1x1_switches_every_1x1() -> None:
     m = resnet50()
     n1 = sum(1 for mm in m.modules() if isinstance(mm, nn.Conv2d) and mm.kernel_size == (1, 1))

@@ -30,13 +30,16 @@ import distributed_kfac_pytorch_amd as kfac
 from distributed_kfac_pytorch_amd.graphs import GraphedTrainStep
 from distributed_kfac_pytorch_amd.models.resnet import resnet50
 from distributed_kfac_pytorch_amd.ops.cast import enable_fused_weight_cast
+from distributed_kfac_pytorch_amd.ops.conv import use_gemm_conv1x1
 
 pytestmark = pytest.mark.gpu
 
 
 def _build(base: torch.nn.Module, cuda: torch.device, graphs: bool, amp: bool,
-           use_kfac: bool, kinds=('plain',)):
+           use_kfac: bool, kinds=('plain',), conv_mode=None):
     model = copy.deepcopy(base).to(cuda).to(memory_format=torch.channels_last)
+    if conv_mode == 'gemm':  # the eager twin computes its 1x1 convs the same way
+        use_gemm_conv1x1(model)
     if amp:
         enable_fused_weight_cast(model)
     opt = torch.optim.SGD(model.parameters(), lr=0.0125, momentum=0.9, weight_decay=5e-5,
@@ -57,7 +60,8 @@ def _build(base: torch.nn.Module, cuda: torch.device, graphs: bool, amp: bool,
         return loss
 
     if graphs:
-        runner = GraphedTrainStep(fb, opt, pre, warmup=1, enabled=True, kinds=kinds, model=model)
+        runner = GraphedTrainStep(fb, opt, pre, warmup=1, enabled=True, kinds=kinds, model=model,
+                                  conv_mode=conv_mode)
     else:
         def runner() -> torch.Tensor:
             opt.zero_grad(set_to_none=False)
@@ -69,12 +73,13 @@ def _build(base: torch.nn.Module, cuda: torch.device, graphs: bool, amp: bool,
     return model, pre, x, y, runner
 
 
-@pytest.mark.parametrize('amp,use_kfac,kinds', [
-    (True, True, ('plain',)),
-    (False, True, ('plain', 'factor')),
-    (False, False, ('plain',)),
+@pytest.mark.parametrize('amp,use_kfac,kinds,conv_mode', [
+    (True, True, ('plain',), None),
+    (True, True, ('plain',), 'gemm'),  # the bench's bf16 mode
+    (False, True, ('plain', 'factor'), None),
+    (False, False, ('plain',), None),
 ])
-def test_graph_replay_interleaved_with_eager_twin(cuda, amp, use_kfac, kinds) -> None:
+def test_graph_replay_interleaved_with_eager_twin(cuda, amp, use_kfac, kinds, conv_mode) -> None:
     det = torch.backends.cudnn.deterministic
     torch.backends.cudnn.deterministic = True
     try:
@@ -84,8 +89,8 @@ def test_graph_replay_interleaved_with_eager_twin(cuda, amp, use_kfac, kinds) ->
         pool = [(torch.randn(32, 3, 224, 224, generator=gen),
                  torch.randint(0, 1000, (32,), generator=gen)) for _ in range(4)]
         steps = 18  # K-FAC refreshes at steps 0, 8, 16
-        A = _build(base, cuda, True, amp, use_kfac, kinds)
-        B = _build(base, cuda, False, amp, use_kfac)
+        A = _build(base, cuda, True, amp, use_kfac, kinds, conv_mode)
+        B = _build(base, cuda, False, amp, use_kfac, conv_mode=conv_mode)
         for i in range(steps):
             x, y = pool[i % len(pool)]
             for m in (A, B):

@@ -7,7 +7,7 @@ set -o pipefail
 R="$GRAFT_REPO_ROOT"
 cd /tmp && export TMPDIR=/tmp
 O=/tmp/pmc4; mkdir -p $O
-S=$R/gpurun_out/r4pmc; mkdir -p $S
+S=$R/gpurun_out/r4o/pmc; mkdir -p $S
 export KFAC_EIGH_THREADS=0
 pass() {
   local name=$1; shift
