@@ -481,13 +481,15 @@ __global__ void __launch_bounds__(SY_T) sytrd_syr2k_kernel(
 }  // namespace
 
 // symv blocks per member for `rows` rows of the largest member: the whole
-// launch (blocks x batch) is sized to `waves` waves (default ~3 resident
-// 256-thread blocks on each of the 256 CUs), with every wave streaming the
-// same number of rows.  Chains that run concurrently on other lanes get a
-// smaller budget (ops/linalg.py, KFAC_SYTRD_WAVES).
+// launch (blocks x batch) is sized to `waves` waves, with every wave
+// streaming the same number of rows.  Default 6144 = twice the chip's
+// resident waves (3 blocks of 4 waves per CU): on the ResNet-50 mix, whose
+// three chains run concurrently, 215 ms vs 238 ms with one chip's worth and
+// 383-474 ms with smaller budgets for the smaller chains
+// (profiles/r4_eigh/mix_w*.jsonl).  KFAC_SYTRD_WAVES overrides per chain.
 int sytrd_symv_blocks(int rows, int batch, int waves) {
   if (rows <= 0) return 1;
-  if (waves <= 0) waves = 3 * 256 * 4;
+  if (waves <= 0) waves = 6 * 256 * 4;
   const int per = (int)ceil_div((int64_t)rows * batch, (int64_t)waves);  // rows per wave
   int g = (int)ceil_div((int64_t)rows, (int64_t)4 * per);
   if (g > SY_MAXROWBLK) g = SY_MAXROWBLK;

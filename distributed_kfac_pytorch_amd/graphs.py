@@ -40,12 +40,16 @@ signature; when it changes the affected graphs are dropped and re-captured.
 Correctness: a captured graph may only read memory that its private pool
 or a live tensor owns.  MIOpen's backward-data of strided 1x1 convolutions
 did not (it read free global-pool blocks, so replays broke as soon as other
-eager work -- an eval pass, a second model, the refresh -- reused them:
-profiles/graph_oop_r4.md); the runner therefore switches those convolutions
-to the graph-safe ``ops.conv.StridedConv1x1`` (``model=``), and
-``tools/graph_oop_audit.py`` checks any new model the same way (poisons the
-free global pool between replays).  Every step -- eager or replayed -- runs
-on one persistent stream (``step_stream()``).
+eager work -- an eval pass, a second model, the refresh -- reused them), nor
+do the tuned database's bf16 backward-weights solvers of some stride-1 1x1
+shapes (profiles/graph_oop_r4.md).  The runner therefore switches the
+model's strided 1x1 convolutions to the graph-safe
+``ops.conv.StridedConv1x1`` (``conv_mode='strided'``, fp32) or every 1x1
+convolution to hipBLASLt GEMMs (``conv_mode='gemm'``, required under bf16
+autocast), and ``tools/graph_oop_audit.py`` / ``graph_oop_bisect.py`` check
+any new model the same way (they poison the free global pool between
+replays).  Every step -- eager or replayed -- runs on one persistent stream
+(``step_stream()``).
 
 Multi-rank jobs run every step eagerly by default (the K-FAC precondition
 phase is still replayed from ``StepGraphs``).  The K-FAC collectives
@@ -54,11 +58,14 @@ themselves no longer block capture (``AsyncTensor`` has no host callbacks:
 gradient all-reduce does: DDP's C++ reducer launches its bucket all-reduces
 from autograd hooks, rebuilds its buckets during the first iterations, and
 ProcessGroupNCCL's watchdog polls each collective's HIP event from its own
-thread.  Capturing that needs DDP built under a side stream, the bucket
-rebuild finished before capture, and asynchronous error handling off --
-none of which can be validated here (no multi-GPU RCCL box is available to
-this build).  ``KFAC_STEP_GRAPHS_MULTI=1`` opts a multi-rank job in; a
-capture that raises falls back to eager steps.
+thread.  Capturing that needs DDP built under the step stream (``step_stream()``),
+the bucket rebuild and DDP's runtime-statistics iterations finished before
+capture (``warmup`` >= 11 for a DDP model) and asynchronous error handling
+off (``TORCH_NCCL_ASYNC_ERROR_HANDLING=0``).  That path is exercised at
+world size 1 over RCCL (``bench.py --ddp 1`` under torchrun:
+profiles/bench_r4_ddp_world1_graphs.json, 107 replays, finite); multi-GPU
+capture has not been run.  ``KFAC_STEP_GRAPHS_MULTI=1`` opts a multi-rank
+job in; a capture that raises falls back to eager steps on a fresh stream.
 """
 from __future__ import annotations
 

@@ -9,49 +9,24 @@ pays a per-column chain of dependent launches (about n kernel pairs), so a
 owns one large factor still waits for its whole chain.  ``n^3`` mis-balances
 exactly the N = 8 case the refresh is amortised over.
 
-``solver_ms(n)`` interpolates a MEASURED single-factor refresh time table
-(log-log between measured sizes; ``tools/solver_table.py`` regenerates it and
-``profiles/solver_table_mi355x.json`` holds the run the defaults come from).
-``KFACPreconditioner(assignment_strategy='compute')`` uses it as the factor
-cost on CUDA models with the eigen method (``cost_model='auto'``), so the
-LPT placement (``parallel/assignment.py``, unchanged) balances predicted
-milliseconds instead of flops.  ``plan()`` prints the predicted per-rank
-refresh for a model at any world size without a GPU.
+``refresh_ms(sizes)`` predicts the refresh of a whole factor SET -- one
+rank's ``ops.linalg.eigh_many`` call -- from a model of that schedule (below)
+whose parameters are fitted to measured refreshes (``tools/solver_table.py``
+measures, ``tools/fit_costmodel.py`` fits; ``profiles/solver_table_mi355x.json``
+holds both).  ``solver_ms(n)`` is its single-factor value, the factor cost
+of ``KFACPreconditioner(assignment_strategy='compute', cost_model='measured')``
+(opt-in; ``'auto'`` keeps the reference's ``n^3``), so the LPT placement
+(``parallel/assignment.py``, unchanged) balances predicted milliseconds.
+``plan()`` prints each rank's predicted refresh at any world size without a
+GPU.
 """
 from __future__ import annotations
 
-import bisect
 import json
-import math
 import os
 from typing import Any
 
-# single-factor refresh on one MI355X, ms (tools/solver_table.py).  Sizes
-# <= 128 run in the one-workgroup LDS Jacobi tier (all together in one
-# launch); above that the native chain.
-SOLVER_MS: dict[int, float] = {
-    64: 0.3, 128: 0.5,
-    129: 4.0, 256: 7.0, 512: 13.0, 768: 19.0, 1024: 25.0, 1536: 37.0,
-    2048: 50.0, 2304: 56.0, 3072: 80.0, 4096: 110.0, 4608: 125.0,
-}
-
-
-def solver_ms(n: int, table: dict[int, float] | None = None) -> float:
-    """Predicted refresh milliseconds of one ``n x n`` factor."""
-    t = table or SOLVER_MS
-    keys = sorted(t)
-    if n <= keys[0]:
-        return t[keys[0]] * max(n, 1) / keys[0]
-    if n >= keys[-1]:
-        # beyond the table the bandwidth term dominates: n^3 growth
-        return t[keys[-1]] * (n / keys[-1]) ** 3
-    i = bisect.bisect_left(keys, n)
-    if keys[i] == n:
-        return t[n]
-    lo, hi = keys[i - 1], keys[i]
-    f = (math.log(n) - math.log(lo)) / (math.log(hi) - math.log(lo))
-    return math.exp(math.log(t[lo]) + f * (math.log(t[hi]) - math.log(t[lo])))
-
+import numpy as np
 
 # ---------------------------------------------------------------------------
 # Refresh-time model of a whole factor SET (what one rank decomposes per
@@ -63,25 +38,29 @@ def solver_ms(n: int, table: dict[int, float] | None = None) -> float:
 # * two-stage buckets (ops.linalg.twostage_sizes): per bucket
 #   ts_a * count * n^3 / 1e9 + ts_b * n;
 # * the rest: one-stage Householder chains, split at KFAC_SYTRD_SPLIT.  A
-#   chain advances all its members one column per launch pair, so it costs
-#   L per column of its LARGEST member plus the bytes its symv steps stream
-#   (4 * sum over members and columns of the trailing square (n - k - 1)^2)
-#   at bandwidth BW.  Each symv launch is sized to fill the chip, so
-#   concurrent chains time-share it: their column latencies ADD, and all
-#   chains' bytes share one BW;
-# * the tail of the largest bucket (divide and conquer + blocked
-#   back-transform), tail_a * count * n^2 / 1e6 + tail_b * count * n^3 / 1e9,
-#   is exposed after the chains (smaller buckets' tails overlap them).
+#   chain advances all its members one column per launch pair: column k
+#   costs L0 (the col step and the launch gaps) plus the symv step, which
+#   streams the members' trailing squares, b_k = 4 * sum (n - k - 1)^2
+#   bytes, and takes max(L1 + L2 * (n_max - k) / 1000, b_k / BW): a latency
+#   floor that grows with the launch's grid, or bandwidth, BW = bw_mall
+#   while b_k fits the 256 MB Infinity Cache and bw_hbm above;
+# * chains run concurrently on their own lanes: the slowest sets the pace,
+#   and every other chain adds its bytes (shared bandwidth) and a fraction
+#   nu of its column latency (its kernels take CU slots between the
+#   critical chain's);
+# * a fixed base per call plus bucket_ms per size bucket (its tail's
+#   launches and joins), and the largest bucket's tail (divide and
+#   conquer + back-transform, tail_b * count * n^3 / 1e9) after the chains.
 #
-# T = sum_chains L * N_c + bytes / BW + tail(largest) (+ two-stage buckets,
-# + Jacobi when it is all there is).  Parameters are fitted to measured
-# refreshes by tools/fit_costmodel.py and stored with the measurements in
-# profiles/solver_table_mi355x.json ("fit"); the defaults below are that fit.
+# Parameters are fitted to measured refreshes by tools/fit_costmodel.py and
+# stored with the measurements in profiles/solver_table_mi355x.json
+# ("fit"); REFRESH_PARAMS are the fallback when that file is absent.
 # ---------------------------------------------------------------------------
 
 REFRESH_PARAMS: dict[str, float] = {
-    'L_us': 13.9, 'bw_tbs': 5.9, 'tail_a': 0.25, 'tail_b': 0.06,
-    'jacobi_ms': 1.3, 'ts_a': 1.0, 'ts_b': 0.02,
+    'L0_us': 8.0, 'L1_us': 8.0, 'L2_us': 1.0, 'nu': 0.2, 'bw_mall_tbs': 6.0, 'bw_hbm_tbs': 3.0,
+    'base_ms': 1.5, 'bucket_ms': 0.5,
+    'tail_b': 0.05, 'jacobi_ms': 1.3, 'ts_a': 0.5, 'ts_b': 0.01,
 }
 
 _TABLE = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
@@ -101,6 +80,16 @@ def load_params(path: str | None = None) -> dict[str, float]:
     return dict(REFRESH_PARAMS)
 
 
+_PARAMS: dict[str, float] | None = None
+
+
+def _params() -> dict[str, float]:
+    global _PARAMS
+    if _PARAMS is None:
+        _PARAMS = load_params()
+    return _PARAMS
+
+
 def _split_cuts() -> list[int]:
     return sorted((int(c) for c in os.environ.get('KFAC_SYTRD_SPLIT', '4000,1000').split(',')
                    if c), reverse=True)
@@ -112,7 +101,7 @@ def refresh_terms(sizes: list[int], params: dict[str, float] | None = None) -> d
     from distributed_kfac_pytorch_amd.ops.linalg import JACOBI_MAX_N
     from distributed_kfac_pytorch_amd.ops.linalg import twostage_sizes
 
-    p = params or load_params()
+    p = params or _params()
     counts: dict[int, int] = {}
     for n in sizes:
         counts[int(n)] = counts.get(int(n), 0) + 1
@@ -126,28 +115,48 @@ def refresh_terms(sizes: list[int], params: dict[str, float] | None = None) -> d
         left = {n: c for n, c in left.items() if n < cut}
     groups.append(left)
     groups = [g for g in groups if g]
-    lat = sum(p['L_us'] * 1e-3 * (max(g) - 1) for g in groups)
-    byts = 0.0
-    for n, c in chain_sizes.items():
-        m = n - 1  # trailing squares (n-1)^2 ... 1^2
-        byts += 4.0 * c * m * (m + 1) * (2 * m + 1) / 6.0
-    bw = byts / (p['bw_tbs'] * 1e12) * 1e3
+    chains = []
+    mall = 256.0 * 2 ** 20
+    for g in groups:
+        top = max(g)
+        k = np.arange(top - 1, dtype=np.float64)
+        b = np.zeros_like(k)
+        for n, c in g.items():
+            r = np.clip(n - k - 1, 0, None)
+            b += 4.0 * c * r * r
+        bw = np.where(b <= mall, p['bw_mall_tbs'], p['bw_hbm_tbs']) * 1e12
+        floor = (p['L1_us'] + p['L2_us'] * (top - k) / 1000.0) * 1e-6
+        symv = np.maximum(floor, b / bw)
+        lat = p['L0_us'] * 1e-3 * (top - 1)
+        chains.append((lat, float(symv.sum()) * 1e3))
+    crit = max(range(len(chains)), key=lambda i: sum(chains[i])) if chains else -1
+    lat = chains[crit][0] if chains else 0.0
+    bwt = chains[crit][1] if chains else 0.0
+    share = sum(p['nu'] * (l + b) for i, (l, b) in enumerate(chains) if i != crit)
     tail = 0.0
     if chain_sizes:
         n = max(chain_sizes)
-        c = chain_sizes[n]
-        tail = p['tail_a'] * c * n * n / 1e6 + p['tail_b'] * c * n ** 3 / 1e9
+        tail = p['tail_b'] * chain_sizes[n] * n ** 3 / 1e9
     two = sum(p['ts_a'] * counts[n] * n ** 3 / 1e9 + p['ts_b'] * n for n in ts)
     jacobi = p['jacobi_ms'] * len(jac)
-    return {'latency': lat, 'bandwidth': bw, 'tail': tail, 'twostage': two, 'jacobi': jacobi}
+    base = (p['base_ms'] + p['bucket_ms'] * len(chain_sizes)) if (chains or ts) else 0.0
+    return {'latency': lat, 'bandwidth': bwt, 'other_chains': share, 'tail': tail,
+            'twostage': two, 'jacobi': jacobi, 'base': base}
 
 
 def refresh_ms(sizes: list[int], params: dict[str, float] | None = None) -> float:
     """Predicted milliseconds of one eigen refresh of the factor set
     ``sizes`` on one MI355X (ops.linalg.eigh_many)."""
     t = refresh_terms(sizes, params)
-    main = t['latency'] + t['bandwidth'] + t['tail'] + t['twostage']
-    return max(main, t['jacobi']) if main > 0 else t['jacobi']
+    main = (t['latency'] + t['bandwidth'] + t['other_chains'] + t['tail'] + t['twostage']
+            + t['base'])
+    return max(main, t['jacobi'])
+
+
+def solver_ms(n: int, params: dict[str, float] | None = None) -> float:
+    """Predicted refresh milliseconds of one ``n x n`` factor alone (the KAISA
+    COMPUTE cost of ``cost_model='measured'``)."""
+    return refresh_ms([int(n)], params)
 
 
 def flops_cost(n: int) -> float:

@@ -61,7 +61,8 @@ def main() -> None:
                 del mats
                 torch.cuda.empty_cache()
             out['rank_ms'][f'{model}/N{world}'] = {
-                'measured_ms': per, 'predicted_ms': [round(v, 1) for v in plan['predicted_ms']]}
+                'measured_ms': per, 'predicted_ms': [round(v, 1) for v in plan['predicted_ms']],
+                'sizes': plan['factors_per_rank']}
             print(json.dumps({model: world, 'measured': per,
                               'predicted': plan['predicted_ms']}), file=sys.stderr, flush=True)
     print(json.dumps(out))

@@ -38,7 +38,7 @@ def main(path: str, marker: str = 'max_pool_forward') -> None:
 
     def kind(ks):
         names = ' '.join(n for _, _, n in ks)
-        if 'rocsolver' in names:
+        if 'rocsolver' in names or 'sytrd' in names or 'jacobi_kernel' in names:
             return 'inverse'
         if 'syrk_kernel' in names:
             return 'factor'
@@ -62,6 +62,12 @@ def main(path: str, marker: str = 'max_pool_forward') -> None:
                 d[n[:90]] += (e - s) / 1e3 / len(v)
         return d
 
+    if 'factor' in by and 'plain' in by:
+        f, p = agg(by['factor']), agg(by['plain'])
+        diff = sorted(((f.get(n, 0) - p.get(n, 0), n) for n in set(f) | set(p)), reverse=True)
+        print('\nper-step kernel time, factor-update minus plain K-FAC step (us):')
+        for dt, n in diff[:20]:
+            print(f'{dt:9.1f}  factor {f.get(n, 0):8.1f}  plain {p.get(n, 0):8.1f}  {n}')
     if 'plain' in by and 'sgd' in by:
         p, s = agg(by['plain']), agg(by['sgd'])
         diff = sorted(((p.get(n, 0) - s.get(n, 0), n) for n in set(p) | set(s)), reverse=True)
