@@ -31,6 +31,8 @@
 #include "common.h"
 #include "descs.h"
 
+#include <cstdlib>
+
 namespace kfac {
 
 constexpr int SY_NB = 32;                 // panel width
@@ -38,7 +40,8 @@ constexpr int SY_T = 256;                 // threads per block
 constexpr int SY_P1 = 2 * SY_NB + 4;      // partial stride: xn2, dW[NB], dV[NB]
 constexpr int SY_ROWS = 16;               // symv rows per workgroup
 constexpr int SY_RPW = SY_ROWS / (SY_T / 64);  // symv rows per wave (4)
-constexpr int SY_SU = 4;                  // symv column blocks in flight per row
+// symv column blocks (float4 per lane) in flight per row: a template
+// parameter of the symv kernel, chosen by KFAC_SYTRD_SU (4 or 8)
 constexpr int SY_MAXN = 8192;             // v staged in LDS (32 KiB)
 constexpr int SY_MAXCH = SY_MAXN / SY_T;  // col-step chunks
 constexpr int SY_MAXROWBLK = SY_MAXN / SY_ROWS;
@@ -245,6 +248,7 @@ __global__ void __launch_bounds__(SY_T) sytrd_col_kernel(
 // the scalars and its panel correction terms on its own.  Every block
 // writes its partial w.v (0 without rows) to part2[b]; the next col step
 // gets G as an argument.
+template <int SY_SU>
 __global__ void __launch_bounds__(SY_T) sytrd_symv_kernel(
     const SytrdDesc* __restrict__ descs, int k, int p) {
   const GView D = gview(descs[blockIdx.y]);
@@ -505,6 +509,10 @@ void sytrd_batched_range(const SytrdDesc* descs_dev, const int* ns, int batch,
   for (int b = 0; b < batch; ++b) maxn = ns[b] > maxn ? ns[b] : maxn;
   if (maxn <= 0) return;
   if (k_end > maxn) k_end = maxn;
+  static const int su = [] {
+    const char* e = getenv("KFAC_SYTRD_SU");
+    return e && atoi(e) == 8 ? 8 : 4;
+  }();
   // segments start on panel boundaries: panel [p, p+NB) is issued whole
   for (int p = k_begin; p < k_end; p += SY_NB) {
     const int q = (p + SY_NB < maxn) ? p + SY_NB : maxn;
@@ -515,9 +523,11 @@ void sytrd_batched_range(const SytrdDesc* descs_dev, const int* ns, int batch,
                          dim3(SY_T), 0, stream, descs_dev, k, p, 0,
                          sytrd_symv_blocks(maxn - k, batch, waves));
       if (k < maxn - 1) {
-        hipLaunchKernelGGL(sytrd_symv_kernel,
-                           dim3((unsigned)sytrd_symv_blocks(rem - 1, batch, waves), batch),
-                           dim3(SY_T), 0, stream, descs_dev, k, p);
+        const dim3 grid((unsigned)sytrd_symv_blocks(rem - 1, batch, waves), batch);
+        if (su == 8)
+          hipLaunchKernelGGL(sytrd_symv_kernel<8>, grid, dim3(SY_T), 0, stream, descs_dev, k, p);
+        else
+          hipLaunchKernelGGL(sytrd_symv_kernel<4>, grid, dim3(SY_T), 0, stream, descs_dev, k, p);
       }
     }
     if (q < maxn) {

@@ -14,11 +14,14 @@ gpu_r2_pmc.sh) and writes a CSV plus a markdown table:
   streaming reads by 2x on gfx950: MI355X_MICROARCH.md), L2 hit rate;
 * LDS bank-conflict cycles / LDS active cycles.
 
-    python tools/pmc_summary.py gpurun_out/pmc step out_prefix
+    python tools/pmc_summary.py gpurun_out/pmc step out_prefix [pass1,pass2,...]
+
+(the first pass's dispatch timestamps give the kernel times)
 """
 from __future__ import annotations
 
 import csv
+import glob
 import json
 import os
 import sys
@@ -49,21 +52,28 @@ def short(name: str) -> str:
     return name[:90]
 
 
-def load(base: str, prefix: str) -> dict:
+def _find(d: str, suffix: str) -> str:
+    """The rocprofv3 CSV ending in ``suffix`` under pass directory ``d``
+    (directly, or in rocprofv3's host / pid subdirectories)."""
+    hits = sorted(glob.glob(os.path.join(d, '**', '*' + suffix), recursive=True))
+    return hits[0] if hits else os.path.join(d, suffix)
+
+
+def load(base: str, prefix: str, passes: tuple[str, ...] = ('sq', 'fetch', 'write')) -> dict:
     counters: dict = defaultdict(lambda: defaultdict(float))
     times: dict = defaultdict(float)
     counts: dict = defaultdict(int)
-    for p in ('sq', 'fetch', 'write'):
+    for p in passes:
         d = os.path.join(base, f'{prefix}_{p}')
-        rows = _read(os.path.join(d, f'{prefix}_{p}_counter_collection.csv'))
+        rows = _read(_find(d, 'counter_collection.csv'))
         for r in rows:
             k = _col(r, 'Kernel_Name', 'Kernel-Name', 'KernelName')
             c = _col(r, 'Counter_Name', 'Counter-Name')
             v = _col(r, 'Counter_Value', 'Counter-Value')
             if k and c and v:
                 counters[short(r[k])][r[c]] += float(r[v] or 0)
-        if p == 'sq':
-            trace = _read(os.path.join(d, f'{prefix}_{p}_kernel_trace.csv'))
+        if p == passes[0]:
+            trace = _read(_find(d, 'kernel_trace.csv'))
             if not trace:
                 # counter-only pass (no --kernel-trace): one row per
                 # (dispatch, counter) carries the dispatch's timestamps
@@ -106,16 +116,23 @@ def load(base: str, prefix: str) -> dict:
         if lds:
             row['lds_conflict'] = round(c.get('SQ_LDS_BANK_CONFLICT', 0.0) / lds, 4)
         row['waves'] = c.get('SQ_WAVES', 0.0)
+        for name, key in (('valu_insts', 'SQ_INSTS_VALU'), ('lds_insts', 'SQ_INSTS_LDS'),
+                          ('wait_inst_any', 'SQ_WAIT_INST_ANY'), ('wave_cycles', 'SQ_WAVE_CYCLES'),
+                          ('busy_cycles', 'SQ_BUSY_CYCLES')):
+            if key in c:
+                row[name] = c[key]
         out[k] = row
     return out
 
 
 def main() -> None:
     base, prefix, dest = sys.argv[1], sys.argv[2], sys.argv[3]
-    rows = sorted(load(base, prefix).values(), key=lambda r: -r['time_ms'])
+    passes = tuple(sys.argv[4].split(',')) if len(sys.argv) > 4 else ('sq', 'fetch', 'write')
+    rows = sorted(load(base, prefix, passes).values(), key=lambda r: -r['time_ms'])
     keys = ['kernel', 'dispatches', 'time_ms', 'mfma_util', 'mfma_tflops',
             'fetch_gbs', 'write_gbs', 'l2_hit', 'lds_conflict', 'fetch_kb', 'write_kb',
-            'mfma_mops_bf16', 'mfma_mops_f32', 'waves']
+            'mfma_mops_bf16', 'mfma_mops_f32', 'waves', 'valu_insts', 'lds_insts',
+            'wait_inst_any', 'wave_cycles', 'busy_cycles']
     with open(dest + '.csv', 'w', newline='') as f:
         w = csv.DictWriter(f, fieldnames=keys, extrasaction='ignore')
         w.writeheader()
