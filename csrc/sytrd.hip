@@ -24,10 +24,11 @@
 // Storage is row-major and the math is LAPACK's slatrd / ssytrd with
 // uplo = 'L' on the transpose: reflector k (v[k+1] = 1 implicit,
 // v[k+2:n] stored) lives in ROW k, which is exactly LAPACK's column-major
-// lower layout, so rocSOLVER's stedc + ormtr finish the eigensolve
-// (csrc/solver.cpp).  The algorithm is checked step for step on the CPU by
+// lower layout; the native divide and conquer (csrc/tridiag.hip) and the
+// blocked back-transform (ops/linalg.py apply_q_blocked) finish the
+// eigensolve (csrc/solver.cpp).  The algorithm is checked step for step on the CPU by
 // tools/sytrd_proto.py.  Replaces the reference's torch.linalg.eigh
-// (kfac/layers/eigen.py:294-347) for n >= KFAC_SYTRD_MIN_N.
+// (kfac/layers/eigen.py:294-347) for 128 < n <= 8192 (ops/linalg.py).
 #include "common.h"
 #include "descs.h"
 
