@@ -149,6 +149,7 @@ def _bucket_cost(n: int, count: int) -> float:
 
 def eigh_many(mats: list[torch.Tensor]) -> list[tuple[torch.Tensor, torch.Tensor]]:
     """Eigendecompose each symmetric matrix; returns ``[(evals, evecs)]``."""
+    last_stats['tiers'] = []  # this call's buckets only
     out: list[tuple[torch.Tensor, torch.Tensor] | None] = [None] * len(mats)
     buckets: dict[tuple, list[int]] = defaultdict(list)
     for i, m in enumerate(mats):
