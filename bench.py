@@ -510,7 +510,9 @@ def main() -> None:
             'kind_ms': sec['kind_ms'], 'params_finite': sec['params_finite'],
             'eigen_refresh_ms': round(sec.get('refresh_ms', 0.0), 3),
             'host_issue_ms': sec['host_issue_ms'],
-            'graphs': 'step_graphs' in sec,
+            # replayed from graphs (not just requested)
+            'graphs': bool((sec.get('step_graphs') or {}).get('replays')),
+            'step_graphs': sec.get('step_graphs'),
         }
     line['host_issue_ms'] = res['host_issue_ms']
     if base is not None:
