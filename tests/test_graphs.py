@@ -161,3 +161,29 @@ def test_table_rekey_every_step_matches(cuda, deterministic) -> None:
         run_b()
     torch.cuda.synchronize()
     assert _state_diff(ma, oa, pa, mb, ob, pb) <= 1e-6
+
+
+def test_graph_safe_conv_modes_cpu() -> None:
+    """``GraphedTrainStep``'s conv conversion (``conv_mode``) on CPU: the
+    model's and K-FAC's registered 1x1 convolutions, same parameters."""
+    from distributed_kfac_pytorch_amd.graphs import _graph_safe
+    from distributed_kfac_pytorch_amd.ops.conv import GemmConv1x1
+    from distributed_kfac_pytorch_amd.ops.conv import StridedConv1x1
+
+    def net() -> torch.nn.Module:
+        torch.manual_seed(0)
+        return torch.nn.Sequential(torch.nn.Conv2d(3, 8, 1, stride=2), torch.nn.ReLU(),
+                                   torch.nn.Conv2d(8, 8, 1), torch.nn.Conv2d(8, 4, 3))
+
+    m = net()
+    x = torch.randn(2, 3, 8, 8).contiguous(memory_format=torch.channels_last)
+    ref = m(x)
+    assert _graph_safe(m, None, 'strided') == 1
+    assert type(m[0]) is StridedConv1x1 and type(m[2]) is torch.nn.Conv2d
+    torch.testing.assert_close(m(x), ref)
+    m = net().to(memory_format=torch.channels_last)
+    pre = kfac.KFACPreconditioner(m)
+    assert _graph_safe(m, pre, 'gemm') == 2  # the model's two 1x1 convs
+    assert type(m[0]) is GemmConv1x1 and type(m[2]) is GemmConv1x1
+    assert type(m[3]) is torch.nn.Conv2d
+    torch.testing.assert_close(m(x), ref, rtol=1e-5, atol=1e-6)

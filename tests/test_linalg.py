@@ -28,3 +28,12 @@ def test_twostage_bucket_rule():
               1152: 4, 2048: 6, 2049: 1, 2304: 6, 4608: 3}
     assert linalg.twostage_sizes(neox) == set(neox)
     assert linalg.twostage_sizes(resnet) == set()
+
+
+def test_chain_waves_knob(monkeypatch) -> None:
+    from distributed_kfac_pytorch_amd.ops.linalg import _chain_waves
+
+    monkeypatch.delenv('KFAC_SYTRD_WAVES', raising=False)
+    assert _chain_waves(0) == 0 and _chain_waves(2) == 0  # 0 = the kernel's default
+    monkeypatch.setenv('KFAC_SYTRD_WAVES', '6144,2048')
+    assert [_chain_waves(g) for g in range(4)] == [6144, 2048, 2048, 2048]
