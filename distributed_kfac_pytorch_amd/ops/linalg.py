@@ -38,7 +38,8 @@ per call (``_repair_nonfinite``).
 Other knobs: ``KFAC_EIGH_STREAMS`` (lanes, default 8, capped at
 ``GPU_MAX_HW_QUEUES``), ``KFAC_EIGH_THREADS=0`` (issue every lane from the
 calling thread), ``KFAC_SYTRD_GRAPHS`` (replay chain segments from captured
-HIP graphs), ``KFAC_JACOBI_SWEEPS`` / ``KFAC_JACOBI_TOL``.
+HIP graphs), ``KFAC_SYTRD_WAVES`` / ``KFAC_SYTRD_SU`` (symv launch size /
+loads in flight per row), ``KFAC_JACOBI_SWEEPS`` / ``KFAC_JACOBI_TOL``.
 """
 from __future__ import annotations
 
@@ -449,7 +450,7 @@ def _launch_sytrd(
     """Large buckets: native tridiagonalisation chains (``_chain_groups``),
     one lane each, issued in segments that end where each bucket's size
     ends.  As soon as a segment is enqueued, an event marks it and that
-    bucket's tail (stedc + back-transform, ``_tail_job``) is issued on
+    bucket's tail (native divide and conquer + back-transform, ``_tail_job``) is issued on
     another lane behind the event, so tails run while the chains are still
     reducing the larger factors.  The small buckets' syevd share the
     non-chain lanes.  Only as many lanes as the process has hardware queues
