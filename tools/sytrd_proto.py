@@ -5,7 +5,8 @@ row k, panel width NB): per column k a ``col`` step (finalise column k-1,
 update row k with the panel's V/W, larfg partial sums) and a ``symv`` step
 (w = tau (A22 v - V Wᵀv - W Vᵀv)), and per panel a ``fin`` step plus the
 rank-2NB trailing update.  Checks A = Q T Qᵀ and the eigenvalues against
-numpy.  Run: python tools/sytrd_proto.py
+numpy.  Run: python tools/sytrd_proto.py (also checks the triangle-tile symv algebra
+of BASELINE.md round 4: slot-summed y and w.v = tau (v^T A22 v - 2 t1.t2))
 """
 from __future__ import annotations
 
@@ -15,7 +16,7 @@ import scipy.linalg
 NB = 8
 
 
-def sytrd(A: np.ndarray, nb: int = NB):
+def sytrd(A: np.ndarray, nb: int = NB, tri: bool = False, tt: int = 4):
     A = A.copy()
     n = A.shape[0]
     Wt = np.zeros((nb, n))
@@ -69,12 +70,41 @@ def sytrd(A: np.ndarray, nb: int = NB):
             v = np.concatenate([[1.0], s * x])
             t1 = np.array([Wt[j, k + 1] + s * dW[j] for j in range(i)])
             t2 = np.array([A[p + j, k + 1] + s * dV[j] for j in range(i)])
-            y = A[k + 1:, k + 1:] @ v
+            if tri:
+                # triangle-tile symv: lower
+                # tiles (I >= J) of the stale trailing matrix add A_IJ v_J to
+                # the row slots of I and A_IJ^T v_I to those of J; a row's
+                # y is the sum of its slots; w.v from the tiles' quadratic
+                # partials, w.v = tau (v^T A22 v - 2 t1.t2)
+                m = n - k - 1
+                nt = -(-m // tt)
+                slots = np.zeros((nt, m))
+                quad = 0.0
+                A22 = A[k + 1:, k + 1:]
+                for I in range(nt):
+                    for J in range(I + 1):
+                        ri = slice(I * tt, min(m, (I + 1) * tt))
+                        cj = slice(J * tt, min(m, (J + 1) * tt))
+                        blk = A22[ri, cj]
+                        slots[J, ri] += blk @ v[cj]
+                        qt = float(v[ri] @ (blk @ v[cj]))
+                        if I != J:
+                            slots[I, cj] += blk.T @ v[ri]
+                            qt *= 2.0
+                        quad += qt
+                y = slots.sum(axis=0)
+            else:
+                y = A[k + 1:, k + 1:] @ v
             for j in range(i):
                 y -= vrow(p, j, k + 1) * t1[j] + Wt[j, k + 1:] * t2[j]
             w = t * y
             Wt[i, k + 1:] = w
-            sc[k] = (t, s, float(w @ v))
+            wv = float(w @ v)
+            if tri:
+                wv_tiles = t * (quad - 2.0 * float(t1 @ t2))
+                assert abs(wv_tiles - wv) <= 1e-9 * max(1.0, abs(wv)), (k, wv_tiles, wv)
+                wv = wv_tiles
+            sc[k] = (t, s, wv)
         # panel end: finalise the last column, trailing rank-2nb update
         klast = q - 1
         if klast < n - 1:
@@ -98,17 +128,18 @@ def form_q(A, tau):
 
 def main() -> None:
     rng = np.random.default_rng(0)
-    for n in (1, 2, 3, 5, 8, 9, 17, 40):
+    for n, tri in ((1, False), (2, False), (3, False), (5, False), (8, False), (9, False),
+                   (17, False), (40, False), (9, True), (17, True), (40, True)):
         x = rng.standard_normal((n, 2 * n))
         M = x @ x.T / (2 * n)
-        R, d, e, tau = sytrd(M)
+        R, d, e, tau = sytrd(M, tri=tri)
         Q = form_q(R, tau)
         T = np.diag(d) + np.diag(e, 1) + np.diag(e, -1)
         err = np.abs(Q @ T @ Q.T - M).max()
         orth = np.abs(Q.T @ Q - np.eye(n)).max()
         w = scipy.linalg.eigh_tridiagonal(d, e, eigvals_only=True) if n > 1 else d
         ew = np.abs(np.sort(w) - np.linalg.eigvalsh(M)).max()
-        print(f'n={n:3d} recon={err:.2e} orth={orth:.2e} eig={ew:.2e}')
+        print(f'n={n:3d} tri={int(tri)} recon={err:.2e} orth={orth:.2e} eig={ew:.2e}')
         assert err < 1e-10 and orth < 1e-10 and ew < 1e-10
 
 
