@@ -102,13 +102,53 @@ def make_graph_safe(model: nn.Module, mode: str | None = None) -> int:
 
 
 
+def _splitk(m: int) -> int:
+    """Slabs of the weight-gradient reduction over ``m`` = N*H*W rows: the
+    largest power of two that divides ``m`` and leaves >= 2048 rows each."""
+    s = 1
+    while m % (2 * s) == 0 and m // (2 * s) >= 2048:
+        s *= 2
+    return s
+
+
+class _Conv1x1Gemm(torch.autograd.Function):
+    """``Y = X W^T (+ b)`` on the NHWC activation matrix, with the weight
+    gradient ``dW = dY^T X`` reduced in slabs: one GEMM with K = N*H*W
+    (100k rows at the 56x56 stage) leaves a 64x256 output to a handful of
+    workgroups, while a batched GEMM over ``_splitk`` slabs plus a sum
+    spreads it over the chip."""
+
+    @staticmethod
+    def forward(ctx, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None) -> torch.Tensor:  # type: ignore[override]
+        ctx.save_for_backward(x, w)
+        ctx.has_bias = b is not None
+        return F.linear(x, w, b)
+
+    @staticmethod
+    def backward(ctx, gy: torch.Tensor) -> tuple:  # type: ignore[override]
+        x, w = ctx.saved_tensors
+        gy = gy.contiguous()
+        gx = gy @ w if ctx.needs_input_grad[0] else None
+        gw = None
+        if ctx.needs_input_grad[1]:
+            m = gy.shape[0]
+            s = _splitk(m)
+            if s > 1:
+                part = torch.bmm(gy.view(s, m // s, -1).transpose(1, 2), x.view(s, m // s, -1))
+                gw = part.sum(0, dtype=torch.promote_types(w.dtype, torch.float32)).to(w.dtype)
+            else:
+                gw = gy.t() @ x
+        gb = gy.sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        return gx, gw, gb
+
+
 class GemmConv1x1(StridedConv1x1):
     """``nn.Conv2d`` (1x1, unpadded, undilated, ungrouped, any stride) on
     channels_last activations evaluated as one GEMM:
     ``Y[NHW, Cout] = X[NHW, Cin] W[Cout, Cin]^T`` on the NHWC activation
     matrix (a strided conv first subsamples, as ``StridedConv1x1``).  The
-    backward is two GEMMs (``dX = dY W``, ``dW = dY^T X``) through
-    hipBLASLt.  Same module, parameters and state-dict keys; other layouts
+    backward is ``dX = dY W`` and a slab-reduced ``dW = dY^T X``
+    (``_Conv1x1Gemm``), all hipBLASLt.  Same module, parameters and state-dict keys; other layouts
     or groups fall back to the convolution."""
 
     def _conv_forward(  # type: ignore[override]
@@ -124,8 +164,15 @@ class GemmConv1x1(StridedConv1x1):
         if (sh, sw) != (1, 1):
             x = input[:, :, ::sh, ::sw].contiguous(memory_format=torch.channels_last)
         n, c, h, w = x.shape
-        y = F.linear(x.permute(0, 2, 3, 1).reshape(n * h * w, c),
-                     weight.view(weight.shape[0], c), bias)
+        x2 = x.permute(0, 2, 3, 1).reshape(n * h * w, c)
+        w2 = weight.view(weight.shape[0], c)
+        dev = x.device.type
+        if torch.is_autocast_enabled(dev):
+            dt = torch.get_autocast_dtype(dev)
+            x2, w2 = x2.to(dt), w2.to(dt)
+            bias = bias.to(dt) if bias is not None else None
+        with torch.autocast(dev, enabled=False):
+            y = _Conv1x1Gemm.apply(x2, w2, bias)
         return y.view(n, h, w, -1).permute(0, 3, 1, 2)
 
 

@@ -26,6 +26,7 @@ import torch.nn.functional as F  # noqa: E402
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from distributed_kfac_pytorch_amd.models.resnet import resnet50  # noqa: E402
+from distributed_kfac_pytorch_amd.ops.conv import _Conv1x1Gemm  # noqa: E402
 
 
 def shapes(batch: int, image: int) -> list[tuple[int, int, int, int]]:
@@ -70,7 +71,7 @@ def main() -> None:
     args = ap.parse_args()
     dev = torch.device('cuda', 0)
     dt = torch.bfloat16 if args.bf16 else torch.float32
-    tot = {'miopen': 0.0, 'gemm': 0.0}
+    tot = {'miopen': 0.0, 'gemm': 0.0, 'gemm_plain': 0.0}
     for h, w, ci, co, cnt in shapes(args.batch, args.image):
         x = torch.randn(args.batch, ci, h, w, device=dev, dtype=dt).contiguous(
             memory_format=torch.channels_last).requires_grad_(True)
@@ -82,20 +83,27 @@ def main() -> None:
             y = F.conv2d(x, wt)
             return (y,) + torch.autograd.grad(y, (x, wt), gy)
 
-        def gemm() -> tuple:
+        def gemm() -> tuple:  # ops/conv.py GemmConv1x1 (slab-reduced dW)
+            xm = x.permute(0, 2, 3, 1).reshape(-1, ci)
+            ym = _Conv1x1Gemm.apply(xm, wt.view(co, ci), None)
+            y = ym.view(args.batch, h, w, co).permute(0, 3, 1, 2)
+            return (y,) + torch.autograd.grad(y, (x, wt), gy)
+
+        def gemm_plain() -> tuple:  # one GEMM per product (dW with K = N*H*W)
             xm = x.permute(0, 2, 3, 1).reshape(-1, ci)
             ym = xm @ wt.view(co, ci).t()
             y = ym.view(args.batch, h, w, co).permute(0, 3, 1, 2)
             return (y,) + torch.autograd.grad(y, (x, wt), gy)
 
         a, b = miopen(), gemm()
-        rel = max(float((p.float() - q.float()).abs().max() / q.float().abs().max())
+        rel = max(float((p.detach().float() - q.detach().float()).abs().max() / q.detach().float().abs().max())
                   for p, q in zip(a, b))
-        tm, tg = timed(miopen), timed(gemm)
+        tm, tg, tp = timed(miopen), timed(gemm), timed(gemm_plain)
         tot['miopen'] += cnt * tm
         tot['gemm'] += cnt * tg
+        tot['gemm_plain'] += cnt * tp
         print(json.dumps({'shape': [args.batch, ci, h, w, co], 'count': cnt, 'miopen_us': round(tm, 1),
-                          'gemm_us': round(tg, 1), 'maxrel': rel,
+                          'gemm_us': round(tg, 1), 'gemm_plain_us': round(tp, 1), 'maxrel': rel,
                           'y_strides_gemm': list(b[0].stride()),
                           'dx_cl': b[1].is_contiguous(memory_format=torch.channels_last)}),
               flush=True)

@@ -96,7 +96,7 @@ def build(args: argparse.Namespace, dev: torch.device):  # type: ignore[no-untyp
         loss.backward()
         return loss
 
-    runner = GraphedTrainStep(fb, opt, pre, warmup=1, enabled=True)
+    runner = GraphedTrainStep(fb, opt, pre, warmup=1, enabled=True, conv_mode=args.conv_mode)
     return model, opt, pre, runner
 
 
@@ -112,6 +112,8 @@ def _state(model, opt) -> list[torch.Tensor]:  # type: ignore[no-untyped-def]
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument('--bf16', action='store_true')
+    ap.add_argument('--conv-mode', default=None, choices=[None, 'strided', 'gemm'],
+                    help="GraphedTrainStep conv_mode (bench: 'gemm' under bf16)")
     ap.add_argument('--no-kfac', action='store_true')
     ap.add_argument('--image', type=int, default=224)
     ap.add_argument('--batch', type=int, default=32)
