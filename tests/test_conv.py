@@ -66,3 +66,33 @@ def test_use_gemm_conv1x1_switches_every_1x1() -> None:
     x = torch.randn(2, 3, 32, 32).contiguous(memory_format=torch.channels_last)
     m = m.to(memory_format=torch.channels_last)
     assert torch.isfinite(m(x)).all()
+
+
+@pytest.mark.parametrize('shape', [(4, 16, 56, 56, 32, True), (2, 8, 7, 7, 16, False),
+                                   (8, 64, 28, 28, 128, True)])
+def test_gemm_conv1x1_slab_weight_grad_matches_conv(shape) -> None:
+    """``GemmConv1x1``'s weight gradient, reduced in ``_splitk`` slabs,
+    equals the convolution's (float64)."""
+    from distributed_kfac_pytorch_amd.ops.conv import _splitk
+
+    n, c, h, w, co, bias = shape
+    torch.manual_seed(0)
+    a = nn.Conv2d(c, co, 1, bias=bias).double()
+    b = nn.Conv2d(c, co, 1, bias=bias).double()
+    b.load_state_dict(a.state_dict())
+    b.__class__ = GemmConv1x1
+    x = torch.randn(n, c, h, w, dtype=torch.float64).contiguous(
+        memory_format=torch.channels_last).requires_grad_()
+    x2 = x.detach().clone().contiguous(memory_format=torch.channels_last).requires_grad_()
+    ya, yb = a(x), b(x2)
+    g = torch.randn_like(ya)
+    ya.backward(g)
+    yb.backward(g)
+    torch.testing.assert_close(yb, ya, rtol=1e-12, atol=1e-12)
+    torch.testing.assert_close(x2.grad, x.grad, rtol=1e-12, atol=1e-12)
+    torch.testing.assert_close(b.weight.grad, a.weight.grad, rtol=1e-10, atol=1e-10)
+    if bias:
+        torch.testing.assert_close(b.bias.grad, a.bias.grad, rtol=1e-10, atol=1e-10)
+    m = n * h * w
+    s = _splitk(m)
+    assert m % s == 0 and (s == 1 or m // s >= 2048)
