@@ -61,6 +61,10 @@ def add_common_args(p: argparse.ArgumentParser, *, batch_size: int, epochs: int,
                         '(distributed_kfac_pytorch_amd.graphs.GraphedTrainStep; single-rank '
                         'jobs, or KFAC_STEP_GRAPHS_MULTI=1; no gradient accumulation, no fp16 '
                         'GradScaler); K-FAC second-order updates stay eager')
+    p.add_argument('--conv1x1', default='miopen', choices=['miopen', 'gemm'],
+                   help='gemm: 1x1 convolutions as GEMMs on the NHWC activation matrix '
+                        '(distributed_kfac_pytorch_amd.ops.conv.GemmConv1x1, same values; '
+                        "the bench's default, channels_last CUDA only)")
     p.add_argument('--no-resume', dest='resume', action='store_false', default=True)
 
 
@@ -80,6 +84,9 @@ def run(args: argparse.Namespace,
     model = build_model(args).to(args.device)
     if args.channels_last and args.cuda:
         model = model.to(memory_format=torch.channels_last)
+        if getattr(args, 'conv1x1', 'miopen') == 'gemm':
+            from distributed_kfac_pytorch_amd.ops.conv import use_gemm_conv1x1
+            use_gemm_conv1x1(model)
     if args.world_size > 1:
         ctx = contextlib.nullcontext()
         if getattr(args, 'graphs', 0) and args.cuda:
