@@ -15,10 +15,16 @@ python3 -c "import json;d=json.loads(open('$O/rehearsal_gloo_w2.json').read().st
 python3 -c "import json;d=json.loads(open('$O/bench_driver_cmd.json').read().strip().splitlines()[-1]);print(d['value'],d['kind_ms'],d.get('kfac_overhead_ms'),d.get('step_graphs'));print(d['bf16'])"
 timeout -k 10 200 python3 -u tools/conv1x1_probe.py --bf16 > $O/conv1x1_bf16.jsonl 2> $O/conv.err || exit 1
 tail -1 $O/conv1x1_bf16.jsonl
+timeout -k 10 200 python3 -u tools/conv1x1_probe.py > $O/conv1x1_fp32.jsonl 2>> $O/conv.err || exit 1
+tail -1 $O/conv1x1_fp32.jsonl
 timeout -k 10 600 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_graphs_refresh_gpu.py tests/test_conv.py > $O/pytest_graphs.log 2>&1 || { tail -20 $O/pytest_graphs.log; exit 1; }
 tail -2 $O/pytest_graphs.log
 timeout -k 10 400 python3 -u tools/graph_oop_audit.py --bf16 --conv-mode gemm --deterministic 0 > $O/audit_bf16_gemm.jsonl 2> $O/audit.err || exit 1
 tail -2 $O/audit_bf16_gemm.jsonl | cut -c1-400
 timeout -k 10 400 python3 bench.py --bf16 --steps 100 --warmup 10 --baseline 0 > $O/bench_bf16.json 2> $O/bench_bf16.err || exit 1
 python3 -c "import json;d=json.load(open('$O/bench_bf16.json'));print('bf16', d['value'], d['kind_ms'], d.get('step_graphs'), d.get('host_issue_ms'), d['params_finite'])"
+for m in miopen gemm; do
+  timeout -k 10 400 python3 bench.py --steps 100 --warmup 10 --secondary-bf16 0 --conv1x1 $m > $O/bench_fp32_$m.json 2>> $O/bench_fp32.err || exit 1
+  python3 -c "import json;d=json.load(open('$O/bench_fp32_$m.json'));print('fp32 $m', d['value'], d['kind_ms'], d.get('sgd_ms_per_step'), d['params_finite'])"
+done
 du -sh gpurun_out
