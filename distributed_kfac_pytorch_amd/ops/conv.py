@@ -1,4 +1,16 @@
-"""Graph-safe strided 1x1 convolutions.
+"""1x1 convolutions: graph-safe strided form and GEMM form.
+
+Two modules replace ``nn.Conv2d`` 1x1 convolutions in place (same
+parameters, state-dict keys and values):
+
+* ``StridedConv1x1`` -- a strided 1x1 convolution as subsample + stride-1
+  convolution (graph-safe, see below; the in-tree ResNets build their
+  projection shortcuts with it);
+* ``GemmConv1x1`` -- on channels_last activations, forward and ``dX`` as
+  hipBLASLt GEMMs on the NHWC activation matrix and ``dW`` reduced in slabs
+  (``_Conv1x1Gemm``); no MIOpen solver at all, and faster than MIOpen's 1x1
+  solvers end to end (the bench default, ``bench.py --conv1x1``; required
+  inside bf16 graphs, ``GraphedTrainStep(conv_mode='gemm')``).
 
 Root cause of the whole-step graph corruption of rounds 2-3
 (``profiles/graph_replay_r3_investigation.txt``; found with
