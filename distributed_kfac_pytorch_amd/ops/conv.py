@@ -131,7 +131,9 @@ class _Conv1x1Gemm(torch.autograd.Function):
     spreads it over the chip."""
 
     @staticmethod
-    def forward(ctx, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None) -> torch.Tensor:  # type: ignore[override]
+    def forward(  # type: ignore[override]
+        ctx, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None,
+    ) -> torch.Tensor:
         ctx.save_for_backward(x, w)
         ctx.has_bias = b is not None
         return F.linear(x, w, b)
