@@ -114,11 +114,16 @@ def make_graph_safe(model: nn.Module, mode: str | None = None) -> int:
 
 
 
-def _splitk(m: int) -> int:
+_SLAB_ROWS = int(os.environ.get('KFAC_CONV1X1_SLAB_ROWS', '2048'))
+
+
+def _splitk(m: int, rows: int | None = None) -> int:
     """Slabs of the weight-gradient reduction over ``m`` = N*H*W rows: the
-    largest power of two that divides ``m`` and leaves >= 2048 rows each."""
+    largest power of two that divides ``m`` and leaves >= ``rows`` rows each
+    (``KFAC_CONV1X1_SLAB_ROWS``, default 2048)."""
+    rows = rows or _SLAB_ROWS
     s = 1
-    while m % (2 * s) == 0 and m // (2 * s) >= 2048:
+    while m % (2 * s) == 0 and m // (2 * s) >= rows:
         s *= 2
     return s
 
