@@ -18,10 +18,29 @@ one's eager work lands between the other's replays), at the bench shape
 weight casts in bf16), with refreshes inside the replay window.  With
 deterministic MIOpen every replayed step must equal the eager twin's to the
 bit, and parameters must stay finite.
+
+MIOpen is not always deterministic, though: ``cudnn.deterministic`` (and
+``torch.use_deterministic_algorithms``) does not keep it from running a
+solver that accumulates with atomics when its database selects one.  With
+the bench's tuned database two EAGER twins already differ at step 0, with a
+fresh one they were bit-identical over 40 steps, eager and graphed alike;
+within a long pytest session the database is filled by the earlier tests'
+find calls, and one full-suite run saw a step that both twins ran eagerly
+(a K-FAC factor step, not a replay) diverge after ten bit-exact steps
+(``tools/determinism_probe.py``, profiles/determinism_r4.md).  Once twins
+have diverged they cannot be compared at any tolerance: two eager twins
+under the tuned database drift apart chaotically (global parameter
+difference 3e-4 after one step, 9e-3 after 18; BN gradients uncorrelated
+from step 1).  So the twins are compared bit for bit up to the first
+mismatch; the mismatching step -- the only one that starts from identical
+state -- must stay within one step of solver noise (measured eager vs
+eager: parameters 5e-6, un-preconditioned gradients 0.09); from there on
+the graphed model must stay finite and keep replaying.
 """
 from __future__ import annotations
 
 import copy
+import warnings
 
 import pytest
 import torch
@@ -73,6 +92,11 @@ def _build(base: torch.nn.Module, cuda: torch.device, graphs: bool, amp: bool,
     return model, pre, x, y, runner
 
 
+def _rel(p: torch.Tensor, q: torch.Tensor) -> float:
+    p, q = p.detach().double(), q.detach().double()
+    return float((p - q).norm() / q.norm().clamp_min(1e-12))
+
+
 @pytest.mark.parametrize('amp,use_kfac,kinds,conv_mode', [
     (True, True, ('plain',), None),
     (True, True, ('plain',), 'gemm'),  # the bench's bf16 mode
@@ -91,6 +115,9 @@ def test_graph_replay_interleaved_with_eager_twin(cuda, amp, use_kfac, kinds, co
         steps = 18  # K-FAC refreshes at steps 0, 8, 16
         A = _build(base, cuda, True, amp, use_kfac, kinds, conv_mode)
         B = _build(base, cuda, False, amp, use_kfac, conv_mode=conv_mode)
+        first_bad = None
+        pre_ids = set() if A[1] is None else {
+            id(p) for _, layer in A[1]._layers.values() for p in layer.module.module.parameters()}
         for i in range(steps):
             x, y = pool[i % len(pool)]
             for m in (A, B):
@@ -101,9 +128,25 @@ def test_graph_replay_interleaved_with_eager_twin(cuda, amp, use_kfac, kinds, co
             torch.cuda.synchronize()
             pa, pb = list(A[0].parameters()), list(B[0].parameters())
             assert all(bool(torch.isfinite(p).all()) for p in pa), f'non-finite params at step {i}'
+            if first_bad is not None:
+                continue
             bad = [n for (n, _), p, q in zip(A[0].named_parameters(), pa, pb)
                    if not torch.equal(p, q) or not torch.equal(p.grad, q.grad)]
-            assert not bad, (i, len(bad), bad[:3])
+            if bad and first_bad is None:
+                first_bad = (i, len(bad), bad[:3])
+                # one step of solver noise from identical state: parameters as a
+                # whole (zero-initialised biases are all update), the gradients
+                # K-FAC does not precondition one by one
+                dp = _rel(torch.cat([p.detach().flatten() for p in pa]),
+                          torch.cat([q.detach().flatten() for q in pb]))
+                dg, dn = max(((_rel(p.grad, q.grad), n) for (n, p), q
+                              in zip(A[0].named_parameters(), pb)
+                              if id(p) not in pre_ids), default=(0.0, None))
+                assert all(bool(torch.isfinite(p.grad).all()) for p in pa), i
+                assert dp <= 1e-4 and dg <= 0.5, (first_bad, dp, dg, dn)
+                warnings.warn(f'graphed and eager twins diverged at step {i} on {len(bad)} '
+                              f'parameters ({bad[:3]}; rel. parameter difference {dp:.1e}, '
+                              f'gradient {dg:.2e} at {dn}): MIOpen solver nondeterminism')
         run = A[4]
         assert isinstance(run, GraphedTrainStep)
         assert run.captures == (len(kinds) if use_kfac else 1), run.captures
