@@ -403,6 +403,9 @@ class BaseKFACPreconditioner:
             )
         # early preconditioning (set up at the first step, _setup_early)
         self._early: dict[str, Any] | None = None
+        # packed factor buffers are laid out once, before the first factor
+        # update (_plan_packed)
+        self._packed_planned = False
 
     # ----------------------------------------------------------------- repr
     def __repr__(self) -> str:
@@ -610,6 +613,7 @@ class BaseKFACPreconditioner:
             not self._update_factors_in_hook
             and self.steps % self.factor_update_steps == 0
         ):
+            self._plan_packed()
             with tracing.phase('factor_update'):
                 decay = self.factor_decay
                 for name, layer in ordered:
@@ -871,6 +875,29 @@ class BaseKFACPreconditioner:
         sizes['total'] = sum(sizes.values())
         return sizes
 
+    def _plan_packed(self) -> None:
+        """Reserve every packed factor slot in hook order -- A factors in
+        forward (registration) order, then G factors in backward order -- so
+        each group's ``PackedFactorBuffer`` is allocated once at its final
+        size and its chunks complete (and launch from the hooks) in the order
+        the hooks fill them."""
+        if self._packed_planned:
+            return
+        self._packed_planned = True
+        layers = list(self._layers.values())
+        order = [(n, l, 'A') for n, l in layers] + [(n, l, 'G') for n, l in reversed(layers)]
+        plans: dict[Any, list] = {}
+        for name, layer, which in order:
+            group = self._assignment.factor_group(name, which)
+            if not layer._packed_ok(group):
+                continue
+            shape = layer.module.a_factor_shape if which == 'A' else layer.module.g_factor_shape
+            d = int(shape[0])
+            key = (group, torch.float32, layer.module.device)
+            plans.setdefault(key, []).append(((id(layer), which), d * (d + 1) // 2))
+        for (group, dtype, device), layout in plans.items():
+            self._tdc.packed_buffer(group, dtype, device).reserve(layout, dtype, device)
+
     # ----------------------------------------------------------------- hooks
     def _forward_hook(
         self,
@@ -894,7 +921,9 @@ class BaseKFACPreconditioner:
     def _stream_friendly_backend() -> bool:
         """Collectives that stay device-side: RCCL ('nccl') orders its
         all-reduce after the issuing (side) stream with a HIP event, so the
-        factor SYRK + all-reduce chain overlaps forward / backward.  gloo
+        factor SYRKs and the all-reduce of every packed-factor chunk they
+        complete (launched from the hook, ``PackedFactorBuffer.mark``)
+        overlap the rest of forward / backward.  gloo
         stages GPU tensors through the host: there the side stream only adds
         host round trips (2-rank gloo rehearsal on one GPU: factor phases
         65-236 ms/step against <1 ms inline,
@@ -968,6 +997,8 @@ class BaseKFACPreconditioner:
             return
         if self.steps % self.factor_update_steps != 0:
             return
+        if not self._packed_planned:
+            self._plan_packed()
         name, layer = self._layers[module]
         self._mini_steps[name] += 1
         in_hook = (

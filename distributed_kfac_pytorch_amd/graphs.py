@@ -180,8 +180,10 @@ class GraphedTrainStep:
         model: torch.nn.Module | None = None,
         stream: torch.cuda.Stream | None = None,
         conv_mode: str | None = None,
+        verify: bool | None = None,
     ) -> None:
         self.forward_backward = forward_backward
+        self.model = model
         self.optimizer = optimizer
         self.preconditioner = preconditioner
         if isinstance(model, torch.nn.parallel.DistributedDataParallel):
@@ -198,11 +200,19 @@ class GraphedTrainStep:
         self.stream = stream
         if enabled and self.stream is None:
             self.stream = step_stream()
+        self.conv_mode = conv_mode or os.environ.get('KFAC_GRAPH_SAFE_CONV', 'strided')
         if enabled:
             # 1x1 convolutions through the graph-safe formulations (some
             # MIOpen solvers read memory outside the graph: ops/conv.py); the
             # model's, or at least K-FAC's layers'
-            _graph_safe(model, preconditioner, conv_mode)
+            _graph_safe(model, preconditioner, self.conv_mode)
+        if verify is None:
+            verify = os.environ.get('KFAC_GRAPH_VERIFY', '1') != '0'
+        self.verify = verify
+        # autocast seen by a convolution during the eager warmup steps
+        self.autocast_dtype: torch.dtype | None = None
+        self._probe_handles: list = []
+        self.verify_report: dict[str, dict] = {}
         # Step kinds replayed from graphs.  Factor-update steps stay eager by
         # default: their SYRKs run on the factor side stream concurrently with
         # backward, and a replayed graph executes its nodes in one queue, so
@@ -232,6 +242,7 @@ class GraphedTrainStep:
         self.captures = 0
         self.eager_steps = 0
         self._inverse_done = preconditioner is None
+        self._caller: torch.cuda.Stream | None = None
 
     # ------------------------------------------------------------ helpers
     def kind(self) -> str:
@@ -259,17 +270,58 @@ class GraphedTrainStep:
     def _params(self) -> list:
         return [q for group in self.optimizer.param_groups for q in group['params']]
 
+    def _conv_modules(self) -> list:
+        mods = list(self.model.modules()) if self.model is not None else [
+            layer.module.module for _, layer in
+            (getattr(self.preconditioner, '_layers', None) or {}).values()]
+        return [m for m in mods if isinstance(m, torch.nn.Conv2d)]
+
+    def _probe_autocast(self) -> None:
+        """Record, from a forward pre-hook on the convolutions, whether the
+        step runs them under 16-bit autocast (removed again after the step)."""
+        def hook(mod: torch.nn.Module, inp: Any) -> None:
+            if torch.is_autocast_enabled('cuda'):
+                dt = torch.get_autocast_dtype('cuda')
+                if dt in (torch.bfloat16, torch.float16):
+                    self.autocast_dtype = dt
+        self._probe_handles = [m.register_forward_pre_hook(hook) for m in self._conv_modules()]
+
+    def _end_probe(self) -> None:
+        for h in self._probe_handles:
+            h.remove()
+        self._probe_handles = []
+        if self.autocast_dtype is not None and self.conv_mode != 'gemm':
+            # MIOpen's tuned 16-bit 1x1 backward-weights solvers read memory
+            # outside a captured graph (ops/conv.py): every 1x1 convolution
+            # goes through the GEMM formulation before anything is captured
+            n = _graph_safe(self.model, self.preconditioner, 'gemm')
+            logger.warning('step runs under %s autocast: conv_mode %r -> \'gemm\' '
+                           '(%d 1x1 convolutions as GEMMs)', self.autocast_dtype,
+                           self.conv_mode, n)
+            self.conv_mode = 'gemm'
+
     def _eager(self) -> torch.Tensor:
-        self.optimizer.zero_grad(set_to_none=False)
-        loss = self.forward_backward()
-        if self.preconditioner is not None:
-            self.preconditioner.step()
-        self.optimizer.step()
+        probe = self.enabled and not self.graphs and self.captures == 0
+        if probe:
+            self._probe_autocast()
+        try:
+            loss = self._eager_step()
+        finally:
+            if probe:
+                self._end_probe()
         self.eager_steps += 1
         # detached: a caller holding the loss must not keep this step's
         # autograd graph (and its AccumulateGrad nodes, bound to the eager
         # stream) alive across the next capture
         return loss.detach()
+
+    def _eager_step(self) -> torch.Tensor:
+        self.optimizer.zero_grad(set_to_none=False)
+        loss = self.forward_backward()
+        if self.preconditioner is not None:
+            self.preconditioner.step()
+        self.optimizer.step()
+        return loss
 
     def _advance(self) -> None:
         """Host-side K-FAC state change of one replayed step."""
@@ -356,13 +408,138 @@ class GraphedTrainStep:
         self.grads[kind] = [q.grad for q in self._params()]
         self.captures += 1
 
+    # ------------------------------------------------------- verification
+    def _state(self, kind: str) -> list[torch.Tensor]:
+        """Every tensor a step of ``kind`` reads and writes besides its
+        inputs: parameters, module buffers (BN statistics), optimizer state
+        and, for factor-update steps, the K-FAC factors."""
+        out: list[torch.Tensor] = []
+        seen: set[int] = set()
+
+        def add(t: Any) -> None:
+            if isinstance(t, torch.Tensor) and t.is_cuda and id(t) not in seen:
+                seen.add(id(t))
+                out.append(t)
+        for q in self._params():
+            add(q)
+        if self.model is not None:
+            for b in self.model.buffers():
+                add(b)
+        for st in self.optimizer.state.values():
+            for v in st.values():
+                add(v)
+        p = self.preconditioner
+        if p is not None and kind == 'factor':
+            for _, layer in p._layers.values():
+                add(layer.a_factor)
+                add(layer.g_factor)
+        return out
+
+    def _verify(self, kind: str) -> bool:
+        """Capture-time self-check of the ``kind`` graph.
+
+        From one saved state (and CUDA RNG state) run the step eagerly twice
+        and replay the graph twice.  Eager vs eager is the noise floor of the
+        step's nondeterministic kernels (atomics in MIOpen solvers); a replay
+        must agree with the eager step, and with the other replay, within
+        ``max(10 x noise, 1e-3)`` -- relative to the parameter update and to
+        the gradient norm -- and be finite.  A graph that depends on memory
+        or library state outside the capture (the round-2..4 failures:
+        free global-pool blocks, MIOpen solvers) fails it.  The state is
+        restored afterwards."""
+        p = self.preconditioner
+        state = self._state(kind)
+        with torch.no_grad():
+            saved = [t.detach().clone() for t in state]
+        rng = torch.cuda.get_rng_state()
+        steps = p._steps if p is not None else 0
+        at = self._next_step_of(kind) if p is not None else 0
+        params = self._params()
+
+        def restore() -> None:
+            with torch.no_grad():
+                for t, s0 in zip(state, saved):
+                    t.copy_(s0)
+            torch.cuda.set_rng_state(rng)
+
+        def snap(grads: list) -> tuple[list, list]:
+            return ([q.detach().clone() for q in params],
+                    [None if g is None else g.detach().clone() for g in grads])
+
+        def eager() -> tuple[list, list]:
+            restore()
+            if p is not None:
+                p._steps = at
+            self._eager_step()
+            if p is not None:
+                p._steps = steps
+                p._mini_steps = defaultdict(int)
+                p._mini_steps_g = defaultdict(int)
+            return snap([q.grad for q in params])
+
+        def replay() -> tuple[list, list]:
+            restore()
+            self.graphs[kind].replay()
+            return snap(self.grads[kind])
+
+        p0 = [q.detach().clone() for q in params]
+        e1, e2 = eager(), eager()
+        r1, r2 = replay(), replay()
+        restore()
+
+        @torch.no_grad()
+        def dist_(a: tuple, b: tuple) -> tuple[float, float]:
+            num = den = gnum = gden = torch.zeros((), dtype=torch.float64, device=p0[0].device)
+            for x, y, z in zip(a[0], b[0], p0):
+                num = num + (x.double() - y.double()).square().sum()
+                den = den + (y.double() - z.double()).square().sum()
+            for x, y in zip(a[1], b[1]):
+                if x is None or y is None:
+                    continue
+                gnum = gnum + (x.double() - y.double()).square().sum()
+                gden = gden + y.double().square().sum()
+            v = torch.stack([num, den, gnum, gden]).cpu().tolist()
+            dp = (v[0] / v[1]) ** 0.5 if v[1] > 0 else (0.0 if v[0] == 0 else float('inf'))
+            dg = (v[2] / v[3]) ** 0.5 if v[3] > 0 else (0.0 if v[2] == 0 else float('inf'))
+            return dp, dg
+
+        noise = max(dist_(e2, e1))
+        worst = max(max(dist_(r1, e1)), max(dist_(r2, e1)), max(dist_(r2, r1)))
+        finite = all(bool(torch.isfinite(t).all()) for r in (r1, r2) for t in r[0])
+        tol = max(10.0 * noise, 1e-3)
+        ok = finite and worst <= tol  # NaN compares False
+        self.verify_report[kind] = {'noise': noise, 'worst': worst, 'tol': tol,
+                                    'finite': finite, 'ok': ok}
+        if not ok:
+            logger.warning('step graph %r failed its capture-time check (replay vs eager %.3g, '
+                           'eager noise %.3g, finite %s): graphs dropped, running eagerly',
+                           kind, worst, noise, finite)
+        return ok
+
+    def _drop_graphs(self) -> None:
+        """Give up on graphs: run every later step eagerly, on a fresh
+        stream ordered after the caller's and the old step stream's work."""
+        old = self.stream
+        self.enabled = False
+        self.stream = torch.cuda.Stream()
+        self.stream.wait_stream(self._caller or torch.cuda.current_stream())
+        if old is not None:
+            self.stream.wait_stream(old)
+        self.graphs.clear()
+        self.outputs.clear()
+        self.grads.clear()
+        _native.flush_table_uploads()
+        gc.collect()
+
     # --------------------------------------------------------------- step
     def __call__(self) -> torch.Tensor:
-        if not self.enabled or self.stream is None:
-            return self._call()
-        caller = torch.cuda.current_stream()
-        if caller == self.stream:
-            return self._call()
+        caller = torch.cuda.current_stream() if torch.cuda.is_available() else None
+        self._caller = caller
+        if not self.enabled or self.stream is None or caller == self.stream:
+            out = self._call()
+            if self.stream is not None and caller is not None and caller != self.stream:
+                caller.wait_stream(self.stream)  # graphs were dropped mid-call
+            return out
         self.stream.wait_stream(caller)
         with torch.cuda.stream(self.stream):
             out = self._call()
@@ -398,6 +575,9 @@ class GraphedTrainStep:
                         self._capture(k)
                     except Exception as e:  # noqa: BLE001
                         failed = repr(e)
+                    if failed is None and self.verify and k in self.graphs:
+                        if not self._verify(k):
+                            failed = f'capture-time check failed: {self.verify_report[k]}'
                     if failed is not None:
                         # something in the step is not capturable: run eagerly.
                         # (Outside the except block: the exception's traceback
@@ -406,14 +586,8 @@ class GraphedTrainStep:
                         logger.warning('step graph capture failed (%s); running eagerly', failed)
                         if self.preconditioner is not None:
                             self.preconditioner._steps = self._steps_before_capture
-                        self.enabled = False
                         # a stream whose capture was invalidated is not reused
-                        self.stream = torch.cuda.Stream()
-                        self.graphs.clear()
-                        self.outputs.clear()
-                        self.grads.clear()
-                        _native.flush_table_uploads()
-                        gc.collect()
+                        self._drop_graphs()
                         with torch.cuda.stream(self.stream):
                             return self._eager()
             if kind not in self.graphs:

@@ -153,7 +153,13 @@ class _Conv1x1Gemm(torch.autograd.Function):
             m = gy.shape[0]
             s = _splitk(m)
             if s > 1:
-                part = torch.bmm(gy.view(s, m // s, -1).transpose(1, 2), x.view(s, m // s, -1))
+                a, b = gy.view(s, m // s, -1).transpose(1, 2), x.view(s, m // s, -1)
+                if gy.is_cuda and gy.dtype in (torch.bfloat16, torch.float16):
+                    # fp32 slab partials (no per-slab rounding to 16 bits
+                    # before the sum): hipBLASLt's fp32-output GEMM
+                    part = torch.bmm(a, b, out_dtype=torch.float32)
+                else:
+                    part = torch.bmm(a, b)
                 gw = part.sum(0, dtype=torch.promote_types(w.dtype, torch.float32)).to(w.dtype)
             else:
                 gw = gy.t() @ x

@@ -33,6 +33,7 @@ MI355X-first design differences (behaviour visible to callers is the same):
 """
 from __future__ import annotations
 
+import collections
 from typing import Any
 from typing import Callable
 from typing import Union
@@ -242,15 +243,29 @@ class PackedFactorBuffer:
     """Persistent all-reduce buffer of the packed factor triangles of one
     process group (see the module docstring).
 
-    Slots are assigned in first-use order -- identical on every rank, since
-    every rank registers the same factors in the same order -- and never
-    move once the buffer has been launched (a later registration re-allocates
-    the buffer and copies it, after waiting for every collective in flight).
-    ``launch()`` all-reduces, in cap-sized contiguous chunks, every chunk
-    holding a slot marked since the previous launch.
+    Layout: the preconditioner ``reserve()``s every factor of the group once,
+    before the first factor update -- A factors in forward order, then G
+    factors in backward order, i.e. the order the hooks produce them -- and
+    the buffer is allocated ONCE at its final size.  A factor that was not
+    reserved still gets a slot on first use (the buffer is then re-allocated
+    and copied, after waiting for every collective in flight); slots never
+    move otherwise.  The layout is identical on every rank: every rank
+    registers the same layers in the same order.
+
+    Launch: the buffer is cut into contiguous cap-sized chunks.  With
+    ``eager_launch`` (default; ``KFAC_PACKED_EAGER_LAUNCH=0`` turns it off) a
+    chunk is all-reduced from ``mark()`` -- i.e. from the forward / backward
+    hook, on the stream that just wrote the slot -- as soon as EVERY slot of
+    the chunk has been marked, so the factor all-reduce overlaps the rest of
+    forward / backward as the reference's hook-launched buckets do
+    (``kfac/distributed.py:299-368``, ``kfac/base_preconditioner.py:450-477``).
+    ``launch()`` (from ``step()``) all-reduces the chunks still holding marked
+    slots.  Chunks complete in hook order, which is the same on every rank,
+    so every rank issues the same collective sequence.
     """
 
-    def __init__(self, group: dist.ProcessGroup | None, cap_bytes: int) -> None:
+    def __init__(self, group: dist.ProcessGroup | None, cap_bytes: int,
+                 eager_launch: bool | None = None) -> None:
         self.group = group
         self._cap = cap_bytes
         self._slots: dict[Any, tuple[int, int]] = {}
@@ -259,8 +274,31 @@ class PackedFactorBuffer:
         self._chunks: list[tuple[int, int, list[Any]]] = []
         self._chunk_of: dict[Any, int] = {}
         self._dirty: list[Any] = []
+        self._marked: dict[int, set] = {}
         self._works: dict[Any, Any] = {}
+        if eager_launch is None:
+            import os
+
+            eager_launch = os.environ.get('KFAC_PACKED_EAGER_LAUNCH', '1') != '0'
+        self.eager_launch = eager_launch
         self.launches = 0
+        self.allocations = 0
+        # (chunk index, 'hook' | 'step') of the latest chunk all-reduces
+        self.launch_log: collections.deque = collections.deque(maxlen=4096)
+
+    def reserve(self, layout: list[tuple[Any, int]], dtype: torch.dtype,
+                device: torch.device) -> None:
+        """Assign every slot of ``layout`` (``(key, numel)`` in hook order)
+        and allocate the buffer once.  A no-op once the buffer exists."""
+        if self.flat is not None or not layout:
+            return
+        for key, n in layout:
+            if key not in self._slots:
+                self._slots[key] = (self._size, int(n))
+                self._size += int(n)
+        self.flat = torch.zeros(self._size, dtype=dtype, device=device)
+        self.allocations += 1
+        self._rechunk()
 
     def _rechunk(self) -> None:
         self._chunks = []
@@ -299,33 +337,53 @@ class PackedFactorBuffer:
             self._slots[key] = (self._size, numel)
             self._size += numel
             self.flat = torch.zeros(self._size, dtype=like.dtype, device=like.device)
+            self.allocations += 1
             if old is not None:
                 self.flat[: old.numel()].copy_(old)
             self._rechunk()
+            self._marked = {}
+            for k in self._dirty:
+                self._marked.setdefault(self._chunk_of[k], set()).add(k)
         off, n = self._slots[key]
         assert self.flat is not None
         return self.flat[off: off + n]
 
     def mark(self, key: Any) -> None:
-        """The slot holds a new pre-scaled local value to be summed."""
-        if key not in self._dirty:
-            self._dirty.append(key)
+        """The slot holds a new pre-scaled local value to be summed.  With
+        ``eager_launch``, all-reduce its chunk now if this completes it
+        (collective: every rank marks the same keys in the same order)."""
+        if key in self._dirty:
+            return
+        self._dirty.append(key)
+        i = self._chunk_of[key]
+        marked = self._marked.setdefault(i, set())
+        marked.add(key)
+        if self.eager_launch and len(marked) == len(self._chunks[i][2]):
+            self._launch_chunk(i, 'hook')
+            done = set(self._chunks[i][2])
+            self._dirty = [k for k in self._dirty if k not in done]
 
     def pending(self, key: Any) -> bool:
         return key in self._dirty
 
+    def _launch_chunk(self, i: int, where: str) -> None:
+        assert self.flat is not None
+        start, end, keys = self._chunks[i]
+        work = dist.all_reduce(self.flat[start:end], group=self.group, async_op=True)
+        for k in keys:
+            self._works[k] = work
+        self._marked.pop(i, None)
+        self.launch_log.append((i, where))
+
     def launch(self) -> None:
-        """All-reduce every chunk holding a marked slot (collective)."""
+        """All-reduce every chunk still holding a marked slot (collective)."""
         if not self._dirty:
             return
         assert self.flat is not None
         todo = sorted({self._chunk_of[k] for k in self._dirty})
         self._dirty = []
         for i in todo:
-            start, end, keys = self._chunks[i]
-            work = dist.all_reduce(self.flat[start:end], group=self.group, async_op=True)
-            for k in keys:
-                self._works[k] = work
+            self._launch_chunk(i, 'step')
         self.launches += 1
 
     def wait(self, key: Any) -> None:

@@ -96,3 +96,34 @@ def test_gemm_conv1x1_slab_weight_grad_matches_conv(shape) -> None:
     m = n * h * w
     s = _splitk(m)
     assert m % s == 0 and (s == 1 or m // s >= 2048)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('shape', [(32, 64, 56, 56, 256), (32, 1024, 14, 14, 256)])
+def test_gemm_conv1x1_bf16_weight_grad(cuda, shape) -> None:
+    """Under bf16 autocast the slab partials of ``GemmConv1x1``'s weight
+    gradient are fp32 (one rounding to bf16 at the end): the result matches
+    the float64 weight gradient of the same bf16 operands to bf16 precision,
+    and is at least as close as MIOpen's bf16 convolution."""
+    n, c, h, w, co = shape
+    torch.manual_seed(0)
+    conv = nn.Conv2d(c, co, 1, bias=False).to(cuda)
+    gem = nn.Conv2d(c, co, 1, bias=False).to(cuda)
+    gem.load_state_dict(conv.state_dict())
+    gem.__class__ = GemmConv1x1
+    x = torch.randn(n, c, h, w, device=cuda).contiguous(memory_format=torch.channels_last)
+    g = torch.randn(n, co, h, w, device=cuda).contiguous(memory_format=torch.channels_last)
+    grads = []
+    for m in (gem, conv):
+        m.weight.grad = None
+        with torch.autocast('cuda', dtype=torch.bfloat16):
+            y = m(x)
+        y.backward(g.to(y.dtype))
+        grads.append(m.weight.grad.double().view(co, c))
+    xb = x.to(torch.bfloat16).double().permute(0, 2, 3, 1).reshape(-1, c)
+    gb = g.to(torch.bfloat16).double().permute(0, 2, 3, 1).reshape(-1, co)
+    ref = gb.t() @ xb
+    err_gemm = float((grads[0] - ref).norm() / ref.norm())
+    err_miopen = float((grads[1] - ref).norm() / ref.norm())
+    assert err_gemm < 4e-3, (err_gemm, err_miopen)
+    assert err_gemm <= 1.5 * err_miopen + 1e-4, (err_gemm, err_miopen)

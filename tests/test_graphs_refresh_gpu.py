@@ -149,6 +149,10 @@ def test_graph_replay_interleaved_with_eager_twin(cuda, amp, use_kfac, kinds, co
                               f'gradient {dg:.2e} at {dn}): MIOpen solver nondeterminism')
         run = A[4]
         assert isinstance(run, GraphedTrainStep)
+        print(f'verify report: {run.verify_report}', flush=True)
+        # the capture-time self-check ran and passed for every captured kind
+        assert set(run.verify_report) == set(kinds), run.verify_report
+        assert all(r['ok'] for r in run.verify_report.values()), run.verify_report
         assert run.captures == (len(kinds) if use_kfac else 1), run.captures
         assert run.replays >= (6 if use_kfac else steps - 2), run.replays
         if use_kfac:

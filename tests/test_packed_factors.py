@@ -116,3 +116,66 @@ def _reload_after_packed() -> None:
 
 def test_load_state_dict_after_packed():
     run_distributed(_reload_after_packed, 2)
+
+
+def _launch_timing(eager: str, bucket_mb: float) -> tuple:
+    """Train a few steps; per factor step, the chunk launches issued before
+    ``step()`` (from the hooks) and the buffer's allocation count."""
+    os.environ['KFAC_PACKED_FACTORS'] = '1'
+    os.environ['KFAC_PACKED_EAGER_LAUNCH'] = eager
+    rank = dist.get_rank()
+    torch.manual_seed(0)
+    model = torch.nn.parallel.DistributedDataParallel(_Net())
+    opt = torch.optim.SGD(model.parameters(), lr=0.05)
+    pre = kfac.KFACPreconditioner(
+        model, factor_update_steps=2, inv_update_steps=4, allreduce_bucket_cap_mb=bucket_mb,
+        grad_worker_fraction=0.5,
+    )
+    g = torch.Generator().manual_seed(rank)
+    before_step, grads = [], []
+    for i in range(9):
+        x = torch.randn(8, 3, 8, 8, generator=g)
+        y = torch.randint(0, 10, (8,), generator=g)
+        opt.zero_grad()
+        torch.nn.functional.cross_entropy(model(x), y).backward()
+        bufs = list(pre._tdc._packed.values())
+        if i % 2 == 0:
+            assert len(bufs) == 1
+            before_step.append(list(bufs[0].launch_log))
+        pre.step()
+        for b in bufs:
+            b.launch_log.clear()
+        grads.append([p.grad.clone() for p in model.parameters()])
+        opt.step()
+    buf = next(iter(pre._tdc._packed.values()))
+    factors = {n: (l.a_factor.clone(), l.g_factor.clone()) for n, l in pre._layers.values()}
+    return before_step, buf.allocations, len(buf._chunks), grads, factors
+
+
+def _check_hook_launch(bucket_mb: float) -> None:
+    hook = _launch_timing('1', bucket_mb)
+    late = _launch_timing('0', bucket_mb)
+    logs, allocs, chunks = hook[0], hook[1], hook[2]
+    # one allocation of the whole buffer, at its final size
+    assert allocs == 1 and late[1] == 1, (allocs, late[1])
+    # every factor step launched every chunk from the hooks, before step()
+    for log in logs:
+        assert sorted(i for i, _ in log) == list(range(chunks)), (log, chunks)
+        assert all(w == 'hook' for _, w in log), log
+    # nothing launched before step() without eager launch
+    assert all(not log for log in late[0]), late[0]
+    # the same chunk order on every rank
+    every: list = [None] * dist.get_world_size()
+    dist.all_gather_object(every, logs)
+    assert all(e == every[0] for e in every), every
+    # bit-identical to the launch-at-step() path
+    for ga, gb in zip(hook[3], late[3]):
+        for a, b in zip(ga, gb):
+            assert torch.equal(a, b)
+    for name, (a, gg) in hook[4].items():
+        assert torch.equal(a, late[4][name][0]) and torch.equal(gg, late[4][name][1])
+
+
+@pytest.mark.parametrize('bucket_mb', [25.0, 0.01])
+def test_chunks_launch_from_hooks(bucket_mb):
+    run_distributed(_check_hook_launch, 4, bucket_mb)
