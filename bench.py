@@ -516,6 +516,17 @@ def main() -> None:
             'graphs': bool((sec.get('step_graphs') or {}).get('replays')),
             'step_graphs': sec.get('step_graphs'),
         }
+    if not args.no_kfac and args.impl == 'native':
+        from distributed_kfac_pytorch_amd.ops import factors as fops
+        from distributed_kfac_pytorch_amd.ops import precondition as pops
+        # precision of the K-FAC math on fp32 operands: bf16x3 = three-term
+        # bf16 split on MFMA (~1e-5 relative; csrc/syrk.hip, csrc/gemm3s.hip),
+        # fp32 = exact fp32 products
+        line['kfac_math'] = {
+            'factor_syrk': 'fp32' if fops.fp32_exact() else 'bf16x3',
+            'precondition': 'bf16x3' if pops.grouped_gemm_enabled() else 'fp32',
+            'eigensolver': 'fp32',
+        }
     line['host_issue_ms'] = res['host_issue_ms']
     if base is not None:
         line['sgd_host_issue_ms'] = base['host_issue_ms']

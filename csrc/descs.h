@@ -94,7 +94,9 @@ struct SytrdDesc {
   float* tau;    // [n-1]
   float* part1;  // [SY_MAXCH][SY_P1] col-step partials
   float* part2;  // [SY_MAXROWBLK] symv partial w.v
-  float* sc;     // [2]: tau, v scale of the last reflector
+  float* sc;     // [4 + 2 NB]: tau, v scale, t1.t2 of the last reflector,
+                 // then t1 = W^T v and t2 = V^T v (tile symv)
+  float* P;      // [ceil(n / 64)][n] tile symv row partials (tile symv only)
   int32_t n, pad;
 };
 

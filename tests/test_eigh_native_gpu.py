@@ -91,3 +91,42 @@ def test_cold_process_chain_1000_2049() -> None:
                        capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
     assert 'ok' in p.stdout and 'sytrd+dc' in p.stdout, p.stdout
+
+
+_MODES = r'''
+import sys, torch
+sys.path.insert(0, {root!r})
+from tests.test_eigh_native_gpu import _factor, _check
+from distributed_kfac_pytorch_amd.ops import linalg
+sizes = [147, 577, 1000, 1152, 2049, 2304, 4608, 4608]
+mats64 = [_factor(n, 50 + i) for i, n in enumerate(sizes)]
+for rnd in range(2):
+    res = linalg.eigh_many([m.float().cuda() for m in mats64])
+    torch.cuda.synchronize()
+    for a64, (d, q) in zip(mats64, res):
+        _check(a64, d, q)
+print('ok', sorted({{t[0] for t in linalg.last_stats['tiers']}}))
+'''
+
+
+@pytest.mark.parametrize('env', [
+    {'KFAC_SYTRD_TILE': '1'},                                   # lower-triangle tile symv
+    {'KFAC_SYTRD_PERSIST': '1'},                                # one launch per panel
+    {'KFAC_SYTRD_PERSIST': '1', 'KFAC_SYTRD_BARRIER': 'flat'},
+    {'KFAC_SYTRD_TILE': '1', 'KFAC_SYTRD_PERSIST': '1'},
+    {'KFAC_SYTRD_TILE': '1', 'KFAC_SYTRD_PERSIST': '1500'},     # persistent tail only
+])
+def test_chain_variants_match_float64(env) -> None:
+    """Every Householder-chain variant (csrc/sytrd.hip: tile symv, persistent
+    panels with either barrier, hybrid) on a mix of chain sizes, twice in a
+    fresh process (the variants are chosen once per process)."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, '-c', _MODES.format(root=root)], cwd=root,
+                       capture_output=True, text=True, timeout=240,
+                       env={**os.environ, **env})
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
+    assert 'ok' in p.stdout and 'sytrd+dc' in p.stdout, p.stdout

@@ -118,7 +118,14 @@ def test_graph_replay_interleaved_with_eager_twin(cuda, amp, use_kfac, kinds, co
         first_bad = None
         pre_ids = set() if A[1] is None else {
             id(p) for _, layer in A[1]._layers.values() for p in layer.module.module.parameters()}
+        b_gemm = conv_mode == 'gemm'
         for i in range(steps):
+            if not b_gemm and A[4].conv_mode == 'gemm':
+                # the runner saw bf16 autocast in its warmup step and moved
+                # every 1x1 convolution to the GEMM form: so does the twin,
+                # at the same step
+                use_gemm_conv1x1(B[0])
+                b_gemm = True
             x, y = pool[i % len(pool)]
             for m in (A, B):
                 m[2].copy_(x)
@@ -149,6 +156,8 @@ def test_graph_replay_interleaved_with_eager_twin(cuda, amp, use_kfac, kinds, co
                               f'gradient {dg:.2e} at {dn}): MIOpen solver nondeterminism')
         run = A[4]
         assert isinstance(run, GraphedTrainStep)
+        # bf16 autocast is detected during the warmup step: 1x1 convs as GEMMs
+        assert (run.conv_mode == 'gemm') == (amp or conv_mode == 'gemm'), run.conv_mode
         print(f'verify report: {run.verify_report}', flush=True)
         # the capture-time self-check ran and passed for every captured kind
         assert set(run.verify_report) == set(kinds), run.verify_report

@@ -12,6 +12,9 @@
 //      L2 writeback on release, invalidate on acquire)
 //   1  relaxed agent-scope atomics + explicit vmcnt wait; the shared data go
 //      through sc1 (L2-bypassing) loads/stores, so no L2 maintenance
+//   2  as 1, two-level: blocks arrive on one of 16 group counters, the last
+//      arrival of a group on the top counter (fewer serialised atomics on
+//      one address); everyone polls the top counter
 // Every spin is bounded: after ~2^24 polls a workgroup sets an error flag and
 // returns, so a grid that is not co-resident cannot hang the GPU; the host
 // also refuses grids larger than the occupancy calculator's resident count.
@@ -34,12 +37,30 @@ __device__ __forceinline__ float ld_coherent(const float* p) {
   return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+constexpr int NGRP = 16;
+
 template <int MODE>
 __device__ __forceinline__ bool grid_barrier(unsigned* ctr, unsigned target, int* err) {
   __syncthreads();
   bool ok = true;
   if (threadIdx.x == 0) {
-    if (MODE == 0) {
+    if (MODE == 2) {
+      // ctr[0] top, ctr[1 + g] group counters; target = epoch * G
+      const unsigned G = gridDim.x, epoch = target / G;
+      const unsigned g = blockIdx.x % NGRP;
+      const unsigned gsize = G / NGRP + (g < G % NGRP ? 1u : 0u);
+      const unsigned ngrp = G < NGRP ? G : NGRP;
+      __builtin_amdgcn_s_waitcnt(0);
+      const unsigned old =
+          __hip_atomic_fetch_add(ctr + 1 + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (old + 1 == epoch * gsize)
+        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      unsigned polls = 0;
+      while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < epoch * ngrp) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++polls > SPIN_LIMIT) { ok = false; break; }
+      }
+    } else if (MODE == 0) {
       __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
       unsigned polls = 0;
       while (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
@@ -78,7 +99,7 @@ __global__ void __launch_bounds__(T) bar_kernel(float* vec, unsigned* ctr, int* 
     const float v = ld_coherent(&vec[(size_t)other * T + threadIdx.x]);
     wrong += v != (float)(it * 7 + other);
     // second barrier: nobody overwrites vec before everyone has read it
-    if (!grid_barrier<MODE>(ctr + 1, (unsigned)(it + 1) * (unsigned)G, err)) return;
+    if (!grid_barrier<MODE>(ctr + 32, (unsigned)(it + 1) * (unsigned)G, err)) return;
   }
   if (wrong) atomicAdd(bad, wrong);
 }
@@ -96,7 +117,7 @@ int main(int argc, char** argv) {
   unsigned* ctr;
   int *err, *bad;
   CK(hipMalloc(&vec, sizeof(float) * 2048 * T));
-  CK(hipMalloc(&ctr, sizeof(unsigned) * 2));
+  CK(hipMalloc(&ctr, sizeof(unsigned) * 64));
   CK(hipMalloc(&err, sizeof(int)));
   CK(hipMalloc(&bad, sizeof(int)));
   hipEvent_t a, b;
@@ -104,17 +125,19 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&b));
   printf("{\"cus\": %d, \"resident_blocks\": %d, \"iters\": %d}\n", cus, resident, iters);
   const int grids[] = {1, 8, 32, 64, 128, 256, 512, 1024};
-  for (int mode = 0; mode < 2; ++mode) {
+  for (int mode = 0; mode < 3; ++mode) {
     for (int G : grids) {
       if (G > resident || G > 2048) continue;
-      CK(hipMemset(ctr, 0, sizeof(unsigned) * 2));
+      CK(hipMemset(ctr, 0, sizeof(unsigned) * 64));
       CK(hipMemset(err, 0, sizeof(int)));
       CK(hipMemset(bad, 0, sizeof(int)));
       CK(hipEventRecord(a, 0));
       if (mode == 0)
         hipLaunchKernelGGL(bar_kernel<0>, dim3(G), dim3(T), 0, 0, vec, ctr, err, iters, bad);
-      else
+      else if (mode == 1)
         hipLaunchKernelGGL(bar_kernel<1>, dim3(G), dim3(T), 0, 0, vec, ctr, err, iters, bad);
+      else
+        hipLaunchKernelGGL(bar_kernel<2>, dim3(G), dim3(T), 0, 0, vec, ctr, err, iters, bad);
       CK(hipGetLastError());
       CK(hipEventRecord(b, 0));
       CK(hipEventSynchronize(b));
