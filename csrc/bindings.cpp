@@ -112,6 +112,16 @@ std::vector<at::Tensor> sytrd_begin(std::vector<at::Tensor> stacks);
 void sytrd_advance(at::Tensor descs, std::vector<int64_t> sizes, int64_t k0, int64_t k1,
                    int64_t waves);
 
+namespace kfac {
+// gemm_f32.hip
+void gemm_f32_batched(int ta, int tb, int M, int N, int K, float alpha, const float* A,
+                      int64_t lda, int64_t sA, const float* B, int64_t ldb, int64_t sB,
+                      float beta, float* C, int64_t ldc, int64_t sC, int batch,
+                      hipStream_t s);
+void trinv_upper_batched(float* T, int64_t ld, int64_t sT, int n, int batch, float* work,
+                         hipStream_t s);
+}  // namespace kfac
+
 namespace {
 
 hipStream_t cur_stream() {
@@ -1138,6 +1148,53 @@ std::vector<int64_t> tridiag_dc_plan(int64_t n);
 std::vector<at::Tensor> eigh_twostage(const at::Tensor& A, bool timed);
 int64_t eigh_twostage_max_n();
 
+// ---- native batched fp32 GEMM (csrc/gemm_f32.hip) ----------------------
+// 3-D fp32 CUDA views [batch, rows, cols] with unit column stride (any row /
+// batch stride; a 2-D tensor is a batch of one).  C = alpha op(A) op(B) +
+// beta C, op = transpose when ta / tb.
+namespace {
+struct Mat3 {
+  int64_t b, r, c, ld, sb;
+  float* p;
+};
+Mat3 mat3(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat, name, ": fp32 CUDA tensor");
+  TORCH_CHECK(t.dim() == 2 || t.dim() == 3, name, ": 2-D or 3-D");
+  const bool three = t.dim() == 3;
+  Mat3 m{three ? t.size(0) : 1, t.size(three ? 1 : 0), t.size(three ? 2 : 1),
+         t.stride(three ? 1 : 0), three ? t.stride(0) : 0, t.data_ptr<float>()};
+  TORCH_CHECK(t.stride(three ? 2 : 1) == 1 || m.c == 1, name, ": unit column stride");
+  if (m.r == 1) m.ld = std::max<int64_t>(m.ld, m.c);
+  return m;
+}
+}  // namespace
+
+void gemm_f32(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, bool ta, bool tb,
+              double alpha, double beta) {
+  const Mat3 A = mat3(a, "a"), B = mat3(b, "b"), C = mat3(c, "c");
+  const int64_t M = ta ? A.c : A.r, K = ta ? A.r : A.c;
+  const int64_t Kb = tb ? B.c : B.r, N = tb ? B.r : B.c;
+  TORCH_CHECK(K == Kb && C.r == M && C.c == N, "gemm_f32: shape mismatch");
+  const int64_t batch = C.b;
+  TORCH_CHECK((A.b == batch || A.b == 1) && (B.b == batch || B.b == 1),
+              "gemm_f32: batch mismatch");
+  TORCH_CHECK(M < (1LL << 31) && N < (1LL << 31) && K < (1LL << 31) && batch < 65536);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(c.device());
+  kfac::gemm_f32_batched(ta, tb, (int)M, (int)N, (int)K, (float)alpha, A.p, A.ld,
+                         A.b == 1 ? 0 : A.sb, B.p, B.ld, B.b == 1 ? 0 : B.sb, (float)beta, C.p,
+                         C.ld, C.sb, (int)batch, cur_stream());
+}
+
+// T <- T^-1 in place for a batch of upper-triangular [batch, n, n] fp32
+void trinv_upper_(at::Tensor& t) {
+  const Mat3 T = mat3(t, "t");
+  TORCH_CHECK(T.r == T.c, "trinv_upper_: square matrices");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(t.device());
+  auto work = at::empty({std::max<int64_t>(T.b * T.r * T.r / 2 + T.r, 1)}, t.options());
+  kfac::trinv_upper_batched(T.p, T.ld, T.sb == 0 ? T.r * T.ld : T.sb, (int)T.r, (int)T.b,
+                            work.data_ptr<float>(), cur_stream());
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "MI355X (gfx950) HIP kernels for distributed K-FAC";
   m.def("triu_pack", &triu_pack);
@@ -1157,6 +1214,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("kl_finalize", &kl_finalize);
   m.def("apply_grad", &apply_grad);
   m.def("fill_identity", &fill_identity);
+  m.def("gemm_f32", &gemm_f32, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("ta"),
+        py::arg("tb"), py::arg("alpha") = 1.0, py::arg("beta") = 0.0);
+  m.def("trinv_upper_", &trinv_upper_);
   m.def("jacobi_eigh", &jacobi_eigh);
   m.def("jacobi_max_n", &kfac::jacobi_max_n);
   m.def("build_layer_table", &build_layer_table, py::arg("ps"), py::arg("ws"),

@@ -1,0 +1,239 @@
+// Batched fp32 GEMM on the matrix cores, for the GEMM-shaped stages of the
+// eigensolver refresh (reference kfac/layers/eigen.py:294-347 runs all of it
+// inside torch.linalg.eigh): the blocked back-transform X -= V (T (V^T X))
+// (ops/linalg.py apply_q_blocked, csrc/twostage_host.cpp stage-1 BT), the
+// divide-and-conquer merges Q_parent = diag(Q1, Q2) W (csrc/tridiag_host.cpp)
+// and the triangular inverse of the compact-WY T (gemm_f32_trinv_upper).
+//
+//   C[b] = alpha * op(A[b]) * op(B[b]) + beta * C[b]        (row-major)
+//   op(A) is M x K (A stored [M][lda] or, transposed, [K][lda]),
+//   op(B) is K x N (B stored [K][ldb] or, transposed, [N][ldb]).
+//
+// v_mfma_f32_32x32x2_f32: exact fp32 products with fp32 accumulation (the
+// accuracy class of a library sgemm; gfx950 has no TF32), so the refresh
+// keeps the float64-parity tests' tolerances.  fp32 MFMA issues at 1/16 of
+// the bf16 rate, so the kernel is matrix-core bound: a 128 x 128 block tile
+// (4 waves in 2 x 2, each 64 x 64 = 2 x 2 MFMA 32 x 32 accumulators), k
+// tiles of 16 staged k-major in LDS ([k][m] / [k][n], 132-float rows, double
+// buffered: the next tile's global loads are in flight during the MFMAs),
+// scalar clamped global loads (any shape, any leading dimension, no
+// alignment requirement).  Grid (n tiles, m tiles, batch); tiles walk n
+// fastest so consecutive blocks share their A row panel in L2.
+#include "common.h"
+
+namespace kfac {
+
+namespace {
+
+constexpr int GT = 128;       // block tile edge
+constexpr int GK = 16;        // k per LDS tile
+constexpr int GLD = GT + 4;   // LDS row (floats)
+constexpr int GTHR = 256;
+
+typedef float v16f __attribute__((ext_vector_type(16)));
+
+struct GemmArgs {
+  const float* A;
+  const float* B;
+  float* C;
+  int64_t lda, ldb, ldc, sA, sB, sC;
+  int M, N, K;
+  float alpha, beta;
+  int ta, tb;
+};
+
+// one k tile of op(X) (rows r0.., k0..k0+15) into LDS as [k][row]; 8 scalar
+// loads per thread, issued together into registers first
+__device__ __forceinline__ void fetch(const float* __restrict__ X, int64_t ld, int trans,
+                                      int rows, int K, int r0, int k0, float (&v)[8]) {
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int e = threadIdx.x + GTHR * u;  // 0 .. 2047
+    int r, k;
+    if (trans) {  // stored [K][ld]: consecutive threads walk the row index
+      r = e & (GT - 1);
+      k = e >> 7;
+    } else {      // stored [rows][ld]: consecutive threads walk k
+      r = e >> 4;
+      k = e & (GK - 1);
+    }
+    const int gr = r0 + r, gk = k0 + k;
+    const bool ok = gr < rows && gk < K;
+    const int64_t off = trans ? (int64_t)(ok ? gk : 0) * ld + (ok ? gr : 0)
+                              : (int64_t)(ok ? gr : 0) * ld + (ok ? gk : 0);
+    const float x = X[off];
+    v[u] = ok ? x : 0.f;
+  }
+}
+
+__device__ __forceinline__ void stash(float* S, int trans, const float (&v)[8]) {
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int e = threadIdx.x + GTHR * u;
+    int r, k;
+    if (trans) {
+      r = e & (GT - 1);
+      k = e >> 7;
+    } else {
+      r = e >> 4;
+      k = e & (GK - 1);
+    }
+    S[k * GLD + r] = v[u];
+  }
+}
+
+__global__ void __launch_bounds__(GTHR) gemm_f32_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) float As[2][GK * GLD];
+  __shared__ __attribute__((aligned(16))) float Bs[2][GK * GLD];
+  const int n0 = blockIdx.x * GT, m0 = blockIdx.y * GT;
+  const int64_t b = blockIdx.z;
+  const float* A = g.A + b * g.sA;
+  const float* B = g.B + b * g.sB;
+  float* C = g.C + b * g.sC;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int wm = (w >> 1) * 64, wn = (w & 1) * 64;
+  const int r = l & 31, h = l >> 5;
+  v16f acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  const int nk = (g.K + GK - 1) / GK;
+  float va[8], vb[8];
+  fetch(A, g.lda, g.ta, g.M, g.K, m0, 0, va);
+  fetch(B, g.ldb, !g.tb, g.N, g.K, n0, 0, vb);  // B[k][n] = row-major [K][N] is "transposed" rows=n
+  stash(As[0], g.ta, va);
+  stash(Bs[0], !g.tb, vb);
+  __syncthreads();
+  for (int t = 0; t < nk; ++t) {
+    const int cur = t & 1;
+    const bool more = t + 1 < nk;
+    if (more) {
+      fetch(A, g.lda, g.ta, g.M, g.K, m0, (t + 1) * GK, va);
+      fetch(B, g.ldb, !g.tb, g.N, g.K, n0, (t + 1) * GK, vb);
+    }
+    const float* as = As[cur];
+    const float* bs = Bs[cur];
+#pragma unroll
+    for (int kk = 0; kk < GK; kk += 2) {
+      const float a0 = as[(kk + h) * GLD + wm + r];
+      const float a1 = as[(kk + h) * GLD + wm + 32 + r];
+      const float b0 = bs[(kk + h) * GLD + wn + r];
+      const float b1 = bs[(kk + h) * GLD + wn + 32 + r];
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+    }
+    if (more) {
+      stash(As[cur ^ 1], g.ta, va);
+      stash(Bs[cur ^ 1], !g.tb, vb);
+    }
+    __syncthreads();
+  }
+  // C/D layout of v_mfma_f32_32x32x2f32: col = lane & 31,
+  // row = (e & 3) + 8 (e >> 2) + 4 (lane >> 5)
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = m0 + wm + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
+        const int col = n0 + wn + 32 * j + r;
+        if (row < g.M && col < g.N) {
+          float* p = C + (int64_t)row * g.ldc + col;
+          const float v = g.alpha * acc[i][j][e];
+          *p = g.beta == 0.f ? v : v + g.beta * *p;
+        }
+      }
+}
+
+}  // namespace
+
+void gemm_f32_batched(int ta, int tb, int M, int N, int K, float alpha, const float* A,
+                      int64_t lda, int64_t sA, const float* B, int64_t ldb, int64_t sB,
+                      float beta, float* C, int64_t ldc, int64_t sC, int batch,
+                      hipStream_t s) {
+  if (M <= 0 || N <= 0 || batch <= 0) return;
+  GemmArgs g{A, B, C, lda, ldb, ldc, sA, sB, sC, M, N, K, alpha, beta, ta, tb};
+  const dim3 grid((unsigned)ceil_div(N, GT), (unsigned)ceil_div(M, GT), (unsigned)batch);
+  hipLaunchKernelGGL(gemm_f32_kernel, grid, dim3(GTHR), 0, s, g);
+}
+
+}  // namespace kfac
+
+namespace kfac {
+
+namespace {
+
+// in-place inverse of the 64 x 64 upper-triangular diagonal blocks of a
+// batch of upper-triangular matrices T ([batch][n][ld]): block (d, b) at
+// rows / cols 64 d.  One 64-thread group per block column j: back
+// substitution T[i][j] = -(sum_{i < k <= j} U[i][k] T[k][j]) / U[i][i]
+// over i = j-1 .. 0, with U staged in LDS.  Entries past n are identity.
+constexpr int TB = 64;
+
+__global__ void __launch_bounds__(TB) trinv64_kernel(float* T, int64_t ld, int64_t sT, int n) {
+  __shared__ float U[TB][TB + 1];
+  const int d = blockIdx.x, j = threadIdx.x;
+  float* base = T + (int64_t)blockIdx.y * sT + (int64_t)d * TB * ld + (int64_t)d * TB;
+  const int lim = n - d * TB;  // valid rows / cols of this block
+  for (int i = 0; i < TB; ++i) {
+    float v = (i == j) ? 1.f : 0.f;
+    if (i < lim && j < lim) v = base[(int64_t)i * ld + j];
+    U[i][j] = v;
+  }
+  __syncthreads();
+  float col[TB];
+#pragma unroll
+  for (int i = 0; i < TB; ++i) col[i] = 0.f;
+  // thread j: column j of U^-1
+#pragma unroll
+  for (int i = TB - 1; i >= 0; --i) {
+    float s = (i == j) ? 1.f : 0.f;
+#pragma unroll
+    for (int k = i + 1; k < TB; ++k) s -= U[i][k] * col[k];
+    col[i] = i <= j ? s / U[i][i] : 0.f;
+  }
+  for (int i = 0; i < TB; ++i)
+    if (i < lim && j < lim) base[(int64_t)i * ld + j] = col[i];
+}
+
+}  // namespace
+
+void gemm_f32_batched(int ta, int tb, int M, int N, int K, float alpha, const float* A,
+                      int64_t lda, int64_t sA, const float* B, int64_t ldb, int64_t sB,
+                      float beta, float* C, int64_t ldc, int64_t sC, int batch,
+                      hipStream_t s);
+
+// T <- T^-1 for a batch of n x n upper-triangular matrices (row-major, row
+// stride ld, batch stride sT), in place; `work` holds >= batch * n * n / 2
+// floats.  64 x 64 diagonal blocks by back substitution, then pairs of
+// blocks merged bottom-up: [[T11, X], [0, T22]] with X = -T11 U12 T22
+// (two batched GEMMs per merge position).
+void trinv_upper_batched(float* T, int64_t ld, int64_t sT, int n, int batch, float* work,
+                         hipStream_t s) {
+  if (n <= 0 || batch <= 0) return;
+  const int nd = (int)ceil_div(n, TB);
+  hipLaunchKernelGGL(trinv64_kernel, dim3((unsigned)nd, (unsigned)batch), dim3(TB), 0, s, T, ld,
+                     sT, n);
+  for (int h = TB; h < n; h *= 2) {
+    for (int p = 0; p + h < n; p += 2 * h) {
+      const int h2 = (p + 2 * h <= n) ? h : n - p - h;  // second block may be short
+      float* t11 = T + (int64_t)p * ld + p;
+      float* u12 = T + (int64_t)p * ld + p + h;
+      float* t22 = T + (int64_t)(p + h) * ld + p + h;
+      // Y = U12 T22 (h x h2), then U12 <- -T11 Y
+      gemm_f32_batched(0, 0, h, h2, h2, 1.f, u12, ld, sT, t22, ld, sT, 0.f, work, h2,
+                       (int64_t)h * h2, batch, s);
+      gemm_f32_batched(0, 0, h, h2, h, -1.f, t11, ld, sT, work, h2, (int64_t)h * h2, 0.f, u12,
+                       ld, sT, batch, s);
+    }
+  }
+}
+
+}  // namespace kfac

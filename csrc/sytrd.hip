@@ -722,8 +722,10 @@ __device__ __forceinline__ bool grid_barrier(unsigned* ctl, int parity, unsigned
         break;
       }
     }
-    if (!ok && blockIdx.x == 0) {
-      // poison this member's result: the caller's finiteness check re-solves
+    if (!ok) {
+      // poison this member's result (every block that leaves does, so every
+      // member of the chain is covered): the caller's finiteness check
+      // re-solves it
       const float nan = __builtin_nanf("");
       __hip_atomic_store((float*)descs[blockIdx.y].d, nan, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
@@ -743,7 +745,14 @@ __global__ void __launch_bounds__(SY_T) sytrd_panel_kernel(
   const int bx = blockIdx.x;
   unsigned* err = ctl + 2;
   const int parity = (p / SY_NB) & 1;
-  if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
+  if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+    // an earlier panel of this chain failed: keep every member poisoned
+    // (a later col step of the two-launch form may have rewritten d[0])
+    if (threadIdx.x == 0)
+      __hip_atomic_store((float*)descs[blockIdx.y].d, __builtin_nanf(""), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
   if (bx == 0 && blockIdx.y == 0 && threadIdx.x <= SY_BAR_GRP) {
     // the next panel launch's counters (nobody uses them during this launch)
     unsigned* w = threadIdx.x == 0 ? ctl + (parity ^ 1)

@@ -32,6 +32,10 @@ void dc_merge_back(int h, int G, const double* sd, const int* perm, const int* i
 void jacobi_eigh_batched(const float* A, int64_t n, int64_t batch, int64_t strideA,
                          float* evals, float* evecs, int64_t strideV, int max_sweeps, float tol,
                          hipStream_t s);
+void gemm_f32_batched(int ta, int tb, int M, int N, int K, float alpha, const float* A,
+                      int64_t lda, int64_t sA, const float* B, int64_t ldb, int64_t sB,
+                      float beta, float* C, int64_t ldc, int64_t sC, int batch,
+                      hipStream_t s);
 }  // namespace kfac
 
 namespace {
@@ -132,7 +136,11 @@ std::vector<at::Tensor> tridiag_eigh_dc(const at::Tensor& d_in, const at::Tensor
                         rot_cs.data_ptr<double>(), W.data_ptr<float>(), s);
     // Q_parent = diag(Q1, Q2) W: the two row halves of every subproblem are
     // the children's blocks times W's row halves
-    Q = at::bmm(Q.view({2 * G, h, h}), W.view({2 * G, h, m})).view({G, m, m});
+    auto Qn = at::empty({G, m, m}, fopt);
+    kfac::gemm_f32_batched(0, 0, (int)h, (int)m, (int)h, 1.f, Q.data_ptr<float>(), h, h * h,
+                           W.data_ptr<float>(), m, h * m, 0.f, Qn.data_ptr<float>(), m, h * m,
+                           (int)(2 * G), s);
+    Q = Qn;
     D = svals;
   }
   auto w = D.view({b, np}).narrow(1, 0, n).to(at::kFloat).contiguous();

@@ -4,7 +4,8 @@
 //   band -> tridiagonal (csrc/sb2st.hip bulge chasing, one workgroup per matrix)
 //   tridiagonal eigenpairs (csrc/tridiag.hip divide and conquer)
 //   X = Q2 Z (csrc/bt2.hip, one launch per step of disjoint rank-16 blocks)
-//   X = Q1 X (blocked UT back-transform, 512 reflectors per batched GEMM)
+//   X = Q1 X (blocked UT back-transform, 512 reflectors per block: native
+//   fp32 MFMA GEMMs and triangular inverse, csrc/gemm_f32.hip)
 //
 // for a batch of same-size fp32 symmetric matrices, all on the current
 // stream, no host synchronisation.  Reference: torch.linalg.eigh in
@@ -15,7 +16,6 @@
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 
 #include <hip/hip_runtime.h>
-#include <rocblas/rocblas.h>
 
 #include <algorithm>
 #include <cstdlib>
@@ -42,16 +42,15 @@ void bt2_prep(const float* V2, const float* tau2, int64_t sV2, int n, int kmax, 
               float* T, hipStream_t stream);
 void bt2_apply(const float* V2, int64_t sV2, const float* T, int n, int kmax, int batch,
                float* X, int64_t sX, int ldx, hipStream_t stream);
+void gemm_f32_batched(int ta, int tb, int M, int N, int K, float alpha, const float* A,
+                      int64_t lda, int64_t sA, const float* B, int64_t ldb, int64_t sB,
+                      float beta, float* C, int64_t ldc, int64_t sC, int batch,
+                      hipStream_t s);
+void trinv_upper_batched(float* T, int64_t ld, int64_t sT, int n, int batch, float* work,
+                         hipStream_t s);
 }  // namespace kfac
 
 std::vector<at::Tensor> tridiag_eigh_dc(const at::Tensor& d, const at::Tensor& e);
-rocblas_handle kfac_rocblas_handle(hipStream_t s);
-
-#define TS_ROCBLAS(expr)                                                         \
-  do {                                                                           \
-    rocblas_status _s = (expr);                                                  \
-    TORCH_CHECK(_s == rocblas_status_success, "rocBLAS error ", (int)_s, " in ", #expr); \
-  } while (0)
 
 namespace {
 
@@ -62,7 +61,7 @@ hipStream_t cur() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().str
 // nb reflectors per UT block (T^-1 = striu(V^T V) + diag(1/tau)), last block
 // first.
 void apply_q1(const at::Tensor& A, const at::Tensor& tau1, int64_t n, int64_t nref,
-              at::Tensor& X, int64_t nb, rocblas_handle hb) {
+              at::Tensor& X, int64_t nb) {
   const int64_t off = kfac::twostage_band();
   auto fopt = X.options();
   const int64_t b = X.size(0);
@@ -78,38 +77,38 @@ void apply_q1(const at::Tensor& A, const at::Tensor& tau1, int64_t n, int64_t nr
     auto live = t.ne(0).to(at::kFloat);
     auto eye_bs = at::eye(bs, rows, fopt).unsqueeze(0);
     vt = (vt + eye_bs) * live.unsqueeze(2);
-    auto g = at::bmm(vt, vt.transpose(1, 2));
+    vt = vt.contiguous();
+    auto g = at::empty({b, bs, bs}, fopt);  // V V^T (native fp32 MFMA)
+    kfac::gemm_f32_batched(0, 1, (int)bs, (int)bs, (int)rows, 1.f, vt.data_ptr<float>(), rows,
+                           bs * rows, vt.data_ptr<float>(), rows, bs * rows, 0.f,
+                           g.data_ptr<float>(), bs, bs * bs, (int)b, cur());
     auto dinv = at::where(t.eq(0), at::ones_like(t), at::reciprocal(at::where(t.eq(0),
                                                                                 at::ones_like(t), t)));
     auto u = at::triu(g, 1) + at::diag_embed(dinv);
     // tm = u^-1 (u upper triangular, row-major) by rocBLAS trsm on the
     // column-major view (u^T, lower): the result read row-major is u^-1
-    u = u.contiguous();
-    auto tm = at::eye(bs, fopt).expand({b, bs, bs}).contiguous();
+    // tm = u^-1 (u upper triangular): native blocked triangular inverse
+    auto tm = u.contiguous();
     {
-      const float one1 = 1.f;
-      TS_ROCBLAS(rocblas_strsm_strided_batched(
-          hb, rocblas_side_left, rocblas_fill_lower, rocblas_operation_none,
-          rocblas_diagonal_non_unit, (int)bs, (int)bs, &one1, u.data_ptr<float>(), (int)bs,
-          bs * bs, tm.data_ptr<float>(), (int)bs, bs * bs, (int)b));
+      auto work = at::empty({std::max<int64_t>(b * bs * bs / 2 + bs, 1)}, fopt);
+      kfac::trinv_upper_batched(tm.data_ptr<float>(), bs, bs * bs, (int)bs, (int)b,
+                                work.data_ptr<float>(), cur());
     }
-    // rows p0+off.. of X in place (leading dimension n): rocBLAS, row-major
-    // operands as column-major transposes (ATen would copy the block)
+    // rows p0+off.. of X in place (leading dimension n), native fp32 MFMA:
+    // W1 = vt Xs ([bs, rows] x [rows, n]), W2 = tm W1, Xs -= vt^T W2
     vt = vt.contiguous();
     float* xs = X.data_ptr<float>() + (p0 + off) * n;
     auto w1 = at::empty({b, bs, n}, fopt);
-    const float one = 1.f, zero = 0.f, mone = -1.f;
-    // W1 = V^T-rows * Xs  <=>  W1^T = Xs^T vt^T
-    TS_ROCBLAS(rocblas_sgemm_strided_batched(
-        hb, rocblas_operation_none, rocblas_operation_none, (int)n, (int)bs, (int)rows, &one, xs,
-        (int)n, n * n, vt.data_ptr<float>(), (int)rows, bs * rows, &zero, w1.data_ptr<float>(),
-        (int)n, bs * n, (int)b));
-    auto w2 = at::bmm(tm, w1).contiguous();
-    // Xs -= vt^T W2  <=>  Xs^T -= W2^T vt
-    TS_ROCBLAS(rocblas_sgemm_strided_batched(
-        hb, rocblas_operation_none, rocblas_operation_transpose, (int)n, (int)rows, (int)bs,
-        &mone, w2.data_ptr<float>(), (int)n, bs * n, vt.data_ptr<float>(), (int)rows, bs * rows,
-        &one, xs, (int)n, n * n, (int)b));
+    auto w2 = at::empty({b, bs, n}, fopt);
+    kfac::gemm_f32_batched(0, 0, (int)bs, (int)n, (int)rows, 1.f, vt.data_ptr<float>(), rows,
+                           bs * rows, xs, n, n * n, 0.f, w1.data_ptr<float>(), n, bs * n,
+                           (int)b, cur());
+    kfac::gemm_f32_batched(0, 0, (int)bs, (int)n, (int)bs, 1.f, tm.data_ptr<float>(), bs,
+                           bs * bs, w1.data_ptr<float>(), n, bs * n, 0.f,
+                           w2.data_ptr<float>(), n, bs * n, (int)b, cur());
+    kfac::gemm_f32_batched(1, 0, (int)rows, (int)n, (int)bs, -1.f, vt.data_ptr<float>(), rows,
+                           bs * rows, w2.data_ptr<float>(), n, bs * n, 1.f, xs, n, n * n,
+                           (int)b, cur());
   }
 }
 
@@ -151,8 +150,6 @@ std::vector<at::Tensor> eigh_twostage(const at::Tensor& A_in, bool timed) {
   auto Tw = at::empty({2, b, B, B}, fopt);
   auto tau1 = at::zeros({b, n}, fopt);
   int64_t nref = 0;
-  rocblas_handle hb = kfac_rocblas_handle(s);
-  TS_ROCBLAS(rocblas_set_pointer_mode(hb, rocblas_pointer_mode_host));
   const int64_t nblk = (n + 63) / 64;
   auto Ypart = at::empty({8, b, n, B}, fopt);
   auto Spart = at::empty({b, nblk * 8, B * B}, fopt);
@@ -221,7 +218,7 @@ std::vector<at::Tensor> eigh_twostage(const at::Tensor& A_in, bool timed) {
   kfac::bt2_apply(V2.data_ptr<float>(), nslot, T2.data_ptr<float>(), (int)n, kmax, (int)b,
                   X.data_ptr<float>(), n * n, (int)n, s);
   mark();
-  if (nref > 0) apply_q1(A, tau1, n, nref, X, 512, hb);
+  if (nref > 0) apply_q1(A, tau1, n, nref, X, 512);
   mark();
   at::Tensor times = at::zeros({std::max<int64_t>((int64_t)ev.size() - 1, 0)},
                                at::TensorOptions().dtype(at::kFloat));

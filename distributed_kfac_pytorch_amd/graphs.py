@@ -440,10 +440,15 @@ class GraphedTrainStep:
 
         From one saved state (and CUDA RNG state) run the step eagerly twice
         and replay the graph twice.  Eager vs eager is the noise floor of the
-        step's nondeterministic kernels (atomics in MIOpen solvers); a replay
-        must agree with the eager step, and with the other replay, within
-        ``max(10 x noise, 1e-3)`` -- relative to the parameter update and to
-        the gradient norm -- and be finite.  A graph that depends on memory
+        step's nondeterministic kernels (atomics in MIOpen solvers), measured
+        per tensor; every parameter (relative to its update) and every
+        gradient (relative to its norm) of both replays must agree with the
+        eager step, and the replays with each other, within ``10 x noise +
+        1e-3`` of that tensor, and be finite.  Per tensor, because a solver
+        that corrupts one layer's input gradient (MIOpen's deterministic
+        bf16 backward-data under the tuned database accumulates into memory
+        the graph never re-zeroes: profiles/r5/conv_replay/) hides in a
+        whole-model norm behind the large layers.  A graph that depends on memory
         or library state outside the capture (the round-2..4 failures:
         free global-pool blocks, MIOpen solvers) fails it.  The state is
         restored afterwards."""
@@ -487,33 +492,45 @@ class GraphedTrainStep:
         r1, r2 = replay(), replay()
         restore()
 
-        @torch.no_grad()
-        def dist_(a: tuple, b: tuple) -> tuple[float, float]:
-            num = den = gnum = gden = torch.zeros((), dtype=torch.float64, device=p0[0].device)
-            for x, y, z in zip(a[0], b[0], p0):
-                num = num + (x.double() - y.double()).square().sum()
-                den = den + (y.double() - z.double()).square().sum()
-            for x, y in zip(a[1], b[1]):
-                if x is None or y is None:
-                    continue
-                gnum = gnum + (x.double() - y.double()).square().sum()
-                gden = gden + y.double().square().sum()
-            v = torch.stack([num, den, gnum, gden]).cpu().tolist()
-            dp = (v[0] / v[1]) ** 0.5 if v[1] > 0 else (0.0 if v[0] == 0 else float('inf'))
-            dg = (v[2] / v[3]) ** 0.5 if v[3] > 0 else (0.0 if v[2] == 0 else float('inf'))
-            return dp, dg
+        idx = [i for i, g in enumerate(e1[1]) if g is not None]
 
-        noise = max(dist_(e2, e1))
-        worst = max(max(dist_(r1, e1)), max(dist_(r2, e1)), max(dist_(r2, r1)))
+        @torch.no_grad()
+        def rel(xs: list, ys: list, refs: list) -> torch.Tensor:
+            num = torch.stack(torch._foreach_norm(torch._foreach_sub(xs, ys))).double()
+            den = torch.stack(torch._foreach_norm(refs)).double()
+            inf = torch.full_like(num, float('inf'))
+            return torch.where(den > 0, num / den.clamp_min(1e-300),
+                               torch.where(num > 0, inf, torch.zeros_like(num)))
+
+        def dist(a: tuple, b: tuple) -> torch.Tensor:
+            # per tensor: parameters relative to the eager update, gradients
+            # relative to the eager gradient
+            upd = torch._foreach_sub(e1[0], p0)
+            dp = rel(a[0], b[0], upd)
+            ga = [a[1][i] for i in idx]
+            gb = [b[1][i] for i in idx]
+            dg = rel(ga, gb, [e1[1][i] for i in idx])
+            return torch.cat([dp, dg])
+
+        names = [f'param[{i}]' for i in range(len(params))] + [f'grad[{i}]' for i in idx]
+        noise = dist(e2, e1)
+        tol = 10.0 * noise + 1e-3
+        worst_ratio, worst_at, worst = 0.0, None, 0.0
+        for a, b in ((r1, e1), (r2, e1), (r2, r1)):
+            d = dist(a, b)
+            ratio = torch.where(torch.isfinite(d), d / tol, torch.full_like(d, float('inf')))
+            r, i = (float(v) for v in torch.max(ratio, 0))
+            if r > worst_ratio or worst_at is None:
+                worst_ratio, worst_at, worst = r, names[int(i)], float(d[int(i)])
         finite = all(bool(torch.isfinite(t).all()) for r in (r1, r2) for t in r[0])
-        tol = max(10.0 * noise, 1e-3)
-        ok = finite and worst <= tol  # NaN compares False
-        self.verify_report[kind] = {'noise': noise, 'worst': worst, 'tol': tol,
+        ok = finite and worst_ratio <= 1.0  # NaN compares False
+        self.verify_report[kind] = {'noise_max': float(noise.max()), 'worst': worst,
+                                    'worst_tensor': worst_at, 'worst_over_tol': worst_ratio,
                                     'finite': finite, 'ok': ok}
         if not ok:
-            logger.warning('step graph %r failed its capture-time check (replay vs eager %.3g, '
-                           'eager noise %.3g, finite %s): graphs dropped, running eagerly',
-                           kind, worst, noise, finite)
+            logger.warning('step graph %r failed its capture-time check (%s differs by %.3g, '
+                           '%.3g x its tolerance; finite %s): graphs dropped, running eagerly',
+                           kind, worst_at, worst, worst_ratio, finite)
         return ok
 
     def _drop_graphs(self) -> None:

@@ -51,6 +51,7 @@ from typing import Any
 import torch
 
 from distributed_kfac_pytorch_amd.ops import twostage
+from distributed_kfac_pytorch_amd.ops._native import load_error as _native_error
 from distributed_kfac_pytorch_amd.ops._native import native
 from distributed_kfac_pytorch_amd.ops._native import use_native
 
@@ -547,18 +548,34 @@ def apply_q_blocked(red: torch.Tensor, tau: torch.Tensor, z: torch.Tensor,
     vt[:, idx, idx + 1] = 1.0
     live = (tau != 0).to(red.dtype)
     vt.mul_(live.unsqueeze(-1))
+    lib = native() if red.is_cuda and red.dtype == torch.float32 else None
+    if red.is_cuda and red.dtype == torch.float32 and lib is None:
+        raise RuntimeError(f'native extension missing: {_native_error()}')
     eye = torch.eye(nb, device=red.device, dtype=red.dtype)
     for p in reversed(range(0, n - 1, nb)):
         q = min(p + nb, n - 1)
         b = q - p
         v = vt[:, p:q, p + 1:]  # [c, b, m]: V_b^T restricted to rows >= p+1
-        g = torch.bmm(v, v.transpose(1, 2))
         t_ = tau[:, p:q]
         dinv = torch.where(t_ == 0, torch.ones_like(t_), 1.0 / torch.where(
             t_ == 0, torch.ones_like(t_), t_))
+        xs = x[:, p + 1:, :]
+        if lib is not None:
+            # native fp32 MFMA GEMMs + blocked triangular inverse
+            # (csrc/gemm_f32.hip): no library GEMM in the refresh
+            g = torch.empty(c, b, b, device=red.device, dtype=red.dtype)
+            lib.gemm_f32(v, v, g, False, True)
+            tm = torch.triu(g, diagonal=1) + torch.diag_embed(dinv)
+            lib.trinv_upper_(tm)
+            y = torch.empty(c, b, n, device=red.device, dtype=red.dtype)
+            lib.gemm_f32(v, xs, y, False, False)
+            w = torch.empty_like(y)
+            lib.gemm_f32(tm, y, w, False, False)
+            lib.gemm_f32(v, w, xs, True, False, -1.0, 1.0)
+            continue
+        g = torch.bmm(v, v.transpose(1, 2))
         u = torch.triu(g, diagonal=1) + torch.diag_embed(dinv)
         tm = torch.linalg.solve_triangular(u, eye[:b, :b].expand(c, b, b), upper=True)
-        xs = x[:, p + 1:, :]
         w = torch.bmm(tm, torch.bmm(v, xs))
         xs.baddbmm_(v.transpose(1, 2), w, alpha=-1.0)
     return x

@@ -524,3 +524,51 @@ def test_eigh_many_repairs_nonfinite_results(cuda, monkeypatch):
     for m, (d, q) in zip(mats, linalg.eigh_many(mats)):
         assert torch.isfinite(q).all()
         _check_eigpairs(m, d, q)
+
+
+@pytest.mark.parametrize('ta,tb', [(False, False), (True, False), (False, True), (True, True)])
+@pytest.mark.parametrize('m,n,k,batch', [(128, 128, 16, 1), (100, 300, 77, 3), (512, 4608, 512, 2),
+                                         (1, 65, 1000, 2), (257, 31, 2049, 1)])
+def test_gemm_f32_matches_float64(cuda, ta, tb, m, n, k, batch) -> None:
+    """csrc/gemm_f32.hip (the eigensolver's back-transform / D&C GEMMs) vs
+    float64: exact fp32 products, fp32 accumulation."""
+    lib = _native.native()
+    g = torch.Generator(device='cpu').manual_seed(m + n + k)
+    a = torch.randn(batch, *((k, m) if ta else (m, k)), generator=g)
+    b = torch.randn(batch, *((n, k) if tb else (k, n)), generator=g)
+    c0 = torch.randn(batch, m, n, generator=g)
+    ref = 0.5 * (a.double().transpose(1, 2) if ta else a.double()) @ (
+        b.double().transpose(1, 2) if tb else b.double()) - 2.0 * c0.double()
+    c = c0.to(cuda)
+    lib.gemm_f32(a.to(cuda), b.to(cuda), c, ta, tb, 0.5, -2.0)
+    err = float((c.double().cpu() - ref).abs().max() / ref.abs().max())
+    assert err < 2e-6, err
+
+
+def test_gemm_f32_strided_views(cuda) -> None:
+    """Row-strided views (the in-place back-transform updates rows p+1.. of
+    X with leading dimension n)."""
+    lib = _native.native()
+    x = torch.randn(2, 300, 300, device=cuda)
+    v = torch.randn(2, 40, 300, device=cuda)[:, :, 17:]  # [2, 40, 283], row stride 300
+    w = torch.randn(2, 40, 300, device=cuda)
+    ref = x.double().clone()
+    ref[:, 17:, :] -= v.double().transpose(1, 2) @ w.double()
+    lib.gemm_f32(v, w, x[:, 17:, :], True, False, -1.0, 1.0)
+    assert float((x.double() - ref).abs().max()) < 1e-4
+
+
+@pytest.mark.parametrize('n,batch', [(1, 1), (64, 2), (200, 3), (512, 4), (511, 1)])
+def test_trinv_upper_matches_float64(cuda, n, batch) -> None:
+    """Blocked triangular inverse (64 x 64 back substitution + GEMM merges)
+    of compact-WY-like upper-triangular matrices."""
+    lib = _native.native()
+    g = torch.Generator(device='cpu').manual_seed(n)
+    u = torch.triu(torch.randn(batch, n, n, generator=g) * 0.1, diagonal=1)
+    u = u + torch.diag_embed(1.0 + torch.rand(batch, n, generator=g))
+    t = u.to(cuda).contiguous()
+    lib.trinv_upper_(t)
+    ref = torch.linalg.inv(u.double())
+    err = float((t.double().cpu() - ref).abs().max() / ref.abs().max())
+    assert err < 1e-5, err
+    assert torch.equal(torch.tril(t, diagonal=-1).cpu(), torch.zeros_like(u))

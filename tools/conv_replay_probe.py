@@ -71,7 +71,10 @@ def main() -> None:
     ap.add_argument('--batch', type=int, default=32)
     ap.add_argument('--image', type=int, default=224)
     ap.add_argument('--only', default='', help='comma list of conv names')
+    ap.add_argument('--deterministic', type=int, default=0,
+                    help='torch.backends.cudnn.deterministic (the twin test sets it)')
     args = ap.parse_args()
+    torch.backends.cudnn.deterministic = bool(args.deterministic)
     torch.backends.cudnn.benchmark = False
     dev = torch.device('cuda', 0)
     torch.manual_seed(0)

@@ -85,7 +85,10 @@ def main() -> None:
     ap.add_argument('--kfac', type=int, default=1)
     ap.add_argument('--steps', type=int, default=8)
     ap.add_argument('--db', default='tuned')
+    ap.add_argument('--deterministic', type=int, default=0,
+                    help='torch.backends.cudnn.deterministic (the twin test sets it)')
     args = ap.parse_args()
+    torch.backends.cudnn.deterministic = bool(args.deterministic)
     dev = torch.device('cuda', 0)
     torch.backends.cudnn.benchmark = False
     torch.manual_seed(0)
@@ -95,7 +98,7 @@ def main() -> None:
              torch.randint(0, 1000, (32,), generator=gen)) for _ in range(4)]
     A = build(base, dev, True, bool(args.fused_cast), bool(args.kfac))
     B = build(base, dev, False, bool(args.fused_cast), bool(args.kfac)) if args.twin else None
-    cfg = {'twin': args.twin, 'fused_cast': args.fused_cast, 'kfac': args.kfac,
+    cfg = {'deterministic': args.deterministic, 'twin': args.twin, 'fused_cast': args.fused_cast, 'kfac': args.kfac,
            'db': args.db, 'factor_stream': os.environ.get('KFAC_FACTOR_STREAM', 'auto')}
     first_bad = None
     for i in range(args.steps):
