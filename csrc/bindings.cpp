@@ -117,10 +117,26 @@ namespace kfac {
 void gemm_f32_batched(int ta, int tb, int M, int N, int K, float alpha, const float* A,
                       int64_t lda, int64_t sA, const float* B, int64_t ldb, int64_t sB,
                       float beta, float* C, int64_t ldc, int64_t sC, int batch,
-                      hipStream_t s);
+                      hipStream_t s, float* ws, int64_t ws_floats);
+int64_t gemm_f32_ws_floats(int M, int N, int K, int batch);
 void trinv_upper_batched(float* T, int64_t ld, int64_t sT, int n, int batch, float* work,
                          hipStream_t s);
 }  // namespace kfac
+
+namespace {
+// native fp32 MFMA GEMM (csrc/gemm_f32.hip) with its split-K workspace
+void gemm_native(int ta, int tb, int64_t M, int64_t N, int64_t K, float alpha, const float* A,
+                 int64_t lda, int64_t sA, const float* B, int64_t ldb, int64_t sB, float beta,
+                 float* C, int64_t ldc, int64_t sC, int64_t batch, hipStream_t s,
+                 const at::TensorOptions& opt) {
+  const int64_t wsf = kfac::gemm_f32_ws_floats((int)M, (int)N, (int)K, (int)batch);
+  at::Tensor ws;
+  if (wsf > 0) ws = at::empty({wsf}, opt.dtype(at::kFloat));
+  kfac::gemm_f32_batched(ta, tb, (int)M, (int)N, (int)K, alpha, A, lda, sA, B, ldb, sB, beta, C,
+                         ldc, sC, (int)batch, s, wsf > 0 ? ws.data_ptr<float>() : nullptr, wsf);
+}
+}  // namespace
+
 
 namespace {
 
@@ -1180,9 +1196,9 @@ void gemm_f32(const at::Tensor& a, const at::Tensor& b, at::Tensor& c, bool ta, 
               "gemm_f32: batch mismatch");
   TORCH_CHECK(M < (1LL << 31) && N < (1LL << 31) && K < (1LL << 31) && batch < 65536);
   c10::hip::HIPGuardMasqueradingAsCUDA g(c.device());
-  kfac::gemm_f32_batched(ta, tb, (int)M, (int)N, (int)K, (float)alpha, A.p, A.ld,
+  gemm_native(ta, tb, (int)M, (int)N, (int)K, (float)alpha, A.p, A.ld,
                          A.b == 1 ? 0 : A.sb, B.p, B.ld, B.b == 1 ? 0 : B.sb, (float)beta, C.p,
-                         C.ld, C.sb, (int)batch, cur_stream());
+                         C.ld, C.sb, (int)batch, cur_stream(), c.options());
 }
 
 // T <- T^-1 in place for a batch of upper-triangular [batch, n, n] fp32

@@ -21,6 +21,8 @@
 // fastest so consecutive blocks share their A row panel in L2.
 #include "common.h"
 
+#include <algorithm>
+
 namespace kfac {
 
 namespace {
@@ -40,6 +42,8 @@ struct GemmArgs {
   int M, N, K;
   float alpha, beta;
   int ta, tb;
+  int splits, kchunk;  // split-K: block z = batch * splits, partials to ws
+  float* ws;
 };
 
 // one k tile of op(X) (rows r0.., k0..k0+15) into LDS as [k][row]; 8 scalar
@@ -86,9 +90,13 @@ __global__ void __launch_bounds__(GTHR) gemm_f32_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) float As[2][GK * GLD];
   __shared__ __attribute__((aligned(16))) float Bs[2][GK * GLD];
   const int n0 = blockIdx.x * GT, m0 = blockIdx.y * GT;
-  const int64_t b = blockIdx.z;
-  const float* A = g.A + b * g.sA;
-  const float* B = g.B + b * g.sB;
+  const int64_t b = blockIdx.z / g.splits;
+  const int split = blockIdx.z % g.splits;
+  // this block's k range [kb, ke): offset the operands to kb
+  const int kb = split * g.kchunk;
+  const int Kc = min(g.K - kb, g.kchunk);
+  const float* A = g.A + b * g.sA + (g.ta ? (int64_t)kb * g.lda : (int64_t)kb);
+  const float* B = g.B + b * g.sB + (g.tb ? (int64_t)kb : (int64_t)kb * g.ldb);
   float* C = g.C + b * g.sC;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int wm = (w >> 1) * 64, wn = (w & 1) * 64;
@@ -101,10 +109,10 @@ __global__ void __launch_bounds__(GTHR) gemm_f32_kernel(GemmArgs g) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
-  const int nk = (g.K + GK - 1) / GK;
+  const int nk = (Kc + GK - 1) / GK;
   float va[8], vb[8];
-  fetch(A, g.lda, g.ta, g.M, g.K, m0, 0, va);
-  fetch(B, g.ldb, !g.tb, g.N, g.K, n0, 0, vb);  // B[k][n] = row-major [K][N] is "transposed" rows=n
+  fetch(A, g.lda, g.ta, g.M, Kc, m0, 0, va);
+  fetch(B, g.ldb, !g.tb, g.N, Kc, n0, 0, vb);  // B[k][n] = row-major [K][N] is "transposed" rows=n
   stash(As[0], g.ta, va);
   stash(Bs[0], !g.tb, vb);
   __syncthreads();
@@ -112,8 +120,8 @@ __global__ void __launch_bounds__(GTHR) gemm_f32_kernel(GemmArgs g) {
     const int cur = t & 1;
     const bool more = t + 1 < nk;
     if (more) {
-      fetch(A, g.lda, g.ta, g.M, g.K, m0, (t + 1) * GK, va);
-      fetch(B, g.ldb, !g.tb, g.N, g.K, n0, (t + 1) * GK, vb);
+      fetch(A, g.lda, g.ta, g.M, Kc, m0, (t + 1) * GK, va);
+      fetch(B, g.ldb, !g.tb, g.N, Kc, n0, (t + 1) * GK, vb);
     }
     const float* as = As[cur];
     const float* bs = Bs[cur];
@@ -145,6 +153,11 @@ __global__ void __launch_bounds__(GTHR) gemm_f32_kernel(GemmArgs g) {
         const int row = m0 + wm + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
         const int col = n0 + wn + 32 * j + r;
         if (row < g.M && col < g.N) {
+          if (g.splits > 1) {
+            // raw partial [b][split][M][N], summed in split order later
+            g.ws[((b * g.splits + split) * g.M + row) * (int64_t)g.N + col] = acc[i][j][e];
+            continue;
+          }
           float* p = C + (int64_t)row * g.ldc + col;
           const float v = g.alpha * acc[i][j][e];
           *p = g.beta == 0.f ? v : v + g.beta * *p;
@@ -152,16 +165,58 @@ __global__ void __launch_bounds__(GTHR) gemm_f32_kernel(GemmArgs g) {
       }
 }
 
+// C = alpha * sum_s ws[b][s] + beta * C, the splits summed in a fixed order
+__global__ void __launch_bounds__(256) gemm_f32_splitk_reduce(GemmArgs g) {
+  const int64_t MN = (int64_t)g.M * g.N;
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t b = blockIdx.y;
+  if (idx >= MN) return;
+  const float* src = g.ws + b * g.splits * MN + idx;
+  float sum = 0.f;
+  for (int s = 0; s < g.splits; ++s) sum += src[s * MN];
+  const int row = (int)(idx / g.N), col = (int)(idx % g.N);
+  float* p = g.C + b * g.sC + (int64_t)row * g.ldc + col;
+  const float v = g.alpha * sum;
+  *p = g.beta == 0.f ? v : v + g.beta * *p;
+}
+
 }  // namespace
+
+// split-K plan: shapes whose output tiles cannot fill the chip (V V^T of a
+// 512-reflector block: 16 tiles over K = 4608) split K into chunks of >= 512
+// so the grid reaches ~1024 blocks; workspace batch * splits * M * N floats
+// (at most 2^26 floats: fewer splits otherwise)
+static int gemm_splits(int M, int N, int K, int batch) {
+  const int64_t tiles = ceil_div(M, GT) * ceil_div(N, GT) * (int64_t)batch;
+  if (tiles >= 512 || K < 1024) return 1;
+  int64_t s = std::min<int64_t>(ceil_div(1024, tiles), K / 512);
+  while (s > 1 && s * batch * (int64_t)M * N > (1LL << 26)) --s;
+  return (int)std::max<int64_t>(1, s);
+}
+
+int64_t gemm_f32_ws_floats(int M, int N, int K, int batch) {
+  const int s = gemm_splits(M, N, K, batch);
+  return s > 1 ? (int64_t)s * batch * M * N : 0;
+}
 
 void gemm_f32_batched(int ta, int tb, int M, int N, int K, float alpha, const float* A,
                       int64_t lda, int64_t sA, const float* B, int64_t ldb, int64_t sB,
                       float beta, float* C, int64_t ldc, int64_t sC, int batch,
-                      hipStream_t s) {
+                      hipStream_t s, float* ws, int64_t ws_floats) {
   if (M <= 0 || N <= 0 || batch <= 0) return;
-  GemmArgs g{A, B, C, lda, ldb, ldc, sA, sB, sC, M, N, K, alpha, beta, ta, tb};
-  const dim3 grid((unsigned)ceil_div(N, GT), (unsigned)ceil_div(M, GT), (unsigned)batch);
+  int splits = gemm_splits(M, N, K, batch);
+  if (ws == nullptr || ws_floats < (int64_t)splits * batch * M * N) splits = 1;
+  const int kchunk = splits > 1 ? (int)(ceil_div(ceil_div(K, splits), GK) * GK) : K;
+  splits = splits > 1 ? (int)ceil_div(K, kchunk) : 1;
+  GemmArgs g{A, B, C, lda, ldb, ldc, sA, sB, sC, M, N, K, alpha, beta, ta, tb,
+             splits, kchunk > 0 ? kchunk : 1, ws};
+  const dim3 grid((unsigned)ceil_div(N, GT), (unsigned)ceil_div(M, GT),
+                  (unsigned)(batch * splits));
   hipLaunchKernelGGL(gemm_f32_kernel, grid, dim3(GTHR), 0, s, g);
+  if (splits > 1) {
+    const dim3 rg((unsigned)ceil_div((int64_t)M * N, 256), (unsigned)batch);
+    hipLaunchKernelGGL(gemm_f32_splitk_reduce, rg, dim3(256), 0, s, g);
+  }
 }
 
 }  // namespace kfac
@@ -205,11 +260,6 @@ __global__ void __launch_bounds__(TB) trinv64_kernel(float* T, int64_t ld, int64
 
 }  // namespace
 
-void gemm_f32_batched(int ta, int tb, int M, int N, int K, float alpha, const float* A,
-                      int64_t lda, int64_t sA, const float* B, int64_t ldb, int64_t sB,
-                      float beta, float* C, int64_t ldc, int64_t sC, int batch,
-                      hipStream_t s);
-
 // T <- T^-1 for a batch of n x n upper-triangular matrices (row-major, row
 // stride ld, batch stride sT), in place; `work` holds >= batch * n * n / 2
 // floats.  64 x 64 diagonal blocks by back substitution, then pairs of
@@ -229,9 +279,9 @@ void trinv_upper_batched(float* T, int64_t ld, int64_t sT, int n, int batch, flo
       float* t22 = T + (int64_t)(p + h) * ld + p + h;
       // Y = U12 T22 (h x h2), then U12 <- -T11 Y
       gemm_f32_batched(0, 0, h, h2, h2, 1.f, u12, ld, sT, t22, ld, sT, 0.f, work, h2,
-                       (int64_t)h * h2, batch, s);
+                       (int64_t)h * h2, batch, s, nullptr, 0);
       gemm_f32_batched(0, 0, h, h2, h, -1.f, t11, ld, sT, work, h2, (int64_t)h * h2, 0.f, u12,
-                       ld, sT, batch, s);
+                       ld, sT, batch, s, nullptr, 0);
     }
   }
 }

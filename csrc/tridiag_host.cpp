@@ -35,8 +35,24 @@ void jacobi_eigh_batched(const float* A, int64_t n, int64_t batch, int64_t strid
 void gemm_f32_batched(int ta, int tb, int M, int N, int K, float alpha, const float* A,
                       int64_t lda, int64_t sA, const float* B, int64_t ldb, int64_t sB,
                       float beta, float* C, int64_t ldc, int64_t sC, int batch,
-                      hipStream_t s);
+                      hipStream_t s, float* ws, int64_t ws_floats);
+int64_t gemm_f32_ws_floats(int M, int N, int K, int batch);
 }  // namespace kfac
+
+namespace {
+// native fp32 MFMA GEMM (csrc/gemm_f32.hip) with its split-K workspace
+void gemm_native(int ta, int tb, int64_t M, int64_t N, int64_t K, float alpha, const float* A,
+                 int64_t lda, int64_t sA, const float* B, int64_t ldb, int64_t sB, float beta,
+                 float* C, int64_t ldc, int64_t sC, int64_t batch, hipStream_t s,
+                 const at::TensorOptions& opt) {
+  const int64_t wsf = kfac::gemm_f32_ws_floats((int)M, (int)N, (int)K, (int)batch);
+  at::Tensor ws;
+  if (wsf > 0) ws = at::empty({wsf}, opt.dtype(at::kFloat));
+  kfac::gemm_f32_batched(ta, tb, (int)M, (int)N, (int)K, alpha, A, lda, sA, B, ldb, sB, beta, C,
+                         ldc, sC, (int)batch, s, wsf > 0 ? ws.data_ptr<float>() : nullptr, wsf);
+}
+}  // namespace
+
 
 namespace {
 
@@ -137,9 +153,9 @@ std::vector<at::Tensor> tridiag_eigh_dc(const at::Tensor& d_in, const at::Tensor
     // Q_parent = diag(Q1, Q2) W: the two row halves of every subproblem are
     // the children's blocks times W's row halves
     auto Qn = at::empty({G, m, m}, fopt);
-    kfac::gemm_f32_batched(0, 0, (int)h, (int)m, (int)h, 1.f, Q.data_ptr<float>(), h, h * h,
+    gemm_native(0, 0, (int)h, (int)m, (int)h, 1.f, Q.data_ptr<float>(), h, h * h,
                            W.data_ptr<float>(), m, h * m, 0.f, Qn.data_ptr<float>(), m, h * m,
-                           (int)(2 * G), s);
+                           (int)(2 * G), s, fopt);
     Q = Qn;
     D = svals;
   }

@@ -45,10 +45,26 @@ void bt2_apply(const float* V2, int64_t sV2, const float* T, int n, int kmax, in
 void gemm_f32_batched(int ta, int tb, int M, int N, int K, float alpha, const float* A,
                       int64_t lda, int64_t sA, const float* B, int64_t ldb, int64_t sB,
                       float beta, float* C, int64_t ldc, int64_t sC, int batch,
-                      hipStream_t s);
+                      hipStream_t s, float* ws, int64_t ws_floats);
+int64_t gemm_f32_ws_floats(int M, int N, int K, int batch);
 void trinv_upper_batched(float* T, int64_t ld, int64_t sT, int n, int batch, float* work,
                          hipStream_t s);
 }  // namespace kfac
+
+namespace {
+// native fp32 MFMA GEMM (csrc/gemm_f32.hip) with its split-K workspace
+void gemm_native(int ta, int tb, int64_t M, int64_t N, int64_t K, float alpha, const float* A,
+                 int64_t lda, int64_t sA, const float* B, int64_t ldb, int64_t sB, float beta,
+                 float* C, int64_t ldc, int64_t sC, int64_t batch, hipStream_t s,
+                 const at::TensorOptions& opt) {
+  const int64_t wsf = kfac::gemm_f32_ws_floats((int)M, (int)N, (int)K, (int)batch);
+  at::Tensor ws;
+  if (wsf > 0) ws = at::empty({wsf}, opt.dtype(at::kFloat));
+  kfac::gemm_f32_batched(ta, tb, (int)M, (int)N, (int)K, alpha, A, lda, sA, B, ldb, sB, beta, C,
+                         ldc, sC, (int)batch, s, wsf > 0 ? ws.data_ptr<float>() : nullptr, wsf);
+}
+}  // namespace
+
 
 std::vector<at::Tensor> tridiag_eigh_dc(const at::Tensor& d, const at::Tensor& e);
 
@@ -79,9 +95,9 @@ void apply_q1(const at::Tensor& A, const at::Tensor& tau1, int64_t n, int64_t nr
     vt = (vt + eye_bs) * live.unsqueeze(2);
     vt = vt.contiguous();
     auto g = at::empty({b, bs, bs}, fopt);  // V V^T (native fp32 MFMA)
-    kfac::gemm_f32_batched(0, 1, (int)bs, (int)bs, (int)rows, 1.f, vt.data_ptr<float>(), rows,
+    gemm_native(0, 1, (int)bs, (int)bs, (int)rows, 1.f, vt.data_ptr<float>(), rows,
                            bs * rows, vt.data_ptr<float>(), rows, bs * rows, 0.f,
-                           g.data_ptr<float>(), bs, bs * bs, (int)b, cur());
+                           g.data_ptr<float>(), bs, bs * bs, (int)b, cur(), fopt);
     auto dinv = at::where(t.eq(0), at::ones_like(t), at::reciprocal(at::where(t.eq(0),
                                                                                 at::ones_like(t), t)));
     auto u = at::triu(g, 1) + at::diag_embed(dinv);
@@ -100,15 +116,15 @@ void apply_q1(const at::Tensor& A, const at::Tensor& tau1, int64_t n, int64_t nr
     float* xs = X.data_ptr<float>() + (p0 + off) * n;
     auto w1 = at::empty({b, bs, n}, fopt);
     auto w2 = at::empty({b, bs, n}, fopt);
-    kfac::gemm_f32_batched(0, 0, (int)bs, (int)n, (int)rows, 1.f, vt.data_ptr<float>(), rows,
+    gemm_native(0, 0, (int)bs, (int)n, (int)rows, 1.f, vt.data_ptr<float>(), rows,
                            bs * rows, xs, n, n * n, 0.f, w1.data_ptr<float>(), n, bs * n,
-                           (int)b, cur());
-    kfac::gemm_f32_batched(0, 0, (int)bs, (int)n, (int)bs, 1.f, tm.data_ptr<float>(), bs,
+                           (int)b, cur(), fopt);
+    gemm_native(0, 0, (int)bs, (int)n, (int)bs, 1.f, tm.data_ptr<float>(), bs,
                            bs * bs, w1.data_ptr<float>(), n, bs * n, 0.f,
-                           w2.data_ptr<float>(), n, bs * n, (int)b, cur());
-    kfac::gemm_f32_batched(1, 0, (int)rows, (int)n, (int)bs, -1.f, vt.data_ptr<float>(), rows,
+                           w2.data_ptr<float>(), n, bs * n, (int)b, cur(), fopt);
+    gemm_native(1, 0, (int)rows, (int)n, (int)bs, -1.f, vt.data_ptr<float>(), rows,
                            bs * rows, w2.data_ptr<float>(), n, bs * n, 1.f, xs, n, n * n,
-                           (int)b, cur());
+                           (int)b, cur(), fopt);
   }
 }
 

@@ -412,7 +412,7 @@ class GraphedTrainStep:
     def _state(self, kind: str) -> list[torch.Tensor]:
         """Every tensor a step of ``kind`` reads and writes besides its
         inputs: parameters, module buffers (BN statistics), optimizer state
-        and, for factor-update steps, the K-FAC factors."""
+        and the K-FAC factors."""
         out: list[torch.Tensor] = []
         seen: set[int] = set()
 
@@ -429,7 +429,7 @@ class GraphedTrainStep:
             for v in st.values():
                 add(v)
         p = self.preconditioner
-        if p is not None and kind == 'factor':
+        if p is not None:  # the check also runs an eager factor-update step
             for _, layer in p._layers.values():
                 add(layer.a_factor)
                 add(layer.g_factor)
@@ -439,7 +439,8 @@ class GraphedTrainStep:
         """Capture-time self-check of the ``kind`` graph.
 
         From one saved state (and CUDA RNG state) run the step eagerly twice
-        and replay the graph twice.  Eager vs eager is the noise floor of the
+        and replay the graph twice, the second replay after an eager step of
+        the other kind.  Eager vs eager is the noise floor of the
         step's nondeterministic kernels (atomics in MIOpen solvers), measured
         per tensor; every parameter (relative to its update) and every
         gradient (relative to its norm) of both replays must agree with the
@@ -471,10 +472,10 @@ class GraphedTrainStep:
             return ([q.detach().clone() for q in params],
                     [None if g is None else g.detach().clone() for g in grads])
 
-        def eager() -> tuple[list, list]:
+        def eager(step_at: int | None = None) -> tuple[list, list]:
             restore()
             if p is not None:
-                p._steps = at
+                p._steps = at if step_at is None else step_at
             self._eager_step()
             if p is not None:
                 p._steps = steps
@@ -489,7 +490,17 @@ class GraphedTrainStep:
 
         p0 = [q.detach().clone() for q in params]
         e1, e2 = eager(), eager()
-        r1, r2 = replay(), replay()
+        r1 = replay()
+        # the second replay follows an eager step of the OTHER kind -- what
+        # runs between replays in training (a factor-update step between
+        # plain replays): a graph that depends on state an eager step
+        # rewrites (MIOpen's deterministic bf16 backward-data under the tuned
+        # database: profiles/r5/) fails here, not on back-to-back replays
+        other = None
+        if p is not None:
+            other = self._next_step_of('factor' if kind == 'plain' else 'plain')
+        eager(other)
+        r2 = replay()
         restore()
 
         idx = [i for i, g in enumerate(e1[1]) if g is not None]

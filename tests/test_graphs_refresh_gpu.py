@@ -104,8 +104,12 @@ def _rel(p: torch.Tensor, q: torch.Tensor) -> float:
     (False, False, ('plain',), None),
 ])
 def test_graph_replay_interleaved_with_eager_twin(cuda, amp, use_kfac, kinds, conv_mode) -> None:
+    _twin(cuda, amp, use_kfac, kinds, conv_mode, deterministic=True)
+
+
+def _twin(cuda, amp, use_kfac, kinds, conv_mode, deterministic: bool) -> None:  # type: ignore[no-untyped-def]
     det = torch.backends.cudnn.deterministic
-    torch.backends.cudnn.deterministic = True
+    torch.backends.cudnn.deterministic = deterministic
     try:
         torch.manual_seed(0)
         base = resnet50()
@@ -170,3 +174,89 @@ def test_graph_replay_interleaved_with_eager_twin(cuda, amp, use_kfac, kinds, co
         assert all(o.grad_fn is None for o in run.outputs.values())
     finally:
         torch.backends.cudnn.deterministic = det
+
+
+_CHILD = r"""
+import sys, torch
+sys.path.insert(0, {root!r})
+from tests.test_graphs_refresh_gpu import _twin
+_twin(torch.device('cuda:0'), True, True, ('plain',), {mode!r}, deterministic={det!r})
+print('TWIN-OK')
+"""
+
+
+def _tuned_db_child(mode, det: bool):  # type: ignore[no-untyped-def]
+    import os
+    import shutil
+    import subprocess
+    import sys
+    import tempfile
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    db = tempfile.mkdtemp(prefix='miopen_tuned_')
+    for f in os.listdir(os.path.join(root, 'miopen_db')):
+        shutil.copy(os.path.join(root, 'miopen_db', f), db)
+    env = {**os.environ, 'MIOPEN_USER_DB_PATH': db}
+    return subprocess.run([sys.executable, '-c', _CHILD.format(root=root, mode=mode, det=det)],
+                          cwd=root, env=env, capture_output=True, text=True, timeout=400)
+
+
+@pytest.mark.parametrize('conv_mode', [None, 'gemm'])
+def test_twin_under_tuned_miopen_db(cuda, conv_mode) -> None:
+    """The bf16 twin test under the bench's tuned MIOpen database
+    (``miopen_db/``, the configuration bench.py runs: MIOpen free to pick
+    its atomic solvers), in a fresh process: finite at every step, replays,
+    capture-time check passed, twins bit-exact up to MIOpen's first
+    nondeterministic step and within one step of solver noise there."""
+    p = _tuned_db_child(conv_mode, False)
+    assert p.returncode == 0 and 'TWIN-OK' in p.stdout, p.stdout[-3000:] + p.stderr[-3000:]
+
+
+_DET_CHILD = r"""
+import sys, json, torch
+sys.path.insert(0, {root!r})
+import tests.test_graphs_refresh_gpu as t
+torch.backends.cudnn.deterministic = True
+torch.manual_seed(0)
+base = t.resnet50()
+A = t._build(base, torch.device('cuda:0'), True, True, True, ('plain',), 'gemm')
+gen = torch.Generator(device='cpu').manual_seed(1)
+for i in range(4):
+    A[2].copy_(torch.randn(32, 3, 224, 224, generator=gen))
+    A[3].copy_(torch.randint(0, 1000, (32,), generator=gen))
+    A[4]()
+torch.cuda.synchronize()
+fin = all(bool(torch.isfinite(p).all()) for p in A[0].parameters())
+print('RESULT ' + json.dumps(dict(finite=fin, replays=A[4].replays, enabled=A[4].enabled,
+                                  verify=A[4].verify_report)))
+"""
+
+
+def test_unsafe_solver_graph_is_refused(cuda) -> None:
+    """With ``cudnn.deterministic`` the tuned database leaves MIOpen's CK
+    grouped backward-data solver for the 3x3 convolutions, whose replays
+    accumulate into memory the graph never re-zeroes (the second replay of
+    a lone conv returns twice the first: profiles/r5/conv_replay/).  The
+    runner's capture-time check must catch it and run eagerly (or the
+    replays must stay finite): parameters finite either way."""
+    import json
+    import os
+    import shutil
+    import subprocess
+    import sys
+    import tempfile
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    db = tempfile.mkdtemp(prefix='miopen_tuned_')
+    for f in os.listdir(os.path.join(root, 'miopen_db')):
+        shutil.copy(os.path.join(root, 'miopen_db', f), db)
+    p = subprocess.run([sys.executable, '-c', _DET_CHILD.format(root=root)], cwd=root,
+                       env={**os.environ, 'MIOPEN_USER_DB_PATH': db},
+                       capture_output=True, text=True, timeout=400)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith('RESULT ')]
+    assert p.returncode == 0 and lines, p.stdout[-3000:] + p.stderr[-3000:]
+    out = json.loads(lines[-1][7:])
+    assert out['finite'], out
+    ok = out['verify'].get('plain', {}).get('ok')
+    # either the check refused the graph (eager from then on) or it passed
+    assert (ok is False and not out['enabled'] and out['replays'] == 0) or ok, out
