@@ -386,7 +386,14 @@ class BaseKFACPreconditioner:
         self._multi_apply: Any = None
         self._grouped: Any = None
         self._graphs: Any = None
-        if os.environ.get('KFAC_GRAPHS', '1') != '0':
+        # Precondition-phase HIP graphs (StepGraphs) are opt-in
+        # (KFAC_GRAPHS=1): on the eager step path -- every multi-rank job --
+        # replaying them left the GPU idle ~7 ms per ResNet-50 step (eager
+        # plain step 24.4-25.1 ms with them vs 17.06 ms without, fp32, same
+        # tree: profiles/r5/eager_stepgraphs/), while the grouped kernels
+        # launched eagerly are only 4 + 3 launches.  Whole-step graphs
+        # (graphs.GraphedTrainStep) capture the phase anyway.
+        if os.environ.get('KFAC_GRAPHS', '0') == '1':
             self._graphs = StepGraphs()
         # factor SYRKs (+ their all-reduce) run on a side stream forked from
         # the hook's stream, so they overlap the rest of forward / backward;

@@ -115,6 +115,9 @@ def test_graph_replay_matches_eager(cuda, prediv, method):
         )
         for m in models
     ]
+    from distributed_kfac_pytorch_amd.base_preconditioner import StepGraphs
+
+    pres[0]._graphs = StepGraphs()  # opt-in (KFAC_GRAPHS=1)
     pres[1]._graphs = None  # eager reference
     opts = [torch.optim.SGD(m.parameters(), lr=0.05) for m in models]
     torch.manual_seed(2)

@@ -79,7 +79,11 @@ def deterministic():
 def _eager_runner(device: torch.device, method: str = 'eigen', step_graphs: bool = True,
                   set_to_none: bool = False):
     model, opt, pre, fb = _setup(device, method=method)
-    if not step_graphs:
+    if step_graphs:
+        from distributed_kfac_pytorch_amd.base_preconditioner import StepGraphs
+
+        pre._graphs = StepGraphs()  # opt-in (KFAC_GRAPHS=1)
+    else:
         pre._graphs = None
 
     def run() -> float:

@@ -19,4 +19,5 @@ timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d "$raw" -o run 
 csv=$(find "$raw" -name '*kernel_trace.csv' | head -n 1)
 [ -n "$csv" ] || { echo "no kernel trace"; exit 1; }
 python3 tools/trace_summary.py "$csv" "$out/window.txt" identity_kernel "${STEPS:-20}"
+python3 tools/trace_gaps_csv.py "$csv" "$out/gaps.txt" 20
 head -n 30 "$out/window.txt"
