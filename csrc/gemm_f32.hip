@@ -46,45 +46,69 @@ struct GemmArgs {
   float* ws;
 };
 
-// one k tile of op(X) (rows r0.., k0..k0+15) into LDS as [k][row]; 8 scalar
-// loads per thread, issued together into registers first
-__device__ __forceinline__ void fetch(const float* __restrict__ X, int64_t ld, int trans,
-                                      int rows, int K, int r0, int k0, float (&v)[8]) {
-#pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    const int e = threadIdx.x + GTHR * u;  // 0 .. 2047
-    int r, k;
-    if (trans) {  // stored [K][ld]: consecutive threads walk the row index
-      r = e & (GT - 1);
-      k = e >> 7;
-    } else {      // stored [rows][ld]: consecutive threads walk k
-      r = e >> 4;
-      k = e & (GK - 1);
-    }
-    const int gr = r0 + r, gk = k0 + k;
-    const bool ok = gr < rows && gk < K;
-    const int64_t off = trans ? (int64_t)(ok ? gk : 0) * ld + (ok ? gr : 0)
-                              : (int64_t)(ok ? gr : 0) * ld + (ok ? gk : 0);
-    const float x = X[off];
-    v[u] = ok ? x : 0.f;
-  }
-}
+// Per-thread staging of one operand: 8 elements of every k tile of op(X),
+// at fixed (row, k) offsets inside the tile, so the 64-bit addresses are
+// formed once per kernel and advanced by a constant per k tile:
+//   not transposed (X stored [rows][ld], k contiguous): k = tid & 15,
+//     rows (tid >> 4) + 16 u  -> 16 consecutive threads read 64 B of a row;
+//   transposed (X stored [K][ld], row contiguous): row = tid & 127,
+//     k = (tid >> 7) + 2 u   -> 128 consecutive threads read 512 B.
+struct Stager {
+  const float* p[8];
+  int64_t step;   // pointer advance per k tile
+  int rlim[8];    // row valid (not transposed) / k offset in the tile (transposed)
+  int kk;         // this thread's k offset in the tile (not transposed)
+  bool rok;       // row valid (transposed)
+  int trans;
 
-__device__ __forceinline__ void stash(float* S, int trans, const float (&v)[8]) {
+  __device__ __forceinline__ void init(const float* X, int64_t ld, int tr, int rows, int r0) {
+    trans = tr;
+    const int t = threadIdx.x;
+    if (!tr) {
+      kk = t & (GK - 1);
 #pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    const int e = threadIdx.x + GTHR * u;
-    int r, k;
-    if (trans) {
-      r = e & (GT - 1);
-      k = e >> 7;
+      for (int u = 0; u < 8; ++u) {
+        const int r = r0 + (t >> 4) + 16 * u;
+        rlim[u] = r < rows;
+        p[u] = X + (int64_t)(r < rows ? r : 0) * ld + kk;
+      }
+      step = GK;
     } else {
-      r = e >> 4;
-      k = e & (GK - 1);
+      const int r = r0 + (t & (GT - 1));
+      rok = r < rows;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        rlim[u] = (t >> 7) + 2 * u;
+        p[u] = X + (int64_t)rlim[u] * ld + (rok ? r : 0);
+      }
+      step = (int64_t)GK * ld;
     }
-    S[k * GLD + r] = v[u];
   }
-}
+
+  // load the k tile at k0 (elements past K read as zero)
+  __device__ __forceinline__ void fetch(int k0, int K, float (&v)[8]) const {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const bool ok = trans ? (rok && k0 + rlim[u] < K) : (rlim[u] && k0 + kk < K);
+      const float x = ok ? *p[u] : 0.f;
+      v[u] = x;
+    }
+  }
+
+  __device__ __forceinline__ void advance() {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) p[u] += step;
+  }
+
+  __device__ __forceinline__ void stash(float* S, const float (&v)[8]) const {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (!trans) S[kk * GLD + (t >> 4) + 16 * u] = v[u];
+      else S[((t >> 7) + 2 * u) * GLD + (t & (GT - 1))] = v[u];
+    }
+  }
+};
 
 __global__ void __launch_bounds__(GTHR) gemm_f32_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) float As[2][GK * GLD];
@@ -110,18 +134,23 @@ __global__ void __launch_bounds__(GTHR) gemm_f32_kernel(GemmArgs g) {
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
   const int nk = (Kc + GK - 1) / GK;
+  Stager sa, sb;
+  sa.init(A, g.lda, g.ta, g.M, m0);
+  sb.init(B, g.ldb, !g.tb, g.N, n0);  // op(B)[k][n]: "rows" are n
   float va[8], vb[8];
-  fetch(A, g.lda, g.ta, g.M, Kc, m0, 0, va);
-  fetch(B, g.ldb, !g.tb, g.N, Kc, n0, 0, vb);  // B[k][n] = row-major [K][N] is "transposed" rows=n
-  stash(As[0], g.ta, va);
-  stash(Bs[0], !g.tb, vb);
+  sa.fetch(0, Kc, va);
+  sb.fetch(0, Kc, vb);
+  sa.stash(As[0], va);
+  sb.stash(Bs[0], vb);
   __syncthreads();
   for (int t = 0; t < nk; ++t) {
     const int cur = t & 1;
     const bool more = t + 1 < nk;
     if (more) {
-      fetch(A, g.lda, g.ta, g.M, Kc, m0, (t + 1) * GK, va);
-      fetch(B, g.ldb, !g.tb, g.N, Kc, n0, (t + 1) * GK, vb);
+      sa.advance();
+      sb.advance();
+      sa.fetch((t + 1) * GK, Kc, va);
+      sb.fetch((t + 1) * GK, Kc, vb);
     }
     const float* as = As[cur];
     const float* bs = Bs[cur];
@@ -137,8 +166,8 @@ __global__ void __launch_bounds__(GTHR) gemm_f32_kernel(GemmArgs g) {
       acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
     }
     if (more) {
-      stash(As[cur ^ 1], g.ta, va);
-      stash(Bs[cur ^ 1], !g.tb, vb);
+      sa.stash(As[cur ^ 1], va);
+      sb.stash(Bs[cur ^ 1], vb);
     }
     __syncthreads();
   }

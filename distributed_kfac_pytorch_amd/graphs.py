@@ -51,6 +51,32 @@ any new model the same way (they poison the free global pool between
 replays).  Every step -- eager or replayed -- runs on one persistent stream
 (``step_stream()``).
 
+Two safety nets guard every capture (round 5):
+
+* autocast detection: the warmup eager steps record, from a forward
+  pre-hook on the convolutions, whether they run under 16-bit autocast; if
+  so every 1x1 convolution is switched to the GEMM form before anything is
+  captured (``conv_mode`` is only a default);
+* a capture-time self-check (``verify``, ``KFAC_GRAPH_VERIFY``): from one
+  saved state the step runs eagerly twice and is replayed twice -- the
+  second replay after an eager step of the other kind -- and every
+  parameter and gradient must agree per tensor within 10x the eager-vs-eager
+  noise; otherwise the graphs are dropped and the runner stays eager.
+
+Under the bench's tuned MIOpen database (``miopen_db/``) bf16 replays are
+sound: every convolution captured alone replays like its eager twin
+(profiles/r5/conv_replay/), the interleaved twin test passes in a fresh
+process (``tests/test_graphs_refresh_gpu.py``), and the round-4 "16.5 %
+clean-replay spread" is the chaotic amplification of MIOpen's atomic
+backward solvers (two EAGER runs from one state differ by 5-8 % in raw
+gradients under that database: profiles/r5/tuned_db_bisect/).  The one
+unsafe configuration found is ``torch.backends.cudnn.deterministic`` with
+that database: MIOpen then falls back to naive direct kernels and to the CK
+grouped backward-data solver, whose replays accumulate into memory the
+graph never re-zeroes (a lone 3x3 conv's second replay returns twice the
+first, profiles/r5/conv_replay/probe_det_tuned.jsonl, solver names in
+profiles/r5/miopen_det/).
+
 Multi-rank jobs run every step eagerly by default (the K-FAC precondition
 phase is still replayed from ``StepGraphs``).  The K-FAC collectives
 themselves no longer block capture (``AsyncTensor`` has no host callbacks:
