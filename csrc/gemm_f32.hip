@@ -12,27 +12,31 @@
 // v_mfma_f32_32x32x2_f32: exact fp32 products with fp32 accumulation (the
 // accuracy class of a library sgemm; gfx950 has no TF32), so the refresh
 // keeps the float64-parity tests' tolerances.  fp32 MFMA issues at 1/16 of
-// the bf16 rate, so the kernel is matrix-core bound: a 128 x 128 block tile
-// (4 waves in 2 x 2, each 64 x 64 = 2 x 2 MFMA 32 x 32 accumulators), k
-// tiles of 16 staged k-major in LDS ([k][m] / [k][n], 132-float rows, double
-// buffered: the next tile's global loads are in flight during the MFMAs),
-// scalar clamped global loads (any shape, any leading dimension, no
-// alignment requirement).  Grid (n tiles, m tiles, batch); tiles walk n
-// fastest so consecutive blocks share their A row panel in L2.
+// the bf16 rate, so the kernel is matrix-core bound once the loads are
+// hidden: a 128 x 128 block tile (4 waves in 2 x 2, each 64 x 64 = 2 x 2 MFMA
+// 32 x 32 accumulators), k tiles of 32 staged k-major in LDS ([k][m] /
+// [k][n], 132-float rows, double buffered: 64 MFMAs per wave cover the next
+// tile's global loads), 16-B global loads from a wave-uniform base plus
+// 32-bit per-thread offsets (scalar clamped loads at the edges and for
+// unaligned operands: any shape, any leading dimension), two blocks per CU.
+// 1-D XCD-aware tile order (gemm_f32_kernel).
 #include "common.h"
 
 #include <algorithm>
+#include <stdexcept>
 
 namespace kfac {
 
 namespace {
 
 constexpr int GT = 128;       // block tile edge
-constexpr int GK = 16;        // k per LDS tile
-constexpr int GLD = GT + 4;   // LDS row (floats)
+constexpr int GK = 32;        // k per LDS tile
+constexpr int GLD = GT + 4;   // LDS row (floats; 528 B, 16-B aligned rows)
 constexpr int GTHR = 256;
+constexpr int GGM = 8;        // tile rows per group of the tile order
 
 typedef float v16f __attribute__((ext_vector_type(16)));
+typedef float f4v __attribute__((ext_vector_type(4)));
 
 struct GemmArgs {
   const float* A;
@@ -42,85 +46,113 @@ struct GemmArgs {
   int M, N, K;
   float alpha, beta;
   int ta, tb;
-  int splits, kchunk;  // split-K: block z = batch * splits, partials to ws
+  int splits, kchunk;  // split-K: grid y = batch * splits, partials to ws
   float* ws;
+  int tiles_m, tiles_n, per_xcd;
+  int vec_a, vec_b;    // 16-B loads allowed (ld % 4 == 0, aligned base)
 };
 
-// Per-thread staging of one operand: 8 elements of every k tile of op(X),
-// at fixed (row, k) offsets inside the tile, so the 64-bit addresses are
-// formed once per kernel and advanced by a constant per k tile:
-//   not transposed (X stored [rows][ld], k contiguous): k = tid & 15,
-//     rows (tid >> 4) + 16 u  -> 16 consecutive threads read 64 B of a row;
-//   transposed (X stored [K][ld], row contiguous): row = tid & 127,
-//     k = (tid >> 7) + 2 u   -> 128 consecutive threads read 512 B.
-struct Stager {
-  const float* p[8];
-  int64_t step;   // pointer advance per k tile
-  int rlim[8];    // row valid (not transposed) / k offset in the tile (transposed)
-  int kk;         // this thread's k offset in the tile (not transposed)
-  bool rok;       // row valid (transposed)
-  int trans;
+// One operand's k tile: 128 "rows" (m of op(A), n of op(B)) x 32 k, 16
+// floats per thread as 4 x 4 consecutive elements of the stored matrix.
+//   KC (k contiguous, X[row][ld]): thread t loads k 4 (t & 7) .. +3 of rows
+//      (t >> 3) + 32 u          -> 8 threads cover 128 B of a row;
+//   RC (rows contiguous, X[k][ld]): thread t loads rows 4 (t & 31) .. +3 at
+//      k (t >> 5) + 8 u          -> 32 threads cover 512 B of a k row.
+// Offsets are 32-bit from a wave-uniform base that advances by one k tile
+// per step (scalar base + vector offset addressing).  Elements outside the
+// matrix read as zero; the 16-B path is taken per chunk when the whole chunk
+// is inside and the operand is 16-B aligned.
+template <bool RC>
+struct Tile {
+  uint32_t off[4];
+  int r0, k0;       // this thread's first row / k inside the tile
 
-  __device__ __forceinline__ void init(const float* X, int64_t ld, int tr, int rows, int r0) {
-    trans = tr;
+  __device__ __forceinline__ void init(int64_t ld) {
     const int t = threadIdx.x;
-    if (!tr) {
-      kk = t & (GK - 1);
+    if (!RC) {
+      k0 = 4 * (t & 7);
+      r0 = t >> 3;
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int r = r0 + (t >> 4) + 16 * u;
-        rlim[u] = r < rows;
-        p[u] = X + (int64_t)(r < rows ? r : 0) * ld + kk;
-      }
-      step = GK;
+      for (int u = 0; u < 4; ++u) off[u] = (uint32_t)((r0 + 32 * u) * ld + k0);
     } else {
-      const int r = r0 + (t & (GT - 1));
-      rok = r < rows;
+      r0 = 4 * (t & 31);
+      k0 = t >> 5;
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        rlim[u] = (t >> 7) + 2 * u;
-        p[u] = X + (int64_t)rlim[u] * ld + (rok ? r : 0);
+      for (int u = 0; u < 4; ++u) off[u] = (uint32_t)((k0 + 8 * u) * ld + r0);
+    }
+  }
+
+  // rows valid below `rlim` (relative to the tile), k below `klim`
+  __device__ __forceinline__ void fetch(const float* __restrict__ X, int64_t ld, int rlim, int klim,
+                                        bool vec, f4v (&v)[4]) const {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float* p = X + off[u];
+      if (!RC) {
+        const int r = r0 + 32 * u;
+        if (vec && r < rlim && k0 + 4 <= klim) {
+          v[u] = *reinterpret_cast<const f4v*>(p);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[u][e] = (r < rlim && k0 + e < klim) ? p[e] : 0.f;
+        }
+      } else {
+        const int k = k0 + 8 * u;
+        if (vec && k < klim && r0 + 4 <= rlim) {
+          v[u] = *reinterpret_cast<const f4v*>(p);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[u][e] = (k < klim && r0 + e < rlim) ? p[e] : 0.f;
+        }
       }
-      step = (int64_t)GK * ld;
     }
   }
 
-  // load the k tile at k0 (elements past K read as zero)
-  __device__ __forceinline__ void fetch(int k0, int K, float (&v)[8]) const {
+  // LDS image [k][row] (GLD floats per k row)
+  __device__ __forceinline__ void stash(float* S, const f4v (&v)[4]) const {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const bool ok = trans ? (rok && k0 + rlim[u] < K) : (rlim[u] && k0 + kk < K);
-      const float x = ok ? *p[u] : 0.f;
-      v[u] = x;
-    }
-  }
-
-  __device__ __forceinline__ void advance() {
+    for (int u = 0; u < 4; ++u) {
+      if (!RC) {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) p[u] += step;
-  }
-
-  __device__ __forceinline__ void stash(float* S, const float (&v)[8]) const {
-    const int t = threadIdx.x;
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      if (!trans) S[kk * GLD + (t >> 4) + 16 * u] = v[u];
-      else S[((t >> 7) + 2 * u) * GLD + (t & (GT - 1))] = v[u];
+        for (int e = 0; e < 4; ++e) S[(k0 + e) * GLD + r0 + 32 * u] = v[u][e];
+      } else {
+        *reinterpret_cast<f4v*>(S + (k0 + 8 * u) * GLD + r0) = v[u];
+      }
     }
   }
 };
 
+// op(A) rows are m: stored [M][lda] (k contiguous) unless ta; op(B) rows are
+// n: stored [N][ldb] (k contiguous) when tb, else [K][ldb] (n contiguous)
+template <bool A_RC, bool B_RC>
 __global__ void __launch_bounds__(GTHR) gemm_f32_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) float As[2][GK * GLD];
   __shared__ __attribute__((aligned(16))) float Bs[2][GK * GLD];
-  const int n0 = blockIdx.x * GT, m0 = blockIdx.y * GT;
-  const int64_t b = blockIdx.z / g.splits;
-  const int split = blockIdx.z % g.splits;
-  // this block's k range [kb, ke): offset the operands to kb
+  // XCD-aware tile order: the blocks the dispatcher puts on one XCD (every
+  // 8th) take a contiguous run of the tile order, and the order walks groups
+  // of GGM tile rows column by column, so the blocks resident on an XCD at
+  // one time share A row panels and B column panels in that XCD's L2
+  const int bid = blockIdx.x;
+  const int t = (bid & 7) * g.per_xcd + (bid >> 3);
+  if (t >= g.tiles_m * g.tiles_n) return;
+  const int per_group = GGM * g.tiles_n;
+  const int first_m = (t / per_group) * GGM;
+  const int gm = min(g.tiles_m - first_m, GGM);
+  const int in_group = t % per_group;
+  const int m0 = (first_m + in_group % gm) * GT;
+  const int n0 = (in_group / gm) * GT;
+
+  const int64_t b = blockIdx.y / g.splits;
+  const int split = blockIdx.y % g.splits;
+  // this block's k range [kb, kb + Kc)
   const int kb = split * g.kchunk;
   const int Kc = min(g.K - kb, g.kchunk);
-  const float* A = g.A + b * g.sA + (g.ta ? (int64_t)kb * g.lda : (int64_t)kb);
-  const float* B = g.B + b * g.sB + (g.tb ? (int64_t)kb : (int64_t)kb * g.ldb);
+  // tile-origin bases (wave-uniform), advanced by one k tile per step
+  const float* A = g.A + b * g.sA + (A_RC ? (int64_t)kb * g.lda + m0 : (int64_t)m0 * g.lda + kb);
+  const float* B = g.B + b * g.sB + (B_RC ? (int64_t)kb * g.ldb + n0 : (int64_t)n0 * g.ldb + kb);
+  const int64_t stepA = A_RC ? (int64_t)GK * g.lda : GK;
+  const int64_t stepB = B_RC ? (int64_t)GK * g.ldb : GK;
+  const int rlimA = g.M - m0, rlimB = g.N - n0;
   float* C = g.C + b * g.sC;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int wm = (w >> 1) * 64, wn = (w & 1) * 64;
@@ -134,23 +166,26 @@ __global__ void __launch_bounds__(GTHR) gemm_f32_kernel(GemmArgs g) {
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
   const int nk = (Kc + GK - 1) / GK;
-  Stager sa, sb;
-  sa.init(A, g.lda, g.ta, g.M, m0);
-  sb.init(B, g.ldb, !g.tb, g.N, n0);  // op(B)[k][n]: "rows" are n
-  float va[8], vb[8];
-  sa.fetch(0, Kc, va);
-  sb.fetch(0, Kc, vb);
-  sa.stash(As[0], va);
-  sb.stash(Bs[0], vb);
+  Tile<A_RC> ta;
+  Tile<B_RC> tb;
+  ta.init(g.lda);
+  tb.init(g.ldb);
+  const bool va = g.vec_a != 0, vb = g.vec_b != 0;
+  f4v ra[4], rb[4];
+  ta.fetch(A, g.lda, rlimA, Kc, va, ra);
+  tb.fetch(B, g.ldb, rlimB, Kc, vb, rb);
+  ta.stash(As[0], ra);
+  tb.stash(Bs[0], rb);
   __syncthreads();
-  for (int t = 0; t < nk; ++t) {
-    const int cur = t & 1;
-    const bool more = t + 1 < nk;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nk;
     if (more) {
-      sa.advance();
-      sb.advance();
-      sa.fetch((t + 1) * GK, Kc, va);
-      sb.fetch((t + 1) * GK, Kc, vb);
+      A += stepA;
+      B += stepB;
+      const int klim = Kc - (kt + 1) * GK;
+      ta.fetch(A, g.lda, rlimA, klim, va, ra);
+      tb.fetch(B, g.ldb, rlimB, klim, vb, rb);
     }
     const float* as = As[cur];
     const float* bs = Bs[cur];
@@ -166,8 +201,8 @@ __global__ void __launch_bounds__(GTHR) gemm_f32_kernel(GemmArgs g) {
       acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
     }
     if (more) {
-      sa.stash(As[cur ^ 1], va);
-      sb.stash(Bs[cur ^ 1], vb);
+      ta.stash(As[cur ^ 1], ra);
+      tb.stash(Bs[cur ^ 1], rb);
     }
     __syncthreads();
   }
@@ -237,11 +272,25 @@ void gemm_f32_batched(int ta, int tb, int M, int N, int K, float alpha, const fl
   if (ws == nullptr || ws_floats < (int64_t)splits * batch * M * N) splits = 1;
   const int kchunk = splits > 1 ? (int)(ceil_div(ceil_div(K, splits), GK) * GK) : K;
   splits = splits > 1 ? (int)ceil_div(K, kchunk) : 1;
+  const int tm = (int)ceil_div(M, GT), tn = (int)ceil_div(N, GT);
+  const int per_xcd = (int)ceil_div((int64_t)tm * tn, 8);
+  // 32-bit per-thread offsets inside a tile (Tile::init)
+  const int64_t span_a = ta ? (int64_t)GK * lda + GT : (int64_t)GT * lda + GK;
+  const int64_t span_b = tb ? (int64_t)GT * ldb + GK : (int64_t)GK * ldb + GT;
+  if (span_a >= (int64_t(1) << 31) || span_b >= (int64_t(1) << 31))
+    throw std::runtime_error("gemm_f32: operand too large for 32-bit tile offsets");
+  auto aligned = [](const float* p, int64_t ld, int64_t stride) {
+    return (reinterpret_cast<uintptr_t>(p) & 15) == 0 && ld % 4 == 0 && stride % 4 == 0;
+  };
   GemmArgs g{A, B, C, lda, ldb, ldc, sA, sB, sC, M, N, K, alpha, beta, ta, tb,
-             splits, kchunk > 0 ? kchunk : 1, ws};
-  const dim3 grid((unsigned)ceil_div(N, GT), (unsigned)ceil_div(M, GT),
-                  (unsigned)(batch * splits));
-  hipLaunchKernelGGL(gemm_f32_kernel, grid, dim3(GTHR), 0, s, g);
+             splits, kchunk > 0 ? kchunk : 1, ws, tm, tn, per_xcd,
+             aligned(A, lda, sA) ? 1 : 0, aligned(B, ldb, sB) ? 1 : 0};
+  const dim3 grid((unsigned)(8 * per_xcd), (unsigned)(batch * splits));
+  const bool arc = ta != 0, brc = tb == 0;
+  if (!arc && !brc) hipLaunchKernelGGL((gemm_f32_kernel<false, false>), grid, dim3(GTHR), 0, s, g);
+  else if (!arc && brc) hipLaunchKernelGGL((gemm_f32_kernel<false, true>), grid, dim3(GTHR), 0, s, g);
+  else if (arc && !brc) hipLaunchKernelGGL((gemm_f32_kernel<true, false>), grid, dim3(GTHR), 0, s, g);
+  else hipLaunchKernelGGL((gemm_f32_kernel<true, true>), grid, dim3(GTHR), 0, s, g);
   if (splits > 1) {
     const dim3 rg((unsigned)ceil_div((int64_t)M * N, 256), (unsigned)batch);
     hipLaunchKernelGGL(gemm_f32_splitk_reduce, rg, dim3(256), 0, s, g);

@@ -401,6 +401,10 @@ class BaseKFACPreconditioner:
         # inline)
         self._factor_streams: dict[Any, torch.cuda.Stream] = {}
         self._factor_forked: set = set()
+        # per device: event on the factor stream after the latest A-factor
+        # (forward hook) work -- step() waits only for that part when the
+        # G-factor work may finish lazily (_lazy_factor_join)
+        self._factor_a_events: dict[Any, torch.cuda.Event] = {}
         self._factor_inputs: list[tuple[torch.Tensor, int]] = []
         self._factor_stream_off = False
         self._hook_handles: list[Any] = []
@@ -610,11 +614,55 @@ class BaseKFACPreconditioner:
     def _bcast_inv(fn: Callable[..., None], src: int, group: Any) -> None:
         fn(src=src, group=group, bucketed=True)
 
+    def _lazy_factor_join(self) -> bool:
+        """May this ``step()`` leave the G-factor SYRKs of the backward hooks
+        running on the factor stream (``KFAC_FACTOR_JOIN``, default
+        ``lazy``; ``full`` joins every step as before)?
+
+        Nothing in a step that does not refresh the second-order state reads
+        the factors: preconditioning uses the eigenbases (or inverses), the
+        KL clip and the optimizer the gradients.  The G SYRKs read only
+        autograd's output gradients (kept alive for the side stream by
+        ``record_stream``), so they can finish under the preconditioning, the
+        optimizer step and the next forward instead of extending the
+        factor-update step.  The A SYRKs read the layer inputs -- tensors the
+        caller may overwrite in place after the step (the input batch) -- so
+        they are always waited for (``_sync_factor_inputs``).  Every reader of
+        the factors joins first: second-order updates, checkpoints,
+        ``memory_usage``, graph capture.  Single process only: with a process
+        group the buckets / packed chunks still unlaunched at ``step()`` are
+        all-reduced from the compute stream and need the full join."""
+        if os.environ.get('KFAC_FACTOR_JOIN', 'lazy') != 'lazy':
+            return False
+        if self.steps % self.inv_update_steps == 0:
+            return False
+        if not self._update_factors_in_hook or self._accumulation_steps != 1:
+            return False
+        return get_world_size() == 1 and self._graphs is None
+
+    def _sync_factor_inputs(self) -> None:
+        """Partial join: the current stream waits for the A-factor work only
+        (the G SYRKs keep running on the side stream); the inputs' in-place
+        modification check runs as in ``_join_factor_streams``."""
+        for dev in self._factor_forked:
+            ev = self._factor_a_events.get(dev)
+            if ev is not None:
+                torch.cuda.current_stream(dev).wait_event(ev)
+        self._check_factor_inputs()
+
+    def sync_factors(self) -> None:
+        """Order the current stream after every pending factor update (the
+        lazy G-factor SYRKs included)."""
+        self._join_factor_streams()
+
     @torch.no_grad()
     def step(self) -> None:
         """One K-FAC step: call after ``loss.backward()`` (gradients already
         averaged by DDP) and before ``optimizer.step()``."""
-        self._join_factor_streams()
+        if self._lazy_factor_join():
+            self._sync_factor_inputs()
+        else:
+            self._join_factor_streams()
         ordered = list(reversed(list(self._layers.values())))
         if (
             not self._update_factors_in_hook
@@ -967,6 +1015,9 @@ class BaseKFACPreconditioner:
         for dev in self._factor_forked:
             torch.cuda.current_stream(dev).wait_stream(self._factor_streams[dev])
         self._factor_forked = set()
+        self._check_factor_inputs()
+
+    def _check_factor_inputs(self) -> None:
         # the side stream read each layer input / output gradient after the
         # hook returned: if the model modified one in place meanwhile (the
         # hazard the reference's input clone guards against), that factor
@@ -982,7 +1033,8 @@ class BaseKFACPreconditioner:
                 stacklevel=2,
             )
 
-    def _on_factor_stream(self, t: torch.Tensor, fn: Callable[[], None]) -> None:
+    def _on_factor_stream(self, t: torch.Tensor, fn: Callable[[], None],
+                          which: str = 'G') -> None:
         """Run ``fn`` (SYRK + EMA + all-reduce issue of one factor) on the
         side stream after the work that produced ``t``; ``t`` is kept alive
         for the side stream by the caching allocator."""
@@ -993,6 +1045,11 @@ class BaseKFACPreconditioner:
         s.wait_stream(torch.cuda.current_stream(t.device))
         with torch.cuda.stream(s):
             fn()
+        if which == 'A':
+            ev = self._factor_a_events.get(t.device)
+            if ev is None:
+                ev = self._factor_a_events[t.device] = torch.cuda.Event()
+            ev.record(s)
         t.record_stream(s)
         self._factor_inputs.append((t, t._version))
         self._factor_forked.add(t.device)
@@ -1020,7 +1077,7 @@ class BaseKFACPreconditioner:
                 with tracing.phase('factor_a'):
                     layer.save_and_update_a(list(input), alpha=decay)
                 layer.reduce_a_factor(group)
-            self._on_factor_stream(input[0], work)
+            self._on_factor_stream(input[0], work, 'A')
             return
         self._join_factor_streams()
         with tracing.phase('factor_a'):

@@ -118,6 +118,13 @@ def main() -> None:
                  if p.grad is not None and not bool(torch.isfinite(p.grad).all())]
         rec = {'step': i, 'kind': kind, 'replays': A[3].replays, 'bad_params': len(bad_p),
                'bad_grads': len(bad_g), 'first_bad_grads': bad_g[:4]}
+        if B is not None:
+            # the eager twin: is the step itself (not the replay) non-finite?
+            rec['twin_bad_params'] = sum(not bool(torch.isfinite(p).all())
+                                         for p in B[0].parameters())
+            rec['twin_bad_grads'] = [n for n, p in reversed(list(B[0].named_parameters()))
+                                     if p.grad is not None
+                                     and not bool(torch.isfinite(p.grad).all())][:4]
         print(json.dumps(rec), flush=True)
         if (bad_p or bad_g) and first_bad is None:
             first_bad = i
