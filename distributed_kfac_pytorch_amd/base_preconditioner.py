@@ -638,6 +638,8 @@ class BaseKFACPreconditioner:
             return False
         if not self._update_factors_in_hook or self._accumulation_steps != 1:
             return False
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            return False  # a captured step joins every stream it forked
         return get_world_size() == 1 and self._graphs is None
 
     def _sync_factor_inputs(self) -> None:

@@ -76,7 +76,11 @@ that database: MIOpen then falls back to naive direct kernels and to the CK
 grouped backward-data solver, whose replays accumulate into memory the
 graph never re-zeroes (a lone 3x3 conv's second replay returns twice the
 first, profiles/r5/conv_replay/probe_det_tuned.jsonl, solver names in
-profiles/r5/miopen_det/).
+profiles/r5/miopen_det/).  The capture-time check does not catch it (its
+replays from a restored state agree with the eager step; the training
+replays after them go non-finite while an eager twin stays finite:
+profiles/r5/unsafe_det_bisect.log), so 16-bit autocast steps under
+``cudnn.deterministic`` are never captured (``_capturable``).
 
 Multi-rank jobs run every step eagerly by default (the K-FAC precondition
 phase is still replayed from ``StepGraphs``).  The K-FAC collectives
@@ -359,6 +363,19 @@ class GraphedTrainStep:
             p._mini_steps_g = defaultdict(int)
 
     def _capturable(self) -> bool:
+        if self.autocast_dtype is not None and torch.backends.cudnn.deterministic:
+            # 16-bit convolutions with cudnn.deterministic: MIOpen falls back
+            # to its naive direct kernels and to the CK grouped backward-data
+            # solver, whose captured replays accumulate into memory the graph
+            # never re-zeroes (profiles/r5/conv_replay/probe_det_tuned.jsonl).
+            # The capture-time check cannot be relied on here: its replays
+            # from a restored state pass and the training replays after them
+            # go non-finite (profiles/r5/unsafe_det_bisect.log).  Eager only.
+            if self.enabled:
+                logger.warning('16-bit autocast with cudnn.deterministic: step graphs '
+                               'disabled (MIOpen deterministic solvers are not replay-safe)')
+                self.enabled = False
+            return False
         p = self.preconditioner
         if p is None:
             return True
@@ -591,7 +608,11 @@ class GraphedTrainStep:
         self.graphs.clear()
         self.outputs.clear()
         self.grads.clear()
-        _native.flush_table_uploads()
+        # tables built during the failed capture serve the eager steps too;
+        # upload them from the new stream (the old one may still report the
+        # invalidated capture)
+        with torch.cuda.stream(self.stream):
+            _native.flush_table_uploads()
         gc.collect()
 
     # --------------------------------------------------------------- step

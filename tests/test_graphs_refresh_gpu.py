@@ -237,8 +237,11 @@ def test_unsafe_solver_graph_is_refused(cuda) -> None:
     grouped backward-data solver for the 3x3 convolutions, whose replays
     accumulate into memory the graph never re-zeroes (the second replay of
     a lone conv returns twice the first: profiles/r5/conv_replay/).  The
-    runner's capture-time check must catch it and run eagerly (or the
-    replays must stay finite): parameters finite either way."""
+    capture-time check passed such a graph whose training replays then went
+    non-finite while the eager twin stayed finite
+    (profiles/r5/unsafe_det_bisect.log), so the runner refuses to capture
+    16-bit autocast steps under ``cudnn.deterministic``: eager steps, finite
+    parameters."""
     import json
     import os
     import shutil
@@ -257,6 +260,4 @@ def test_unsafe_solver_graph_is_refused(cuda) -> None:
     assert p.returncode == 0 and lines, p.stdout[-3000:] + p.stderr[-3000:]
     out = json.loads(lines[-1][7:])
     assert out['finite'], out
-    ok = out['verify'].get('plain', {}).get('ok')
-    # either the check refused the graph (eager from then on) or it passed
-    assert (ok is False and not out['enabled'] and out['replays'] == 0) or ok, out
+    assert not out['enabled'] and out['replays'] == 0, out
