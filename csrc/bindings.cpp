@@ -1,3 +1,5 @@
+#include <cstdlib>
+#include <string>
 // Python bindings for the MI355X K-FAC kernels (module
 // distributed_kfac_pytorch_amd._C).  This is the only translation unit that
 // includes torch; it validates tensors, picks the current HIP stream and
@@ -125,10 +127,40 @@ void trinv_upper_batched(float* T, int64_t ld, int64_t sT, int n, int batch, flo
 
 namespace {
 // native fp32 MFMA GEMM (csrc/gemm_f32.hip) with its split-K workspace
+// KFAC_GEMM_IMPL=lib: the same GEMM through ATen's batched matmul (hipBLASLt)
+// -- an A/B switch for measurements, not a default
+bool gemm_use_lib() {
+  static const bool lib = [] {
+    const char* e = std::getenv("KFAC_GEMM_IMPL");
+    return e != nullptr && std::string(e) == "lib";
+  }();
+  return lib;
+}
+
 void gemm_native(int ta, int tb, int64_t M, int64_t N, int64_t K, float alpha, const float* A,
                  int64_t lda, int64_t sA, const float* B, int64_t ldb, int64_t sB, float beta,
                  float* C, int64_t ldc, int64_t sC, int64_t batch, hipStream_t s,
                  const at::TensorOptions& opt) {
+  if (gemm_use_lib()) {
+    auto o = opt.dtype(at::kFloat);
+    // ATen launches on the current stream: make it the caller's stream
+    at::hip::HIPStreamGuardMasqueradingAsCUDA sg(
+        at::hip::getStreamFromExternalMasqueradingAsCUDA(s, opt.device().index()));
+    // op(A) [batch, M, K], op(B) [batch, K, N], C [batch, M, N] as strided views
+    at::Tensor a = ta ? at::from_blob(const_cast<float*>(A), {batch, M, K}, {sA, 1, lda}, o)
+                      : at::from_blob(const_cast<float*>(A), {batch, M, K}, {sA, lda, 1}, o);
+    at::Tensor b = tb ? at::from_blob(const_cast<float*>(B), {batch, K, N}, {sB, 1, ldb}, o)
+                      : at::from_blob(const_cast<float*>(B), {batch, K, N}, {sB, ldb, 1}, o);
+    at::Tensor c = at::from_blob(C, {batch, M, N}, {sC, ldc, 1}, o);
+    if (beta == 0.f) {
+      at::Tensor r = at::bmm(a, b);
+      if (alpha != 1.f) r.mul_(alpha);
+      c.copy_(r);
+    } else {
+      c.baddbmm_(a, b, beta, alpha);
+    }
+    return;
+  }
   const int64_t wsf = kfac::gemm_f32_ws_floats((int)M, (int)N, (int)K, (int)batch);
   at::Tensor ws;
   if (wsf > 0) ws = at::empty({wsf}, opt.dtype(at::kFloat));

@@ -27,6 +27,8 @@
 #include "common.h"
 #include "descs.h"
 
+#include <cstdlib>
+
 namespace kfac {
 
 namespace {
@@ -619,7 +621,8 @@ __global__ void __launch_bounds__(NT)
 syrk_kernel(const void* __restrict__ X, int64_t N, int64_t K, int64_t ldx,
             int bias, float* __restrict__ C, int64_t D, int64_t ldc, int packed,
             float alpha, const float* __restrict__ ascale, float beta, int T, int splits,
-            int64_t rows_per_split, int vec_ok, ConvGeom geom, float* __restrict__ ws) {
+            int64_t rows_per_split, int vec_ok, ConvGeom geom, float* __restrict__ ws,
+            int xcd_order) {
   constexpr bool F32 = std::is_same<TIn, float>::value && !SPLIT;
   using LT = typename std::conditional<F32, float, short>::type;
   constexpr int LW = F32 ? LDS_W32 : LDS_W16;
@@ -628,8 +631,22 @@ syrk_kernel(const void* __restrict__ X, int64_t N, int64_t K, int64_t ldx,
   LT* Li = lds;
   LT* Lj = lds + PLANES * BK * LW;
 
-  const int tile = blockIdx.x / splits;
-  const int split = blockIdx.x % splits;
+  // XCD-aware order: the dispatcher deals blocks to the 8 XCDs round robin,
+  // so XCD x runs blocks x, x + 8, ...  Those take a contiguous run of the
+  // (split, tile) order, tiles fastest: the blocks resident on one XCD at a
+  // time are the tiles of the same row range, which read the same X rows --
+  // from that XCD's L2 after the first tile instead of from HBM
+  // (block-per-(tile, split) order left every tile streaming its panels
+  // from HBM: L2 hit 0.32, MFMA busy 12.5 %, profiles/pmc/pmc_syrk_r3.md).
+  const int tiles = T * (T + 1) / 2;
+  const int nblk = tiles * splits;
+  const int per_xcd = (nblk + 7) >> 3;
+  const int vb = xcd_order ? (int)(blockIdx.x & 7) * per_xcd + (int)(blockIdx.x >> 3)
+                           : (int)blockIdx.x;
+  if (vb >= nblk) return;
+  // (xcd_order 0, KFAC_SYRK_XCD_ORDER=0: the round-4 order, tile-major)
+  const int split = xcd_order ? vb / tiles : vb % splits;
+  const int tile = xcd_order ? vb - split * tiles : vb / splits;
   int bi, bj;
   tile_of(tile, T, bi, bj);
   const bool diag = bi == bj;
@@ -942,7 +959,12 @@ void syrk(int in_dtype, const void* x, int64_t N, int64_t K, int64_t ldx,
   if (splits < 1 || ws == nullptr) splits = 1;
   const int64_t rows_per_split =
       splits > 1 ? ceil_div(ceil_div(N, splits), BK) * BK : (N > 0 ? N : 1);
-  const dim3 grid((unsigned)(tiles * splits));
+  static const int xcd = [] {
+    const char* e = std::getenv("KFAC_SYRK_XCD_ORDER");
+    return (e != nullptr && e[0] == '0') ? 0 : 1;
+  }();
+  // padded to a multiple of the 8 XCDs (syrk_kernel's block order)
+  const dim3 grid((unsigned)(8 * ceil_div(tiles * splits, (int64_t)8)));
   ConvGeom g = geom != nullptr ? *geom : ConvGeom{};
   if (geom != nullptr) {
     // bytes the implicit-im2col buffer loads may touch (bf16 elements: the
@@ -958,7 +980,7 @@ void syrk(int in_dtype, const void* x, int64_t N, int64_t K, int64_t ldx,
 #define SYRK_F32(STAGE, SPLIT_)                                                     \
   syrk_kernel<float, STAGE, SPLIT_><<<grid, dim3(NT), 0, s>>>(                      \
       x, N, K, ldx, bias ? 1 : 0, C, D, ldc, packed, alpha, ascale, beta, T, splits, \
-      rows_per_split, vec_ok, g, ws)
+      rows_per_split, vec_ok, g, ws, xcd)
     if (geom != nullptr && g.plane > 0) {
       // pre-split bf16 planes (syrk_split_planes)
       SYRK_F32(PatchPlanes32<2>, true);
@@ -985,15 +1007,15 @@ void syrk(int in_dtype, const void* x, int64_t N, int64_t K, int64_t ldx,
     if (geom != nullptr && fast32)
       syrk_kernel<bf16_t, PatchPlanes32<1>><<<grid, dim3(NT), 0, s>>>(
           x, N, K, ldx, bias ? 1 : 0, C, D, ldc, packed, alpha, ascale, beta, T, splits,
-          rows_per_split, vec_ok, g, ws);
+          rows_per_split, vec_ok, g, ws, xcd);
     else if (geom != nullptr)
       syrk_kernel<bf16_t, PatchStaging<bf16_t>><<<grid, dim3(NT), 0, s>>>(
           x, N, K, ldx, bias ? 1 : 0, C, D, ldc, packed, alpha, ascale, beta, T, splits,
-          rows_per_split, vec_ok, g, ws);
+          rows_per_split, vec_ok, g, ws, xcd);
     else
       syrk_kernel<bf16_t, DenseStaging<bf16_t>><<<grid, dim3(NT), 0, s>>>(
           x, N, K, ldx, bias ? 1 : 0, C, D, ldc, packed, alpha, ascale, beta, T, splits,
-          rows_per_split, vec_ok, g, ws);
+          rows_per_split, vec_ok, g, ws, xcd);
   }
   if (splits > 1) {
     const int T32 = (int)ceil_div(D, 32);
