@@ -432,7 +432,7 @@ split_pad_kernel(const SplitDesc* __restrict__ descs, int n) {
 }
 
 #ifndef GEMM3S_TILE
-#define GEMM3S_TILE 0  // 0: 128x128 (4 waves), 1: 256x128 (8 waves), 2: 256x256 (8 waves)
+#define GEMM3S_TILE 0  // 0: 128x128 (4 waves), 1: 256x128 (8 waves), 2: 256x256 (8 waves), 8: 256x256 (4 waves)
 #endif
 #ifndef GEMM3S_NSTAGE
 #define GEMM3S_NSTAGE 2
@@ -451,6 +451,8 @@ constexpr int TBM = 128, TBN = 128, TWM = 1, TWN = 2;
 constexpr int TBM = 128, TBN = 256, TWM = 2, TWN = 2;
 #elif GEMM3S_TILE == 7
 constexpr int TBM = 128, TBN = 256, TWM = 2, TWN = 4;
+#elif GEMM3S_TILE == 8
+constexpr int TBM = 256, TBN = 256, TWM = 2, TWN = 2;  // 128 x 128 per wave
 #else
 constexpr int TBM = 256, TBN = 256, TWM = 2, TWN = 4;
 #endif

@@ -31,7 +31,15 @@ namespace {
 
 constexpr int GT = 128;       // block tile edge
 constexpr int GK = 32;        // k per LDS tile
-constexpr int GLD = GT + 4;   // LDS row (floats; 528 B, 16-B aligned rows)
+// LDS row strides (floats).  Rows-contiguous operands are stored with 16-B
+// writes: 132 (528-B rows, aligned).  k-contiguous operands are transposed
+// into LDS by 4-B writes (lane t: k 4 (t & 7) + e, row t >> 3): with 132 the
+// 8 k groups of a wave fall on 2 bank groups (PMC: 33 % LDS bank-conflict
+// cycles, profiles/r5/pmc/gemmf32.md); 134 = 6 mod 16 spreads them over all
+// 64 banks.
+constexpr int GLD_RC = GT + 4;
+constexpr int GLD_KC = GT + 6;
+template <bool RC> constexpr int gld() { return RC ? GLD_RC : GLD_KC; }
 constexpr int GTHR = 256;
 constexpr int GGM = 8;        // tile rows per group of the tile order
 
@@ -108,15 +116,15 @@ struct Tile {
     }
   }
 
-  // LDS image [k][row] (GLD floats per k row)
+  // LDS image [k][row] (gld<RC>() floats per k row)
   __device__ __forceinline__ void stash(float* S, const f4v (&v)[4]) const {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (!RC) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) S[(k0 + e) * GLD + r0 + 32 * u] = v[u][e];
+        for (int e = 0; e < 4; ++e) S[(k0 + e) * GLD_KC + r0 + 32 * u] = v[u][e];
       } else {
-        *reinterpret_cast<f4v*>(S + (k0 + 8 * u) * GLD + r0) = v[u];
+        *reinterpret_cast<f4v*>(S + (k0 + 8 * u) * GLD_RC + r0) = v[u];
       }
     }
   }
@@ -126,8 +134,9 @@ struct Tile {
 // n: stored [N][ldb] (k contiguous) when tb, else [K][ldb] (n contiguous)
 template <bool A_RC, bool B_RC>
 __global__ void __launch_bounds__(GTHR) gemm_f32_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) float As[2][GK * GLD];
-  __shared__ __attribute__((aligned(16))) float Bs[2][GK * GLD];
+  constexpr int LA = gld<A_RC>(), LB = gld<B_RC>();
+  __shared__ __attribute__((aligned(16))) float As[2][GK * LA];
+  __shared__ __attribute__((aligned(16))) float Bs[2][GK * LB];
   // XCD-aware tile order: the blocks the dispatcher puts on one XCD (every
   // 8th) take a contiguous run of the tile order, and the order walks groups
   // of GGM tile rows column by column, so the blocks resident on an XCD at
@@ -191,10 +200,10 @@ __global__ void __launch_bounds__(GTHR) gemm_f32_kernel(GemmArgs g) {
     const float* bs = Bs[cur];
 #pragma unroll
     for (int kk = 0; kk < GK; kk += 2) {
-      const float a0 = as[(kk + h) * GLD + wm + r];
-      const float a1 = as[(kk + h) * GLD + wm + 32 + r];
-      const float b0 = bs[(kk + h) * GLD + wn + r];
-      const float b1 = bs[(kk + h) * GLD + wn + 32 + r];
+      const float a0 = as[(kk + h) * LA + wm + r];
+      const float a1 = as[(kk + h) * LA + wm + 32 + r];
+      const float b0 = bs[(kk + h) * LB + wn + r];
+      const float b1 = bs[(kk + h) * LB + wn + 32 + r];
       acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
       acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
       acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);

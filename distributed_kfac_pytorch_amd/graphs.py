@@ -147,7 +147,11 @@ def step_stream(device: torch.device | int | None = None) -> torch.cuda.Stream:
         dev = device.index if device.index is not None else torch.cuda.current_device()
     s = _STEP_STREAMS.get(dev)
     if s is None:
-        s = torch.cuda.Stream(device=dev)
+        # KFAC_STEP_STREAM_PRIORITY (default 0; -1 = high): a high-priority
+        # step stream lets the forward / backward kernels dispatch ahead of
+        # the factor SYRKs of the side stream (priority 0)
+        prio = int(os.environ.get('KFAC_STEP_STREAM_PRIORITY', '0'))
+        s = torch.cuda.Stream(device=dev, priority=prio)
         _STEP_STREAMS[dev] = s
     return s
 
