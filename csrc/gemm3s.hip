@@ -82,6 +82,29 @@ __device__ __forceinline__ int find_tile_layer(const Gemm3sDesc* d, int n, int t
   return lo;
 }
 
+// One 16-B LDS-DMA wave instruction: lane l's 16 bytes at g land at LDS
+// address dst + 16 l.  Issued from inline asm, not the builtin: the builtin
+// tells the compiler the instruction writes LDS, and its wait-count pass
+// then put an `s_waitcnt vmcnt(0)` in front of the first LDS read after it --
+// every k tile waited for the DMA of the NEXT tile before computing the
+// current one (the stage pipeline ran fully serialised; PMC: 28 % MFMA busy,
+// profiles/r5/pmc/g3s.md).  The stages are ordered by the explicit counted
+// waits + barrier at the top of the k loop instead.  m0 (the LDS base) is
+// saved and restored around the instruction.
+__device__ __forceinline__ void lds_dma16(const uint16_t* g, uint16_t* dst) {
+  const uint32_t la = (uint32_t)(uintptr_t)(lvoid_t)dst;
+  uint32_t saved;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(saved)
+      : "v"((uint64_t)(uintptr_t)g), "s"(__builtin_amdgcn_readfirstlane(la))
+      : "memory");
+}
+
 // One 16-B LDS-DMA wave-instruction (1 KiB) of an operand plane of one
 // stage.  k-contig plane [E rows][32 k] (64-B rows): instruction i covers
 // rows 16i..16i+15, chunk c of row r lands at slot c ^ ((r >> 2) & 3).
@@ -103,7 +126,7 @@ __device__ __forceinline__ void stage_instr(const uint16_t* __restrict__ src, in
     const int c = (flat % CPR) ^ ((r & 3) << 2);
     g = src + (int64_t)(k0 + r) * ld + org + c * 8;
   }
-  __builtin_amdgcn_global_load_lds((gvoid_t)g, (lvoid_t)(plane + i * 512), 16, 0, 0);
+  lds_dma16(g, plane + i * 512);
 }
 
 // k-contig fragment: lane l gets X[row = base + (l & 31)][k = 16 kh + 8 (l >> 5) + 0..7]
