@@ -333,6 +333,12 @@ gemm3s_kernel(const Gemm3sDesc* __restrict__ descs, int nlayers, int total_tiles
   __builtin_amdgcn_s_barrier();  // every wave is done with the stage buffers
   float* region = reinterpret_cast<float*>(lds) + w * (32 * WTN);
   const int mw0 = m0 + wr * WTM, nw0 = n0 + wc * WTN;
+  // The eigenvalue scaling (S[m][n], or dG[m] for the denominator
+  // dG[m] dA[n] + damping) of 16 outputs at a time, loaded together at
+  // clamped addresses: 4 memory round trips per wave instead of one per
+  // element (loads inside the per-element bounds branch were each waited
+  // for alone: 64 dependent round trips per tile in the T2 launch).
+  const int kind = d.S != nullptr ? 1 : (d.dg != nullptr ? 2 : 0);
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
 #pragma unroll
@@ -340,7 +346,24 @@ gemm3s_kernel(const Gemm3sDesc* __restrict__ descs, int nlayers, int total_tiles
       const int cl = j * 32 + (l & 31);
       const int n = nw0 + cl;
       const bool nok = n < d.N;
-      const float dan = (d.da != nullptr && nok) ? ((const GLOBAL float*)d.da)[n] : 0.f;
+      const int nc = min(n, d.N - 1);
+      float sc[16];
+      float dan = 0.f;
+      if (kind == 1) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int rl = (e & 3) + 8 * (e >> 2) + 4 * (l >> 5);
+          const int mc = min(mw0 + i * 32 + rl, d.M - 1);
+          sc[e] = ((const GLOBAL float*)d.S)[(int64_t)mc * d.lds + nc];
+        }
+      } else if (kind == 2) {
+        dan = d.da != nullptr ? ((const GLOBAL float*)d.da)[nc] : 0.f;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int rl = (e & 3) + 8 * (e >> 2) + 4 * (l >> 5);
+          sc[e] = ((const GLOBAL float*)d.dg)[min(mw0 + i * 32 + rl, d.M - 1)];
+        }
+      }
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int rl = (e & 3) + 8 * (e >> 2) + 4 * (l >> 5);
@@ -348,10 +371,10 @@ gemm3s_kernel(const Gemm3sDesc* __restrict__ descs, int nlayers, int total_tiles
         float v = acc[i][j][e];
         if (!nok || m >= d.M) {
           v = 0.f;
-        } else if (d.S != nullptr) {
-          v *= ((const GLOBAL float*)d.S)[(int64_t)m * d.lds + n];
-        } else if (d.dg != nullptr) {
-          v = v / (((const GLOBAL float*)d.dg)[m] * dan + d.damping);
+        } else if (kind == 1) {
+          v *= sc[e];
+        } else if (kind == 2) {
+          v = v / (sc[e] * dan + d.damping);
         }
         region[rl * WTN + cl] = v;
       }

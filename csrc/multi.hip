@@ -74,19 +74,48 @@ kl_dot_multi_kernel(const LayerDesc* __restrict__ descs, int nlayers,
   const LayerDesc d = descs[li];
   const int64_t total = d.rows * d.cols;
   const int64_t base = (int64_t)(blockIdx.x - d.block_start) * MT * EPT;
-  double s = 0.0;
+  // every load of the thread first (clamped in-bounds elements, masked in
+  // the sum): one memory round trip, not one per element
+  float pv[EPT], gv[EPT];
+  uint32_t ii[EPT], jj[EPT];
 #pragma unroll
   for (int k = 0; k < EPT; ++k) {
     const int64_t e = base + k * MT + threadIdx.x;
-    if (e < total) {
-      const uint32_t ue = (uint32_t)e, uc = (uint32_t)d.cols;
-      const uint32_t i = ue / uc, j = ue - i * uc;
-      const float pv = load_p(d.p, (int64_t)i * d.ldp + j);
-      const float g = j < d.wcols ? load_any(d.w, (int64_t)i * d.wcols + j, d.wdt)
-                                  : load_any(d.b, i, d.bdt) * d.bscale;
-      s += (double)pv * (double)g;
-    }
+    const uint32_t ue = (uint32_t)(e < total ? e : 0), uc = (uint32_t)d.cols;
+    ii[k] = ue / uc;
+    jj[k] = ue - ii[k] * uc;
+    pv[k] = load_p(d.p, (int64_t)ii[k] * d.ldp + jj[k]);
   }
+  // gradient element (weight column, or the bias column scaled by bscale);
+  // the dtype branch is uniform, outside the element loop
+#define KFAC_G_SRC(k) (jj[k] < (uint32_t)d.wcols ? d.w : d.b)
+#define KFAC_G_IDX(k) (jj[k] < (uint32_t)d.wcols ? (int64_t)ii[k] * d.wcols + jj[k] : (int64_t)ii[k])
+#define KFAC_G_SC(k) (jj[k] < (uint32_t)d.wcols ? 1.f : d.bscale)
+  if ((d.b == nullptr || d.bdt == d.wdt) && d.wdt == kF32) {
+#pragma unroll
+    for (int k = 0; k < EPT; ++k)
+      gv[k] = ((const GLOBAL float*)KFAC_G_SRC(k))[KFAC_G_IDX(k)] * KFAC_G_SC(k);
+  } else if (d.b == nullptr || d.bdt == d.wdt) {
+    unsigned short u[EPT];
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) u[k] = ((const GLOBAL unsigned short*)KFAC_G_SRC(k))[KFAC_G_IDX(k)];
+#pragma unroll
+    for (int k = 0; k < EPT; ++k)
+      gv[k] = (d.wdt == kBF16 ? __uint_as_float((uint32_t)u[k] << 16)
+                              : __half2float(__ushort_as_half(u[k]))) * KFAC_G_SC(k);
+  } else {
+#pragma unroll
+    for (int k = 0; k < EPT; ++k)
+      gv[k] = load_any(KFAC_G_SRC(k), KFAC_G_IDX(k),
+                       jj[k] < (uint32_t)d.wcols ? d.wdt : d.bdt) * KFAC_G_SC(k);
+  }
+#undef KFAC_G_SRC
+#undef KFAC_G_IDX
+#undef KFAC_G_SC
+  double s = 0.0;
+#pragma unroll
+  for (int k = 0; k < EPT; ++k)
+    if (base + k * MT + threadIdx.x < total) s += (double)pv[k] * (double)gv[k];
   s = wave_reduce_sum(s);
   if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
   __syncthreads();
@@ -150,13 +179,22 @@ apply_multi_kernel(const LayerDesc* __restrict__ descs, int nlayers,
   const float sc = scale != nullptr ? scale[0] : 1.f;
   const int64_t total = d.rows * d.cols;
   const int64_t base = (int64_t)(blockIdx.x - d.block_start) * MT * EPT;
+  // loads first (clamped), then the stores
+  float pv[EPT];
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) {
+    const int64_t e = base + k * MT + threadIdx.x;
+    const uint32_t ue = (uint32_t)(e < total ? e : 0), uc = (uint32_t)d.cols;
+    const uint32_t i = ue / uc, j = ue - i * uc;
+    pv[k] = load_p(d.p, (int64_t)i * d.ldp + j);
+  }
 #pragma unroll
   for (int k = 0; k < EPT; ++k) {
     const int64_t e = base + k * MT + threadIdx.x;
     if (e < total) {
       const uint32_t ue = (uint32_t)e, uc = (uint32_t)d.cols;
       const uint32_t i = ue / uc, j = ue - i * uc;
-      const float v = sc * load_p(d.p, (int64_t)i * d.ldp + j);
+      const float v = sc * pv[k];
       if (j < d.wcols) store_any(d.w, (int64_t)i * d.wcols + j, d.wdt, v);
       else store_any(d.b, i, d.bdt, v);
     }

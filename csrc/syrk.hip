@@ -750,10 +750,10 @@ syrk_kernel(const void* __restrict__ X, int64_t N, int64_t K, int64_t ldx,
 #pragma unroll
     for (int nj = 0; nj < 2; ++nj) {
       const int64_t gc = c0j + wc * 64 + nj * 32 + (l & 31);
+      if (splits > 1) {
 #pragma unroll
-      for (int rb = 0; rb < 4; ++rb) {
-        const int64_t gr0 = c0i + wr * 64 + mi * 32 + 8 * rb + 4 * (l >> 5);
-        if (splits > 1) {
+        for (int rb = 0; rb < 4; ++rb) {
+          const int64_t gr0 = c0i + wr * 64 + mi * 32 + 8 * rb + 4 * (l >> 5);
           // partial tile -> workspace slab [tile][split][BM][BM] (plain
           // stores; 32 lanes write 128 contiguous bytes per row)
           float* slab = ws + ((int64_t)tile * splits + split) * (BM * BM);
@@ -766,7 +766,33 @@ syrk_kernel(const void* __restrict__ X, int64_t N, int64_t K, int64_t ldx,
               if (gr0 + e < D) slab[lr * BM + lc] = acc[mi][nj][rb * 4 + e];
             }
           }
-        } else if (packed) {
+        }
+        continue;
+      }
+      // Read-modify-write of C (the EMA): the 16 old values of this
+      // accumulator are loaded together first, at clamped in-bounds
+      // addresses (masked when combined), then combined and stored.  (Loaded
+      // inside the per-element bounds branch, each load was waited for
+      // alone: 64 dependent round trips per lane per tile.)
+      float old[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) old[q] = 0.f;
+      if (beta != 0.f) {
+        const int64_t gcc = gc < D ? gc : D - 1;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int64_t gr = c0i + wr * 64 + mi * 32 + 8 * (q >> 2) + 4 * (l >> 5) + (q & 3);
+          const int64_t grc = gr < D ? gr : D - 1;
+          int64_t idx;
+          if (packed) idx = grc <= gcc ? triu_index(grc, gcc, D) : 0;
+          else idx = grc * ldc + gcc;
+          old[q] = C[idx];
+        }
+      }
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) {
+        const int64_t gr0 = c0i + wr * 64 + mi * 32 + 8 * rb + 4 * (l >> 5);
+        if (packed) {
           // packed upper triangle (the all-reduce wire layout): owned
           // elements only, read-modify-write in place, no mirror
 #pragma unroll
@@ -774,8 +800,7 @@ syrk_kernel(const void* __restrict__ X, int64_t N, int64_t K, int64_t ldx,
             const int64_t gr = gr0 + e;
             if (gr < D && gc < D && gr <= gc) {
               const int64_t pi = triu_index(gr, gc, D);
-              const float old = beta != 0.f ? C[pi] : 0.f;
-              C[pi] = beta * old + alpha * acc[mi][nj][rb * 4 + e];
+              C[pi] = beta * old[rb * 4 + e] + alpha * acc[mi][nj][rb * 4 + e];
             }
           }
         } else if (!diag) {
@@ -784,9 +809,7 @@ syrk_kernel(const void* __restrict__ X, int64_t N, int64_t K, int64_t ldx,
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int64_t gr = gr0 + e;
-            float old = 0.f;
-            if (beta != 0.f && gr < D && gc < D) old = C[gr * ldc + gc];
-            v[e] = beta * old + alpha * acc[mi][nj][rb * 4 + e];
+            v[e] = beta * old[rb * 4 + e] + alpha * acc[mi][nj][rb * 4 + e];
             if (gr < D && gc < D) C[gr * ldc + gc] = v[e];
           }
           if (gc < D) {
@@ -805,8 +828,7 @@ syrk_kernel(const void* __restrict__ X, int64_t N, int64_t K, int64_t ldx,
           for (int e = 0; e < 4; ++e) {
             const int64_t gr = gr0 + e;
             if (gr < D && gc < D && gr <= gc) {
-              const float old = beta != 0.f ? C[gr * ldc + gc] : 0.f;
-              const float v = beta * old + alpha * acc[mi][nj][rb * 4 + e];
+              const float v = beta * old[rb * 4 + e] + alpha * acc[mi][nj][rb * 4 + e];
               C[gr * ldc + gc] = v;
               if (gr != gc) C[gc * ldc + gr] = v;
             }
@@ -876,16 +898,24 @@ splitk_reduce_kernel(float* __restrict__ ws, int splits, int T, int gs, int fina
   }
   const int64_t gr = (int64_t)bi * 32 + r;
   const float a4[4] = {acc.x, acc.y, acc.z, acc.w};
+  // the EMA's old values, loaded together (clamped addresses) before any
+  // store: one memory round trip instead of four dependent ones
+  bool upper[4];
+  int64_t idx[4];
+  float old[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int64_t gc = (int64_t)bj * 32 + c4 + e;
+    upper[e] = gr < D && gc < D && (bi < bj || gr <= gc);
+    idx[e] = upper[e] ? (packed ? triu_index(gr, gc, D) : gr * ldc + gc) : 0;
+    if (beta != 0.f) old[e] = C[idx[e]];
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
     float v = 0.f;
-    const bool upper = gr < D && gc < D && (bi < bj || gr <= gc);
-    if (upper) {
-      const int64_t idx = packed ? triu_index(gr, gc, D) : gr * ldc + gc;
-      const float old = beta != 0.f ? C[idx] : 0.f;
-      v = beta * old + alpha * a4[e];
-      C[idx] = v;
+    if (upper[e]) {
+      v = beta * old[e] + alpha * a4[e];
+      C[idx[e]] = v;
     }
     tile[r][c4 + e] = v;
   }

@@ -787,24 +787,35 @@ __global__ void __launch_bounds__(SY_T) sytrd_syr2k_kernel(
   if (r0 >= n || c0 >= n) return;
   const int mw = q - p;
   __shared__ float Vr[SY_NB][64], Wr[SY_NB][64], Vc[SY_NB][64], Wc[SY_NB][64];
-  for (int t = threadIdx.x; t < SY_NB * 64; t += SY_T) {
+  // every panel load of the thread first, at clamped in-bounds addresses
+  // (masked when stored): one memory round trip.  (Guarded loads inside
+  // the staging loop were waited for one iteration at a time; with the
+  // per-element read-modify-write below that made this a ~36 us kernel of
+  // dependent round trips on the chain's critical path, 4 FMAs of work per
+  // load.)
+  constexpr int ST = SY_NB * 64 / SY_T;  // staging trips per thread
+  float vr[ST], wr[ST], vc[ST], wc[ST];
+#pragma unroll
+  for (int u = 0; u < ST; ++u) {
+    const int t = threadIdx.x + u * SY_T;
     const int j = t >> 6, x = t & 63;
-    float vr = 0.f, wr = 0.f, vc = 0.f, wc = 0.f;
-    if (j < mw) {
-      const int r = r0 + x, c = c0 + x;
-      if (r < n) {
-        vr = (r == p + j + 1) ? 1.f : D.A[(int64_t)(p + j) * n + r];
-        wr = D.Wt[(int64_t)j * n + r];
-      }
-      if (c < n) {
-        vc = (c == p + j + 1) ? 1.f : D.A[(int64_t)(p + j) * n + c];
-        wc = D.Wt[(int64_t)j * n + c];
-      }
-    }
-    Vr[j][x] = vr;
-    Wr[j][x] = wr;
-    Vc[j][x] = vc;
-    Wc[j][x] = wc;
+    const int jj = j < mw ? j : 0;
+    const int r = min(r0 + x, n - 1), c = min(c0 + x, n - 1);
+    vr[u] = D.A[(int64_t)(p + jj) * n + r];
+    wr[u] = D.Wt[(int64_t)jj * n + r];
+    vc[u] = D.A[(int64_t)(p + jj) * n + c];
+    wc[u] = D.Wt[(int64_t)jj * n + c];
+  }
+#pragma unroll
+  for (int u = 0; u < ST; ++u) {
+    const int t = threadIdx.x + u * SY_T;
+    const int j = t >> 6, x = t & 63;
+    const int r = r0 + x, c = c0 + x;
+    const bool live = j < mw;
+    Vr[j][x] = (live && r < n) ? (r == p + j + 1 ? 1.f : vr[u]) : 0.f;
+    Wr[j][x] = (live && r < n) ? wr[u] : 0.f;
+    Vc[j][x] = (live && c < n) ? (c == p + j + 1 ? 1.f : vc[u]) : 0.f;
+    Wc[j][x] = (live && c < n) ? wc[u] : 0.f;
   }
   __syncthreads();
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
@@ -823,6 +834,13 @@ __global__ void __launch_bounds__(SY_T) sytrd_syr2k_kernel(
 #pragma unroll
       for (int b = 0; b < 4; ++b) acc[a][b] += vr[a] * wc[b] + wr[a] * vc[b];
   }
+  // read-modify-write of the 4 x 4 outputs: the old values loaded together
+  float old[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+      old[a][b] = D.A[(int64_t)min(r0 + ty * 4 + a, n - 1) * n + min(c0 + tx + 16 * b, n - 1)];
 #pragma unroll
   for (int a = 0; a < 4; ++a) {
     const int r = r0 + ty * 4 + a;
@@ -830,7 +848,7 @@ __global__ void __launch_bounds__(SY_T) sytrd_syr2k_kernel(
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       const int c = c0 + tx + 16 * b;
-      if (c < n) D.A[(int64_t)r * n + c] -= acc[a][b];
+      if (c < n) D.A[(int64_t)r * n + c] = old[a][b] - acc[a][b];
     }
   }
 }

@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <vector>
 #include "../csrc/gemm3s.hip"
 
@@ -21,6 +22,12 @@ __global__ void fill_kernel(float* p, size_t n, unsigned seed) {
     h ^= h >> 13; h *= 0x5bd1e995u; h ^= h >> 15;
     p[i] = (float)(h & 0xFFFF) / 32768.f - 1.f;
   }
+}
+
+__global__ void ones_kernel(float* p, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x)
+    p[i] = 1.f;
 }
 
 // C[m][n] = sum_k A(m,k) B(k,n); A(m,k) = amc ? XA[k][m] : XA[m][k]
@@ -106,6 +113,15 @@ int main(int argc, char** argv) {
       d.a_plane = pa; d.b_plane = pb; d.c_plane = osplit ? cpl : 0;
       d.lda = r128(ac); d.ldb = r128(bc); d.ldc = cld;
       d.M = M; d.N = N; d.K = K;
+      if (getenv("G3S_SCALE") != nullptr) {
+        // the T2 epilogue's eigenvalue scaling, by a matrix of ones (the
+        // check below stays exact)
+        float* S;
+        CK(hipMalloc(&S, sizeof(float) * M * N));
+        ones_kernel<<<1024, 256>>>(S, (size_t)M * N);
+        d.S = S;
+        d.lds = N;
+      }
       d.tiles_n = (N + kfac::TBN - 1) / kfac::TBN;
       d.tile_start = tiles;
       tiles += ((M + kfac::TBM - 1) / kfac::TBM) * d.tiles_n;

@@ -7,8 +7,14 @@ set -o pipefail
 for t in "$@"; do
   for set in resnet neox; do
     for cfg in "0 1 1 a" "1 1 1 g" "0 1 1 g" "0 0 0 a"; do
-      echo -n "{\"tile\": \"$t\", \"set\": \"$set\", \"cfg\": \"$cfg\", \"out\": "
-      timeout -k 5 60 tools/bin/g3s_t$t $set $cfg | tail -1 | tr -d '\n'
+      # T2 (1 1 1 g) with its eigenvalue-scaling epilogue (G3S_SCALE)
+      scale=0; [ "$cfg" = "1 1 1 g" ] && scale=1
+      echo -n "{\"tile\": \"$t\", \"set\": \"$set\", \"cfg\": \"$cfg\", \"scale\": $scale, \"out\": "
+      if [ $scale = 1 ]; then
+        G3S_SCALE=1 timeout -k 5 60 tools/bin/g3s_t$t $set $cfg | tail -1 | tr -d '\n'
+      else
+        timeout -k 5 60 tools/bin/g3s_t$t $set $cfg | tail -1 | tr -d '\n'
+      fi
       echo "}"
     done
   done
