@@ -34,9 +34,9 @@
 // LDS-DMA writes lane-linear, so the swizzle is applied to the SOURCE address
 // of each lane and the same involution to the read address.
 //
-// Tiling: 128x128 output tile per 256-thread block (4 waves 2x2, 64x64 each
-// = 2x2 MFMA 32x32x16 accumulators), BK = 32, two LDS stages (64 KiB), two
-// blocks per CU.  XCD-aware chunked tile order and per-layer grouped tile
+// Tiling (GEMM3S_TILE below): 256x256 output tile per 512-thread block
+// (8 waves 2x4, 128x64 each = 4x2 MFMA 32x32x16 accumulators), BK = 32, two
+// LDS stages (128 KiB), one block per CU.  XCD-aware chunked tile order and per-layer grouped tile
 // rows as v1.  Epilogues: eigenvalue scaling (S = dGdA, or 1/(dG dA^T +
 // damping)), then either fp32 (the preconditioned gradient P) or the split
 // image of the result (the next GEMM's operand).
@@ -477,8 +477,13 @@ split_pad_kernel(const SplitDesc* __restrict__ descs, int n) {
   *(GLOBAL u4*)(dst + d.plane) = ll;
 }
 
+// Block tile: 2 (256 x 256, 8 waves of 128 x 64, one block per CU) since
+// round 5: with the serialised DMA wait and epilogue loads gone, the four
+// launches of a step take 1.37 ms (ResNet-50) / 4.62 ms (GPT-NeoX-125M)
+// against 1.41 / 5.01 ms with 128 x 128 tiles and 1.69 / 6.21 ms with three
+// 128 x 128 stages (profiles/r5/g3s_sweep_epilogue.jsonl).
 #ifndef GEMM3S_TILE
-#define GEMM3S_TILE 0  // 0: 128x128 (4 waves), 1: 256x128 (8 waves), 2: 256x256 (8 waves), 8: 256x256 (4 waves)
+#define GEMM3S_TILE 2  // 0: 128x128 (4 waves), 1: 256x128 (8 waves), 2: 256x256 (8 waves), 8: 256x256 (4 waves)
 #endif
 #ifndef GEMM3S_NSTAGE
 #define GEMM3S_NSTAGE 2
