@@ -70,6 +70,35 @@ __device__ __forceinline__ void store8(float* p, const float* v) {
   *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
 }
 
+// Raw 8-channel loads: the guarded load loops of the kernels below issue
+// only these (no conversion inside the bounds branch), and convert in a
+// separate pass.  With the bf16 -> fp32 conversion inside the branch the
+// compiler waited for each row's load before issuing the next row's
+// (12 `s_waitcnt vmcnt(0)` for 14 loads in the bf16 apply kernel: one
+// memory round trip per row instead of one per loop iteration).
+template <typename E> struct Raw8 { uint4 w; };
+template <> struct Raw8<float> { float4 a, b; };
+
+__device__ __forceinline__ void ldraw8(const uint16_t* p, Raw8<uint16_t>& r) {
+  r.w = *reinterpret_cast<const uint4*>(p);
+}
+__device__ __forceinline__ void ldraw8(const float* p, Raw8<float>& r) {
+  r.a = *reinterpret_cast<const float4*>(p);
+  r.b = *reinterpret_cast<const float4*>(p + 4);
+}
+__device__ __forceinline__ void cvt8(const Raw8<uint16_t>& r, float* v) {
+  const uint32_t w[4] = {r.w.x, r.w.y, r.w.z, r.w.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(w[i] << 16);
+    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ void cvt8(const Raw8<float>& r, float* v) {
+  v[0] = r.a.x; v[1] = r.a.y; v[2] = r.a.z; v[3] = r.a.w;
+  v[4] = r.b.x; v[5] = r.b.y; v[6] = r.b.z; v[7] = r.b.w;
+}
+
 // Per-block channel partial sums.  mode 0 (forward): s0 = sum x,
 // s1 = sum x^2.  mode 1 (backward): dz = dy * (y > 0 | !relu),
 // s0 = sum dz, s1 = sum dz * (x - mean).
@@ -98,18 +127,33 @@ __global__ void __launch_bounds__(BN_T) bn_partial_kernel(
     constexpr int U = MODE == 0 ? 8 : 4;
     for (int64_t rb = r0 + rs; rb < r1; rb += U * (int64_t)rpi) {
       float a[U][8], g[U][8], o[U][8];
+      Raw8<E> ra[U], rg[U], ro[U];
       bool ok[U];
+      int64_t offs[U];
+      // unguarded loads at clamped rows (ok[] masks the sums): guards around
+      // the loads made the compiler wait for each row before the next
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t r = rb + (int64_t)u * rpi;
         ok[u] = r < r1;
-        if (ok[u]) {
-          const int64_t off = r * C + c0;
-          load8(x + off, a[u]);
-          if (MODE == 1) {
-            load8(dy + off, g[u]);
-            if (relu) load8(y + off, o[u]);
-          }
+        offs[u] = (ok[u] ? r : r1 - 1) * C + c0;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        ldraw8(x + offs[u], ra[u]);
+        if (MODE == 1) ldraw8(dy + offs[u], rg[u]);
+      }
+      if (MODE == 1 && relu) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) ldraw8(y + offs[u], ro[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (!ok[u]) continue;
+        cvt8(ra[u], a[u]);
+        if (MODE == 1) {
+          cvt8(rg[u], g[u]);
+          if (relu) cvt8(ro[u], o[u]);
         }
       }
 #pragma unroll
@@ -244,13 +288,27 @@ __global__ void __launch_bounds__(BN_T) bn_fwd_apply_kernel(
   const int64_t step = (int64_t)gridDim.x * 4 * rpi;
   for (int64_t rb = (int64_t)blockIdx.x * 4 * rpi + rs; rb < M; rb += step) {
     float a[4][8], r[4][8];
+    Raw8<E> ra[4], rr[4];
+    // unguarded loads at clamped rows (masked at the store): per-row
+    // guards around the loads made the compiler wait for each row's data
+    // before issuing the next row's loads
+    int64_t offs[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int64_t row = rb + (int64_t)u * rpi;
-      if (row < M) {
-        load8(x + row * C + c0, a[u]);
-        if (res) load8(res + row * C + c0, r[u]);
-      }
+      offs[u] = (row < M ? row : M - 1) * C + c0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) ldraw8(x + offs[u], ra[u]);
+    if (res) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) ldraw8(res + offs[u], rr[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (rb + (int64_t)u * rpi >= M) continue;
+      cvt8(ra[u], a[u]);
+      if (res) cvt8(rr[u], r[u]);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -308,15 +366,29 @@ __global__ void __launch_bounds__(BN_T) bn_bwd_apply_kernel(
   const int64_t step = (int64_t)gridDim.x * 4 * rpi;
   for (int64_t rb = (int64_t)blockIdx.x * 4 * rpi + rs; rb < M; rb += step) {
     float a[4][8], g[4][8], o[4][8];
+    Raw8<E> ra[4], rg[4], ro[4];
+    // unguarded loads at clamped rows (masked at the store), as forward
+    int64_t offs[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int64_t row = rb + (int64_t)u * rpi;
-      if (row < M) {
-        const int64_t off = row * C + c0;
-        load8(x + off, a[u]);
-        load8(dy + off, g[u]);
-        if (relu) load8(y + off, o[u]);
-      }
+      offs[u] = (row < M ? row : M - 1) * C + c0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      ldraw8(x + offs[u], ra[u]);
+      ldraw8(dy + offs[u], rg[u]);
+    }
+    if (relu) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) ldraw8(y + offs[u], ro[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (rb + (int64_t)u * rpi >= M) continue;
+      cvt8(ra[u], a[u]);
+      cvt8(rg[u], g[u]);
+      if (relu) cvt8(ro[u], o[u]);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -367,18 +439,33 @@ __global__ void __launch_bounds__(BN_T) bn_partial_sliced_kernel(
   constexpr int U = 4;
   for (int64_t rb = r0 + rt; rb < r1; rb += U * (int64_t)RT) {
     float a[U][8], g[U][8], o[U][8];
+    Raw8<E> ra[U], rg[U], ro[U];
     bool ok[U];
+    int64_t offs[U];
+    // unguarded loads at clamped rows (ok[] masks the sums): guards around
+    // the loads made the compiler wait for each row before the next
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t r = rb + (int64_t)u * RT;
       ok[u] = r < r1;
-      if (ok[u]) {
-        const int64_t off = r * C + c0;
-        load8(x + off, a[u]);
-        if (MODE == 1) {
-          load8(dy + off, g[u]);
-          if (relu) load8(y + off, o[u]);
-        }
+      offs[u] = (ok[u] ? r : r1 - 1) * C + c0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      ldraw8(x + offs[u], ra[u]);
+      if (MODE == 1) ldraw8(dy + offs[u], rg[u]);
+    }
+    if (MODE == 1 && relu) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) ldraw8(y + offs[u], ro[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (!ok[u]) continue;
+      cvt8(ra[u], a[u]);
+      if (MODE == 1) {
+        cvt8(rg[u], g[u]);
+        if (relu) cvt8(ro[u], o[u]);
       }
     }
 #pragma unroll
@@ -494,13 +581,27 @@ __global__ void __launch_bounds__(BN_T) bn_fwd_apply_sliced_kernel(
   const int64_t r1 = r0 + rows_per_chunk < M ? r0 + rows_per_chunk : M;
   for (int64_t rb = r0 + rt; rb < r1; rb += 4 * (int64_t)RT) {
     float a[4][8], r[4][8];
+    Raw8<E> ra[4], rr[4];
+    // unguarded loads at clamped rows (masked at the store): per-row
+    // guards around the loads made the compiler wait for each row's data
+    // before issuing the next row's loads
+    int64_t offs[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int64_t row = rb + (int64_t)u * RT;
-      if (row < r1) {
-        load8(x + row * C + c0, a[u]);
-        if (res) load8(res + row * C + c0, r[u]);
-      }
+      offs[u] = (row < r1 ? row : r1 - 1) * C + c0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) ldraw8(x + offs[u], ra[u]);
+    if (res) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) ldraw8(res + offs[u], rr[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (rb + (int64_t)u * RT >= r1) continue;
+      cvt8(ra[u], a[u]);
+      if (res) cvt8(rr[u], r[u]);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -562,15 +663,29 @@ __global__ void __launch_bounds__(BN_T) bn_bwd_apply_sliced_kernel(
   const int64_t r1 = r0 + rows_per_chunk < M ? r0 + rows_per_chunk : M;
   for (int64_t rb = r0 + rt; rb < r1; rb += 4 * (int64_t)RT) {
     float a[4][8], g[4][8], o[4][8];
+    Raw8<E> ra[4], rg[4], ro[4];
+    // unguarded loads at clamped rows (masked at the store), as forward
+    int64_t offs[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int64_t row = rb + (int64_t)u * RT;
-      if (row < r1) {
-        const int64_t off = row * C + c0;
-        load8(x + off, a[u]);
-        load8(dy + off, g[u]);
-        if (relu) load8(y + off, o[u]);
-      }
+      offs[u] = (row < r1 ? row : r1 - 1) * C + c0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      ldraw8(x + offs[u], ra[u]);
+      ldraw8(dy + offs[u], rg[u]);
+    }
+    if (relu) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) ldraw8(y + offs[u], ro[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (rb + (int64_t)u * RT >= r1) continue;
+      cvt8(ra[u], a[u]);
+      cvt8(rg[u], g[u]);
+      if (relu) cvt8(ro[u], o[u]);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {

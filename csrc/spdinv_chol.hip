@@ -148,11 +148,19 @@ __global__ void __launch_bounds__(CT) chol_update(CholArgs a) {
   const v16f c = tile::mm64(At, Bt, wi, wj);
   float* Mij = tile_at(a.M, mat, N, i, j);
   const int l = threadIdx.x & 63;
+  // old values loaded together before any store (a store may alias the
+  // next load as far as the compiler knows: one round trip per element)
+  float old[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int row = wi * 32 + (e & 3) + 8 * (e >> 2) + 4 * (l >> 5);
+    old[e] = Mij[(int64_t)row * N + wj * 32 + (l & 31)];
+  }
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
     const int row = wi * 32 + (e & 3) + 8 * (e >> 2) + 4 * (l >> 5);
     const int col = wj * 32 + (l & 31);
-    Mij[(int64_t)row * N + col] -= c[e];
+    Mij[(int64_t)row * N + col] = old[e] - c[e];
   }
 }
 
@@ -189,11 +197,17 @@ __global__ void __launch_bounds__(CT) tri_update(CholArgs a) {
   const v16f o = tile::mm64(At, Bt, wi, wj);
   float* Ric = tile_at(a.W, mat, N, i, c);
   const int l = threadIdx.x & 63;
+  float old[16];  // (loads before stores, as chol_update)
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int row = wi * 32 + (e & 3) + 8 * (e >> 2) + 4 * (l >> 5);
+    old[e] = Ric[(int64_t)row * N + wj * 32 + (l & 31)];
+  }
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
     const int row = wi * 32 + (e & 3) + 8 * (e >> 2) + 4 * (l >> 5);
     const int col = wj * 32 + (l & 31);
-    Ric[(int64_t)row * N + col] -= o[e];
+    Ric[(int64_t)row * N + col] = old[e] - o[e];
   }
 }
 
