@@ -938,7 +938,14 @@ splitk_reduce_kernel(float* __restrict__ ws, int splits, int T, int gs, int fina
 int64_t syrk_workspace_splits(int64_t N, int64_t D) {
   const int64_t T = ceil_div(D, BM);
   const int64_t tiles = T * (T + 1) / 2;
-  const int64_t target_blocks = 768;
+  // KFAC_SYRK_TARGET_BLOCKS (default 768 = 3 per CU): the factor SYRKs run
+  // beside backward on the factor stream, so fewer blocks trade their own
+  // latency for less contention (A/B knob)
+  static const int64_t target_blocks = [] {
+    const char* e = std::getenv("KFAC_SYRK_TARGET_BLOCKS");
+    const long v = e != nullptr ? std::atol(e) : 0;
+    return (int64_t)(v > 0 ? v : 768);
+  }();
   int64_t splits = ceil_div(target_blocks, tiles);
   const int64_t max_by_rows = ceil_div(N, 4 * BK);  // >= 4 k-tiles per split
   if (splits > max_by_rows) splits = max_by_rows;

@@ -293,3 +293,22 @@ def test_log_records(caplog):
 def test_skip_layers():
     p = kfac.KFACPreconditioner(LeNet(), skip_layers=['conv'])
     assert [n for n, _ in p._layers.values()] == ['fc1', 'fc2', 'fc3']
+
+
+def test_lazy_factor_join_decision(monkeypatch):
+    """``step()`` leaves the G-factor SYRKs running only on single-process
+    steps that do not refresh the second-order state
+    (``BaseKFACPreconditioner._lazy_factor_join``; GPU behaviour in
+    tests/test_factor_lazy_join_gpu.py)."""
+    model = TinyModel()
+    pre = kfac.KFACPreconditioner(model, factor_update_steps=2, inv_update_steps=4)
+    monkeypatch.delenv('KFAC_FACTOR_JOIN', raising=False)
+    pre._steps = 0  # inverse step: full join
+    assert not pre._lazy_factor_join()
+    pre._steps = 2  # factor step, no refresh
+    assert pre._lazy_factor_join()
+    monkeypatch.setenv('KFAC_FACTOR_JOIN', 'full')
+    assert not pre._lazy_factor_join()
+    monkeypatch.setenv('KFAC_FACTOR_JOIN', 'lazy')
+    pre._accumulation_steps = 2
+    assert not pre._lazy_factor_join()
