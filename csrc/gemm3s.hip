@@ -431,7 +431,6 @@ gemm3s_kernel(const Gemm3sDesc* __restrict__ descs, int nlayers, int total_tiles
 // columns of one row.  The padding of the image (columns >= cols (+1), rows
 // >= rows) is never written: images are zero-filled once at allocation.
 constexpr int SPT = 256;
-constexpr int SQ = 4;  // quads per thread (split_pad_kernel)
 
 __device__ __forceinline__ int find_split(const SplitDesc* d, int n, int64_t blk) {
   int lo = 0, hi = n - 1;
@@ -445,51 +444,37 @@ __device__ __forceinline__ int find_split(const SplitDesc* d, int n, int64_t blk
 
 __global__ void __launch_bounds__(SPT)
 split_pad_kernel(const SplitDesc* __restrict__ descs, int n) {
-  // SQ quads per thread: the layer lookup (a chain of dependent scalar
-  // loads) is paid once per 4 * SQ * SPT elements, and every load of the
-  // thread is issued before the first convert
   const SplitDesc d = descs[find_split(descs, n, blockIdx.x)];
+  const int64_t q = (int64_t)(blockIdx.x - d.block_start) * SPT + threadIdx.x;
   const int total_cols = d.cols + (d.extra != nullptr ? 1 : 0);
   const int qpr = (total_cols + 3) >> 2;  // quads per row
-  const int64_t q0 = (int64_t)(blockIdx.x - d.block_start) * SPT * SQ + threadIdx.x;
-  float v[SQ][4];
+  const int64_t r = q / qpr;
+  if (r >= d.rows) return;
+  const int c0 = (int)(q - r * qpr) * 4;
+  const GLOBAL float* row = (const GLOBAL float*)d.src + r * d.lds;
+  float v[4];
+  if (d.vec && c0 + 4 <= d.cols) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    const f4 x = *(const GLOBAL f4*)(row + c0);
+    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+  } else {
 #pragma unroll
-  for (int u = 0; u < SQ; ++u) {
-    const int64_t q = q0 + (int64_t)u * SPT;
-    const int64_t r = q / qpr;
-    const int c0 = (int)(q - r * qpr) * 4;
-    const int64_t rc = r < d.rows ? r : d.rows - 1;
-    const GLOBAL float* row = (const GLOBAL float*)d.src + rc * d.lds;
-    if (d.vec && c0 + 4 <= d.cols) {
-      typedef float f4 __attribute__((ext_vector_type(4)));
-      const f4 x = *(const GLOBAL f4*)(row + c0);
-      v[u][0] = x.x; v[u][1] = x.y; v[u][2] = x.z; v[u][3] = x.w;
-    } else {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int c = c0 + e;
-        v[u][e] = c < d.cols ? row[c]
-                  : (c == d.cols && d.extra != nullptr ? ((const GLOBAL float*)d.extra)[rc] : 0.f);
-      }
+    for (int e = 0; e < 4; ++e) {
+      const int c = c0 + e;
+      v[e] = c < d.cols ? row[c]
+                        : (c == d.cols && d.extra != nullptr ? ((const GLOBAL float*)d.extra)[r] : 0.f);
     }
   }
+  uint16_t h[4], lo[4];
 #pragma unroll
-  for (int u = 0; u < SQ; ++u) {
-    const int64_t q = q0 + (int64_t)u * SPT;
-    const int64_t r = q / qpr;
-    if (r >= d.rows) break;
-    const int c0 = (int)(q - r * qpr) * 4;
-    uint16_t h[4], lo[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) split1(v[u][e], h[e], lo[e]);
-    GLOBAL uint16_t* dst = (GLOBAL uint16_t*)d.dst + r * d.ldd + c0;
-    // the image row stride is a multiple of 128 elements: 8-B aligned quads
-    typedef unsigned short u4 __attribute__((ext_vector_type(4)));
-    const u4 hh = {h[0], h[1], h[2], h[3]};
-    const u4 ll = {lo[0], lo[1], lo[2], lo[3]};
-    *(GLOBAL u4*)dst = hh;
-    *(GLOBAL u4*)(dst + d.plane) = ll;
-  }
+  for (int e = 0; e < 4; ++e) split1(v[e], h[e], lo[e]);
+  GLOBAL uint16_t* dst = (GLOBAL uint16_t*)d.dst + r * d.ldd + c0;
+  // the image row stride is a multiple of 128 elements: 8-B aligned quads
+  typedef unsigned short u4 __attribute__((ext_vector_type(4)));
+  const u4 hh = {h[0], h[1], h[2], h[3]};
+  const u4 ll = {lo[0], lo[1], lo[2], lo[3]};
+  *(GLOBAL u4*)dst = hh;
+  *(GLOBAL u4*)(dst + d.plane) = ll;
 }
 
 // Block tile: 2 (256 x 256, 8 waves of 128 x 64, one block per CU) since
@@ -538,7 +523,7 @@ int gemm3s_grid(int total_tiles) {
 }
 
 int64_t split_blocks_for(int64_t rows, int64_t total_cols) {
-  return ceil_div(rows * ceil_div(total_cols, 4), (int64_t)SPT * SQ);
+  return ceil_div(rows * ceil_div(total_cols, 4), (int64_t)SPT);
 }
 
 void gemm3s_grouped(const Gemm3sDesc* table, int nlayers, int total_tiles, bool a_mc,
