@@ -933,18 +933,20 @@ splitk_reduce_kernel(float* __restrict__ ws, int splits, int T, int gs, int fina
 }  // namespace
 
 // Row splits for one SYRK.  Only shapes whose upper-triangle tile count
-// cannot fill the chip are split (target ~768 blocks = 3 per CU), and the
-// fp32 partial-tile workspace is capped at 32 MB.
+// cannot fill the chip are split (target ~128 blocks), and the fp32
+// partial-tile workspace is capped at 32 MB.
 int64_t syrk_workspace_splits(int64_t N, int64_t D) {
   const int64_t T = ceil_div(D, BM);
   const int64_t tiles = T * (T + 1) / 2;
-  // KFAC_SYRK_TARGET_BLOCKS (default 768 = 3 per CU): the factor SYRKs run
-  // beside backward on the factor stream, so fewer blocks trade their own
-  // latency for less contention (A/B knob)
+  // KFAC_SYRK_TARGET_BLOCKS (default 128): the factor SYRKs run beside
+  // backward on the factor stream, where fewer, longer blocks cost the
+  // overlapped step less than filling the chip does.  ResNet-50 bench
+  // factor step: 768 -> 22.7 ms, 256 -> 21.3, 128 -> 20.6-20.7, 96 -> 20.9,
+  // 64 -> 24.1 (profiles/r5/syrk_target_ab/)
   static const int64_t target_blocks = [] {
     const char* e = std::getenv("KFAC_SYRK_TARGET_BLOCKS");
     const long v = e != nullptr ? std::atol(e) : 0;
-    return (int64_t)(v > 0 ? v : 768);
+    return (int64_t)(v > 0 ? v : 128);
   }();
   int64_t splits = ceil_div(target_blocks, tiles);
   const int64_t max_by_rows = ceil_div(N, 4 * BK);  // >= 4 k-tiles per split

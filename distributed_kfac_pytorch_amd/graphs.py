@@ -61,7 +61,8 @@ Two safety nets guard every capture (round 5):
   saved state the step runs eagerly twice and is replayed three times -- the
   second replay after an eager step of the other kind, the third straight
   after it -- and every parameter and gradient must agree per tensor within
-  10x the eager-vs-eager noise (capped at 25 %); otherwise the graphs are
+  10x the eager-vs-eager noise (capped at 25 %, floored at the step's
+  largest eager noise: ``verify_tolerance``); otherwise the graphs are
   dropped and the runner stays eager.
 
 Under the bench's tuned MIOpen database (``miopen_db/``) bf16 replays are
@@ -154,6 +155,29 @@ def step_stream(device: torch.device | int | None = None) -> torch.cuda.Stream:
         s = torch.cuda.Stream(device=dev, priority=prio)
         _STEP_STREAMS[dev] = s
     return s
+
+
+def verify_tolerance(noise: torch.Tensor) -> torch.Tensor:
+    """Per-tensor tolerance of the capture-time check from the eager-vs-eager
+    relative distances ``noise`` (one entry per parameter / gradient).
+
+    ``min(10 x n, max(2 x n, 0.25))`` of the tensor's own noise ``n`` -- a
+    replay may be ten times as noisy as one eager pair, but not 25 % off when
+    the eager pair agrees to within 12.5 % -- plus a floor of the step's
+    largest eager noise (itself capped at 25 %) and 1e-3.  The floor: one
+    eager pair under-samples the noise of a tensor fed by atomic reductions
+    (MIOpen's bf16 solvers).  In the ImageNet CLI's bf16 batch-8 steps six
+    eager steps from one state spread by up to 14 % in BatchNorm gradients,
+    six replays by the same 10-15 % around the eager step AND around each
+    other, yet single eager pairs put some of those tensors at 1e-4 and the
+    check dropped sound graphs in half the runs
+    (profiles/r5/graph_verify_probe/).  The hazards the check exists for
+    (memory a graph reads outside its pool, accumulation the graph never
+    re-zeroes) move a gradient by O(1) or make it non-finite; a deterministic
+    fp32 step keeps a floor of ~1e-3.  A non-finite noise entry makes every
+    tolerance NaN (the check fails)."""
+    floor = torch.clamp(noise.max(), max=0.25) if noise.numel() else noise.new_zeros(())
+    return torch.minimum(10.0 * noise, torch.clamp(2.0 * noise, min=0.25)) + floor + 1e-3
 
 
 def _graph_safe(model: torch.nn.Module | None, preconditioner: Any,
@@ -493,8 +517,7 @@ class GraphedTrainStep:
         per tensor; every parameter (relative to its update) and every
         gradient (relative to its norm) of every replay must agree with the
         eager step, and the replays with each other, within
-        ``min(10 x noise, max(2 x noise, 0.25)) + 1e-3`` of that tensor, and be
-        finite.  Per tensor, because a solver
+        ``verify_tolerance`` of that tensor's noise, and be finite.  Per tensor, because a solver
         that corrupts one layer's input gradient (MIOpen's deterministic
         bf16 backward-data under the tuned database accumulates into memory
         the graph never re-zeroes: profiles/r5/conv_replay/) hides in a
@@ -579,28 +602,28 @@ class GraphedTrainStep:
 
         names = [f'param[{i}]' for i in range(len(params))] + [f'grad[{i}]' for i in idx]
         noise = dist(e2, e1)
-        # capped: an eager step whose own noise reaches 10 % for a tensor
-        # (bf16 atomics) must not let a replay that doubles it through; a
-        # tensor that is mostly noise (tiny gradients, small batches) keeps
-        # twice its noise
-        tol = torch.minimum(10.0 * noise, torch.clamp(2.0 * noise, min=0.25)) + 1e-3
-        worst_ratio, worst_at, worst = 0.0, None, 0.0
-        for a, b in ((r1, e1), (r2, e1), (r3, e1), (r2, r1), (r3, r1)):
-            d = dist(a, b)
+        tol = verify_tolerance(noise)
+        worst_ratio, worst_at, worst, worst_pair, worst_noise = 0.0, None, 0.0, None, 0.0
+        runs = {'e1': e1, 'r1': r1, 'r2': r2, 'r3': r3}
+        for pa, pb in (('r1', 'e1'), ('r2', 'e1'), ('r3', 'e1'), ('r2', 'r1'), ('r3', 'r1')):
+            d = dist(runs[pa], runs[pb])
             ratio = torch.where(torch.isfinite(d), d / tol, torch.full_like(d, float('inf')))
             r, i = (float(v) for v in torch.max(ratio, 0))
             if r > worst_ratio or worst_at is None:
                 worst_ratio, worst_at, worst = r, names[int(i)], float(d[int(i)])
+                worst_pair = f'{pa}-{pb}'
+                worst_noise = float(noise[int(i)])
         finite = all(bool(torch.isfinite(t).all()) for r in (r1, r2, r3)
                      for t in list(r[0]) + [g for g in r[1] if g is not None])
         ok = finite and worst_ratio <= 1.0  # NaN compares False
         self.verify_report[kind] = {'noise_max': float(noise.max()), 'worst': worst,
-                                    'worst_tensor': worst_at, 'worst_over_tol': worst_ratio,
+                                    'worst_tensor': worst_at, 'worst_pair': worst_pair,
+                                    'worst_noise': worst_noise, 'worst_over_tol': worst_ratio,
                                     'finite': finite, 'ok': ok}
         if not ok:
-            logger.warning('step graph %r failed its capture-time check (%s differs by %.3g, '
-                           '%.3g x its tolerance; finite %s): graphs dropped, running eagerly',
-                           kind, worst_at, worst, worst_ratio, finite)
+            logger.warning('step graph %r failed its capture-time check (%s differs by %.3g '
+                           'in %s, %.3g x its tolerance; finite %s): graphs dropped, running '
+                           'eagerly', kind, worst_at, worst, worst_pair, worst_ratio, finite)
         return ok
 
     def _drop_graphs(self) -> None:

@@ -79,6 +79,9 @@ def add_runtime_args(p: argparse.ArgumentParser, *, backend: str = 'nccl') -> No
                    help='torch.distributed backend (nccl is RCCL on ROCm)')
     g.add_argument('--verbose', action='store_true', default=None,
                    help='progress bars (default: on for rank 0)')
+    g.add_argument('--cudnn-benchmark', type=int, default=1, choices=[0, 1],
+                   help='torch.backends.cudnn.benchmark (MIOpen find by timing, the '
+                        "reference's setting); 0 = MIOpen's heuristic / database solver")
 
 
 def resolve_precision(args: argparse.Namespace) -> None:
@@ -136,7 +139,7 @@ def init_distributed(args: argparse.Namespace) -> None:
     np.random.seed(args.seed)
     if args.cuda:
         torch.cuda.manual_seed(args.seed)
-        torch.backends.cudnn.benchmark = True
+        torch.backends.cudnn.benchmark = bool(getattr(args, 'cudnn_benchmark', 1))
 
 
 def log(args: argparse.Namespace, msg: str) -> None:

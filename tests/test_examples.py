@@ -37,7 +37,9 @@ def _env() -> dict[str, str]:
     return env
 
 
-def _run(args: list[str], nproc: int = 1, timeout: int = 240) -> list[dict]:
+def _run(args: list[str], nproc: int = 1, timeout: int = 240,
+         stderr: list | None = None) -> list[dict]:
+    """Run a CLI; returns its JSON log lines (``stderr`` collects its stderr)."""
     env = _env()
     if nproc > 1:
         cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
@@ -47,6 +49,8 @@ def _run(args: list[str], nproc: int = 1, timeout: int = 240) -> list[dict]:
         cmd = [sys.executable] + args
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    if stderr is not None:
+        stderr.append(p.stderr)
     out = []
     for line in p.stdout.splitlines():
         if line.startswith('{'):

@@ -14,14 +14,15 @@ pytestmark = pytest.mark.gpu
 
 
 def test_imagenet_cli_graphs(tmp_path):
+    err: list = []
     lines = _run(['examples/torch_imagenet_resnet.py', '--model', 'resnet50', '--epochs', '2',
                   '--image-size', '64', '--synthetic-train-size', '96',
                   '--synthetic-val-size', '32', '--batch-size', '8', '--val-batch-size', '8',
                   '--workers', '0', '--log-dir', str(tmp_path), '--kfac-inv-update-steps', '4',
-                  '--kfac-factor-update-steps', '2', '--graphs', '1', '--checkpoint-freq', '2'])
+                  '--kfac-factor-update-steps', '2', '--graphs', '1', '--checkpoint-freq', '2'], stderr=err)
     assert [line['epoch'] for line in lines] == [0, 1]
     for line in lines:
         assert line['train/loss'] == line['train/loss']  # not NaN
         assert line['val/loss'] == line['val/loss']
     # 12 steps per epoch: plain steps replayed from the captured graph
-    assert lines[-1]['train/graph_replays'] >= 6, lines[-1]
+    assert lines[-1]['train/graph_replays'] >= 6, (lines[-1], err[0][-4000:])

@@ -8,6 +8,7 @@ import torch
 
 import distributed_kfac_pytorch_amd as kfac
 from distributed_kfac_pytorch_amd.graphs import GraphedTrainStep
+from distributed_kfac_pytorch_amd.graphs import verify_tolerance
 
 
 def _setup(device: torch.device, seed: int = 0, method: str = 'eigen'):
@@ -50,6 +51,24 @@ def test_runner_eager_when_disabled() -> None:
     assert pre.steps == ref_pre.steps == 7
     for a, b in zip(model.parameters(), ref_model.parameters()):
         torch.testing.assert_close(a, b)
+
+
+def test_verify_tolerance() -> None:
+    """The capture-time check's per-tensor tolerance: strict for a
+    deterministic step, floored at the step's noise for a noisy one,
+    capped so O(1) corruption never passes, NaN noise fails everything."""
+    det = verify_tolerance(torch.zeros(5, dtype=torch.float64))
+    assert torch.allclose(det, torch.full_like(det, 1e-3))
+    # bf16 step: a tensor whose single eager pair agreed to 1e-4 may still
+    # differ by the 4.6 % seen across replays and eager steps
+    noisy = verify_tolerance(torch.tensor([1e-4, 0.02, 0.09], dtype=torch.float64))
+    assert noisy[0] > 0.046 and noisy[1] > 0.2
+    assert torch.all(noisy < 0.5)
+    # a model whose noise exceeds 25 %: the floor stops at 25 %, so a
+    # quiet tensor off by 100 % still fails
+    big = verify_tolerance(torch.tensor([0.0, 0.6], dtype=torch.float64))
+    assert float(big[0]) == pytest.approx(0.251)
+    assert torch.isnan(verify_tolerance(torch.tensor([0.0, float('nan')]))).all()
 
 
 def test_step_kinds() -> None:
