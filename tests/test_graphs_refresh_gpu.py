@@ -16,7 +16,8 @@ twin from the same weights are stepped ALTERNATELY in one process (each
 one's eager work lands between the other's replays), at the bench shape
 (ResNet-50, 224x224, batch 32, fused SGD, channels_last, fused BN, fused
 weight casts in bf16), with refreshes inside the replay window.  With
-deterministic MIOpen every replayed step must equal the eager twin's to the
+deterministic MIOpen (fp32 twins; bf16 steps under ``cudnn.deterministic``
+are not captured) every replayed step must equal the eager twin's to the
 bit, and parameters must stay finite.
 
 MIOpen is not always deterministic, though: ``cudnn.deterministic`` (and
@@ -98,12 +99,16 @@ def _rel(p: torch.Tensor, q: torch.Tensor) -> float:
 
 
 @pytest.mark.parametrize('amp,use_kfac,kinds,conv_mode', [
-    (True, True, ('plain',), None),
-    (True, True, ('plain',), 'gemm'),  # the bench's bf16 mode
     (False, True, ('plain', 'factor'), None),
     (False, False, ('plain',), None),
 ])
 def test_graph_replay_interleaved_with_eager_twin(cuda, amp, use_kfac, kinds, conv_mode) -> None:
+    # fp32 only: bf16 steps under cudnn.deterministic are never captured
+    # (test_unsafe_solver_graph_is_refused), and without it the default
+    # database's bf16 solvers differ by 84 % in a BN gradient between twins
+    # at step 0 (profiles/r5/pytest_gpu_r6f.log); the bf16 twins run under
+    # the bench's tuned database (test_twin_under_tuned_miopen_db, both
+    # conv modes)
     _twin(cuda, amp, use_kfac, kinds, conv_mode, deterministic=True)
 
 

@@ -20,4 +20,5 @@ csv=$(find "$raw" -name '*kernel_trace.csv' | head -n 1)
 [ -n "$csv" ] || { echo "no kernel trace"; exit 1; }
 python3 tools/trace_summary.py "$csv" "$out/window.txt" identity_kernel "${STEPS:-20}"
 python3 tools/trace_gaps_csv.py "$csv" "$out/gaps.txt" 20
+python3 tools/step_kernel_diff.py "$csv" > "$out/step_diff.txt"
 head -n 30 "$out/window.txt"
