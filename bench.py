@@ -527,6 +527,15 @@ def main() -> None:
             'precondition': 'bf16x3' if pops.grouped_gemm_enabled() else 'fp32',
             'eigensolver': 'fp32',
         }
+    if args.conv1x1 == 'gemm':
+        # fp32 model math outside MIOpen: the 1x1 convolutions' forward and
+        # input-gradient GEMMs (ops/conv.py conv1x1_math; ~5e-6 relative,
+        # TF32 -- the reference's fp32 convolution default on NVIDIA Ampere --
+        # is ~1e-3); 3x3 / 7x7 convolutions are MIOpen fp32, weight
+        # gradients hipBLASLt fp32
+        from distributed_kfac_pytorch_amd.ops.conv import conv1x1_math
+        line['model_math'] = {'conv1x1_fwd_dgrad': conv1x1_math() if args.dtype == 'fp32'
+                              else args.dtype, 'conv1x1_wgrad': 'fp32', 'conv3x3': 'fp32 (MIOpen)'}
     line['host_issue_ms'] = res['host_issue_ms']
     if base is not None:
         line['sgd_host_issue_ms'] = base['host_issue_ms']

@@ -77,6 +77,7 @@ void apply_multi(const LayerDesc* descs, int nlayers, int64_t total_blocks,
                  const float* scale, hipStream_t s);
 // gemm3.hip
 int gemm3_grid(int total_tiles);
+void gemm3_single(const GemmDesc& d, bool a_kc, bool b_kc, hipStream_t s);
 void gemm3_grouped(const GemmDesc* table, int nlayers, int total_tiles,
                    bool a_kc, bool b_kc, hipStream_t s);
 // gemm3s.hip
@@ -1043,6 +1044,45 @@ std::tuple<at::Tensor, int64_t, at::Tensor> build_gemm_table(
   return {dev_t, tiles, cpu};
 }
 
+// One fp32 GEMM C[M,N] = A . B on bf16x3 MFMA (csrc/gemm3.hip), the
+// descriptor passed by value (no table upload: capturable as a single
+// kernel node).  a_kc: A is [M, K], else the stored [K, M]; b_kc: B is the
+// stored [N, K], else [K, N].  C is overwritten.
+void gemm3_mm(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, bool a_kc,
+              bool b_kc) {
+  for (const at::Tensor* t : {&A, &B, &C}) {
+    check_cuda(*t, "gemm3_mm operand");
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->dim() == 2 && t->stride(1) == 1,
+                "gemm3_mm: operands must be fp32 2-D with unit column stride");
+  }
+  TORCH_CHECK(A.device() == B.device() && A.device() == C.device(), "gemm3_mm: one device");
+  const int64_t M = C.size(0), N = C.size(1);
+  const int64_t K = a_kc ? A.size(1) : A.size(0);
+  TORCH_CHECK((a_kc ? A.size(0) : A.size(1)) == M, "gemm3_mm: A shape");
+  TORCH_CHECK(b_kc ? (B.size(0) == N && B.size(1) == K) : (B.size(0) == K && B.size(1) == N),
+              "gemm3_mm: B shape");
+  TORCH_CHECK(M < (1 << 30) && N < (1 << 30) && K < (1 << 30), "gemm3_mm: too large");
+  kfac::GemmDesc d{};
+  d.A = A.data_ptr<float>();
+  d.B = B.data_ptr<float>();
+  d.C = C.data_ptr<float>();
+  d.lda = A.stride(0);
+  d.ldb = B.stride(0);
+  d.ldc = C.stride(0);
+  d.M = (int32_t)M;
+  d.N = (int32_t)N;
+  d.K = (int32_t)K;
+  d.Kmain = (int32_t)K;
+  d.tiles_n = (int32_t)((N + 127) / 128);
+  d.vec = (vec_ok(A) ? 1 : 0) | (vec_ok(B) ? 2 : 0);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(C.device());
+  if (K == 0) {
+    C.zero_();
+    return;
+  }
+  kfac::gemm3_single(d, a_kc, b_kc, cur_stream());
+}
+
 void gemm3_grouped(const at::Tensor& table, int64_t nlayers, int64_t total_tiles,
                    bool a_kc, bool b_kc) {
   check_cuda(table, "table");
@@ -1297,6 +1337,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("A_hls") = std::vector<c10::optional<at::Tensor>>(),
         py::arg("B_hls") = std::vector<c10::optional<at::Tensor>>());
   m.def("gemm3_grouped", &gemm3_grouped);
+  m.def("gemm3_mm", &gemm3_mm, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("a_kc"),
+        py::arg("b_kc"));
   m.def("gemm3s_align", &kfac::gemm3s_align);
   m.def("build_gemm3s_table", &build_gemm3s_table);
   m.def("gemm3s_grouped", &gemm3s_grouped);

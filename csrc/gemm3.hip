@@ -306,9 +306,16 @@ __device__ __forceinline__ v8bf16 frag_mc(const short* L, int base, int kk) {
   return __builtin_bit_cast(v8bf16, c);
 }
 
+// XCD-aware chunked remap of the block index (see header)
+__device__ __forceinline__ int gemm3_tile_of_block() {
+  const int b = blockIdx.x;
+  const int xcd = b & 7, r = b >> 3;
+  return ((r / CH) * 8 + xcd) * CH + (r % CH);
+}
+
+// one 128 x 128 output tile t of the GEMM described by d
 template <bool A_KC, bool B_KC>
-__global__ void __launch_bounds__(GNT, 2)
-gemm3_kernel(const GemmDesc* __restrict__ descs, int nlayers, int total_tiles) {
+__device__ __forceinline__ void gemm3_tile(const GemmDesc& d, int t) {
   constexpr int A_SZ = A_KC ? GT * LDK : GK * LDM;
   constexpr int B_SZ = B_KC ? GT * LDK : GK * LDM;
   constexpr int BUF = 2 * A_SZ + 2 * B_SZ;
@@ -316,12 +323,6 @@ gemm3_kernel(const GemmDesc* __restrict__ descs, int nlayers, int total_tiles) {
   // MFMAs on k-tile kt; one barrier per k-tile
   __shared__ __attribute__((aligned(16))) short lds[2 * BUF];
 
-  // XCD-aware chunked remap (see header)
-  const int b = blockIdx.x;
-  const int xcd = b & 7, r = b >> 3;
-  const int t = ((r / CH) * 8 + xcd) * CH + (r % CH);
-  if (t >= total_tiles) return;
-  const GemmDesc d = descs[find_tile_layer(descs, nlayers, t)];
   // grouped order inside a layer: GM tile rows x one tile column, column
   // after column, so a chunk of CH consecutive tiles covers a GM x CH/GM
   // block of C whose A and B panels are shared in the XCD's L2
@@ -479,7 +480,29 @@ gemm3_kernel(const GemmDesc* __restrict__ descs, int nlayers, int total_tiles) {
   }
 }
 
+template <bool A_KC, bool B_KC>
+__global__ void __launch_bounds__(GNT, 2)
+gemm3_kernel(const GemmDesc* __restrict__ descs, int nlayers, int total_tiles) {
+  const int t = gemm3_tile_of_block();
+  if (t >= total_tiles) return;
+  const GemmDesc d = descs[find_tile_layer(descs, nlayers, t)];
+  gemm3_tile<A_KC, B_KC>(d, t);
+}
+
+// one GEMM whose descriptor travels in the kernel arguments: no device
+// table to upload, so a launch is one graph-capturable kernel node (the
+// fp32 1x1 convolutions, ops/conv.py)
+template <bool A_KC, bool B_KC>
+__global__ void __launch_bounds__(GNT, 2)
+gemm3_single_kernel(const GemmDesc d, int total_tiles) {
+  const int t = gemm3_tile_of_block();
+  if (t >= total_tiles) return;
+  gemm3_tile<A_KC, B_KC>(d, t);
+}
+
 }  // namespace
+
+int gemm3_tile_edge() { return GT; }
 
 int gemm3_grid(int total_tiles) {
   const int per = 8 * CH;
@@ -494,6 +517,16 @@ void gemm3_grouped(const GemmDesc* table, int nlayers, int total_tiles,
   else if (a_kc) gemm3_kernel<true, false><<<grid, dim3(GNT), 0, s>>>(table, nlayers, total_tiles);
   else if (b_kc) gemm3_kernel<false, true><<<grid, dim3(GNT), 0, s>>>(table, nlayers, total_tiles);
   else gemm3_kernel<false, false><<<grid, dim3(GNT), 0, s>>>(table, nlayers, total_tiles);
+}
+
+void gemm3_single(const GemmDesc& d, bool a_kc, bool b_kc, hipStream_t s) {
+  const int tiles = ((d.M + GT - 1) / GT) * d.tiles_n;
+  if (tiles <= 0 || d.K <= 0) return;
+  const dim3 grid((unsigned)gemm3_grid(tiles));
+  if (a_kc && b_kc) gemm3_single_kernel<true, true><<<grid, dim3(GNT), 0, s>>>(d, tiles);
+  else if (a_kc) gemm3_single_kernel<true, false><<<grid, dim3(GNT), 0, s>>>(d, tiles);
+  else if (b_kc) gemm3_single_kernel<false, true><<<grid, dim3(GNT), 0, s>>>(d, tiles);
+  else gemm3_single_kernel<false, false><<<grid, dim3(GNT), 0, s>>>(d, tiles);
 }
 
 }  // namespace kfac

@@ -7,7 +7,8 @@ parameters, state-dict keys and values):
   convolution (graph-safe, see below; the in-tree ResNets build their
   projection shortcuts with it);
 * ``GemmConv1x1`` -- on channels_last activations, forward and ``dX`` as
-  hipBLASLt GEMMs on the NHWC activation matrix and ``dW`` reduced in slabs
+  GEMMs on the NHWC activation matrix (fp32: the native bf16x3 GEMM,
+  ``conv1x1_math``) and ``dW`` reduced in slabs
   (``_Conv1x1Gemm``); no MIOpen solver at all, and faster than MIOpen's 1x1
   solvers end to end (the bench default, ``bench.py --conv1x1``; required
   inside bf16 graphs, ``GraphedTrainStep(conv_mode='gemm')``).
@@ -117,6 +118,62 @@ def make_graph_safe(model: nn.Module, mode: str | None = None) -> int:
 _SLAB_ROWS = int(os.environ.get('KFAC_CONV1X1_SLAB_ROWS', '2048'))
 
 
+def conv1x1_math() -> str:
+    """``KFAC_CONV1X1_MATH``: bf16x3 (default) or fp32 -- how an fp32
+    ``GemmConv1x1`` computes its forward and input-gradient GEMMs.
+
+    ``bf16x3``: the native grouped GEMM of csrc/gemm3.hip on one
+    descriptor (``gemm3_mm``): each fp32 operand split into bf16 hi + lo on
+    its way into LDS and multiplied as hi.hi + hi.lo + lo.hi on bf16 MFMA
+    with fp32 accumulation -- relative error ~5e-6 against float64 (fp32
+    hipBLASLt: 1e-7 - 1e-6; TF32, the reference's default for fp32
+    convolutions on NVIDIA Ampere, ~1e-3).  On ResNet-50's stride-1 1x1
+    shapes at batch 32 it takes 3.65 ms of forward + dX + dW per step
+    against 4.97 ms for fp32 hipBLASLt (profiles/r5/conv1x1_gemm3_probe.jsonl),
+    except where K >= 1024 leaves fewer than 128 output tiles (hipBLASLt's
+    split-K wins there, and keeps those).  The weight gradient (K = N*H*W)
+    stays hipBLASLt's slab-reduced fp32 GEMM either way.  ``fp32``:
+    hipBLASLt for everything (exact fp32 products, the A/B setting)."""
+    return os.environ.get('KFAC_CONV1X1_MATH', 'bf16x3').lower()
+
+
+def _gemm3_lib(*ts: torch.Tensor):  # type: ignore[no-untyped-def]
+    """The native library when the bf16x3 path applies to these operands."""
+    if not all(t.is_cuda and t.dtype == torch.float32 for t in ts) or conv1x1_math() != 'bf16x3':
+        return None
+    from distributed_kfac_pytorch_amd.ops._native import native
+
+    return native()
+
+
+def _gemm3_pays(m: int, n: int, k: int) -> bool:
+    """bf16x3 tile GEMM vs hipBLASLt for C[m, n] with reduction k: the
+    128 x 128 tiles lose to hipBLASLt's split-K only when a long reduction
+    (k >= 1024) has fewer than 128 tiles to spread over 256 CUs."""
+    tiles = -(-m // 128) * -(-n // 128)
+    return k < 1024 or tiles >= 128
+
+
+def _mm_nt(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """``x @ w.T`` for fp32 [m, k] x [n, k]."""
+    lib = _gemm3_lib(x, w)
+    if lib is None or not _gemm3_pays(x.shape[0], w.shape[0], x.shape[1]):
+        return x @ w.t()
+    y = torch.empty(x.shape[0], w.shape[0], device=x.device, dtype=x.dtype)
+    lib.gemm3_mm(x, w, y, True, True)
+    return y
+
+
+def _mm_nn(g: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """``g @ w`` for fp32 [m, k] x [k, n]."""
+    lib = _gemm3_lib(g, w)
+    if lib is None or not _gemm3_pays(g.shape[0], w.shape[1], g.shape[1]):
+        return g @ w
+    y = torch.empty(g.shape[0], w.shape[1], device=g.device, dtype=g.dtype)
+    lib.gemm3_mm(g, w, y, True, False)
+    return y
+
+
 def _splitk(m: int, rows: int | None = None) -> int:
     """Slabs of the weight-gradient reduction over ``m`` = N*H*W rows: the
     largest power of two that divides ``m`` and leaves >= ``rows`` rows each
@@ -141,13 +198,16 @@ class _Conv1x1Gemm(torch.autograd.Function):
     ) -> torch.Tensor:
         ctx.save_for_backward(x, w)
         ctx.has_bias = b is not None
+        if _gemm3_lib(x, w) is not None and x.stride(1) == 1 and w.is_contiguous():
+            y = _mm_nt(x, w)
+            return y if b is None else y.add_(b)
         return F.linear(x, w, b)
 
     @staticmethod
     def backward(ctx, gy: torch.Tensor) -> tuple:  # type: ignore[override]
         x, w = ctx.saved_tensors
         gy = gy.contiguous()
-        gx = gy @ w if ctx.needs_input_grad[0] else None
+        gx = _mm_nn(gy, w.contiguous()) if ctx.needs_input_grad[0] else None
         gw = None
         if ctx.needs_input_grad[1]:
             m = gy.shape[0]
@@ -173,8 +233,10 @@ class GemmConv1x1(StridedConv1x1):
     ``Y[NHW, Cout] = X[NHW, Cin] W[Cout, Cin]^T`` on the NHWC activation
     matrix (a strided conv first subsamples, as ``StridedConv1x1``).  The
     backward is ``dX = dY W`` and a slab-reduced ``dW = dY^T X``
-    (``_Conv1x1Gemm``), all hipBLASLt.  Same module, parameters and state-dict keys; other layouts
-    or groups fall back to the convolution."""
+    (``_Conv1x1Gemm``): in fp32 the forward and ``dX`` run on the native
+    bf16x3 GEMM (``conv1x1_math``), the rest on hipBLASLt.  Same module,
+    parameters and state-dict keys; other layouts or groups fall back to the
+    convolution."""
 
     def _conv_forward(  # type: ignore[override]
         self,
