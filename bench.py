@@ -58,6 +58,7 @@ from distributed_kfac_pytorch_amd.graphs import step_stream  # noqa: E402
 from distributed_kfac_pytorch_amd.models.resnet import get_model  # noqa: E402
 from distributed_kfac_pytorch_amd.ops.cast import enable_fused_weight_cast  # noqa: E402
 from distributed_kfac_pytorch_amd.ops.conv import use_gemm_conv1x1  # noqa: E402
+from distributed_kfac_pytorch_amd.ops.conv import use_implicit_gemm_conv  # noqa: E402
 
 # The reference publishes no number.  Measured on MI355X: the
 # upstream kfac_pytorch package, same config and harness (shipped MIOpen
@@ -130,6 +131,9 @@ def parse_args() -> argparse.Namespace:
                         'slab-reduced weight gradient (ops/conv.py GemmConv1x1; same '
                         'values; default: fp32 1585.9 vs 1508.6 img/s with MIOpen, SGD '
                         'step 15.60 vs 16.67 ms, same box, profiles/r4_final/), or MIOpen')
+    p.add_argument('--conv-kxk', default='gemm', choices=['miopen', 'gemm'],
+                   help="3x3 convolutions: fp32 forward and stride-1 input gradient on the "
+                        'native implicit-GEMM kernel (ops/conv.py ImplicitGemmConv2d), or MIOpen')
     p.add_argument('--lr', type=float, default=0.0125)
     p.add_argument('--data-pool', type=int, default=8,
                    help='distinct synthetic batches cycled through the input buffer')
@@ -196,6 +200,8 @@ def run(args: argparse.Namespace, use_kfac: bool, rank: int, world: int,
     model = get_model(args.model).to(dev)
     if args.conv1x1 == 'gemm' and args.impl == 'native':
         use_gemm_conv1x1(model)
+    if args.conv_kxk == 'gemm' and args.impl == 'native':
+        use_implicit_gemm_conv(model)
     cl = not args.no_channels_last
     if cl:
         model = model.to(memory_format=torch.channels_last)
@@ -476,6 +482,7 @@ def main() -> None:
             'fused_weight_cast': bool(args.fused_weight_cast) and amp,
             'sgd_impl': args.sgd_impl,
             'conv1x1': args.conv1x1,
+            'conv_kxk': args.conv_kxk,
             'graphs': 'step_graphs' in res,
         },
         'timing': (
@@ -534,8 +541,13 @@ def main() -> None:
         # is ~1e-3); 3x3 / 7x7 convolutions are MIOpen fp32, weight
         # gradients hipBLASLt fp32
         from distributed_kfac_pytorch_amd.ops.conv import conv1x1_math
-        line['model_math'] = {'conv1x1_fwd_dgrad': conv1x1_math() if args.dtype == 'fp32'
-                              else args.dtype, 'conv1x1_wgrad': 'fp32', 'conv3x3': 'fp32 (MIOpen)'}
+        from distributed_kfac_pytorch_amd.ops.conv import conv_kxk_math
+        kxk = conv_kxk_math() if args.conv_kxk == 'gemm' else 'fp32'
+        line['model_math'] = {
+            'conv1x1_fwd_dgrad': conv1x1_math() if args.dtype == 'fp32' else args.dtype,
+            'conv1x1_wgrad': 'fp32',
+            'conv3x3_fwd_dgrad_stride1': kxk if args.dtype == 'fp32' else args.dtype,
+            'conv3x3_wgrad_and_strided_dgrad': 'fp32 (MIOpen)'}
     line['host_issue_ms'] = res['host_issue_ms']
     if base is not None:
         line['sgd_host_issue_ms'] = base['host_issue_ms']

@@ -283,6 +283,60 @@ __device__ __forceinline__ void store_mc_hl(const Stage& st, short* Lh, short* L
   }
 }
 
+// ---- implicit im2col (the fp32 3x3 convolutions, ops/conv.py): A is the
+// NHWC input x[N][H][W][C] read as the [N*Ho*Wo][kh*kw*C] patch matrix,
+// k = (tap i*kw + j) * C + c -- the order of a channels_last weight
+// [Cout][kh][kw][C], so B is the weight as stored.  C % 32 == 0 (host
+// check): a 32-wide k-tile lies inside one tap, each thread's 4 channels
+// are one float4.  Rows are decoded once per tile (conv_rows); every load is
+// issued at a clamped in-bounds address and zeroed afterwards (padding and
+// rows past M), so a thread's four row loads stay in flight together.
+struct PatchGeom {
+  int32_t H, W, C, Ho, Wo, kw, stride, pad;
+};
+
+struct ConvRows {
+  int pix[4];  // n * H * W of the row's image
+  int hb[4];   // ho * stride - pad (very negative past M: always padding)
+  int wb[4];   // wo * stride - pad
+};
+
+__device__ __forceinline__ void conv_rows(ConvRows& cr, const PatchGeom& g, int M, int r0) {
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int r = r0 + (threadIdx.x >> 3) + 32 * p;
+    const bool ok = r < M;
+    const int rr = ok ? r : 0;
+    const int wo = rr % g.Wo;
+    const int q = rr / g.Wo;
+    const int ho = q % g.Ho;
+    const int n = q / g.Ho;
+    cr.pix[p] = n * g.H * g.W;
+    cr.hb[p] = ok ? ho * g.stride - g.pad : -(1 << 28);
+    cr.wb[p] = wo * g.stride - g.pad;
+  }
+}
+
+__device__ __forceinline__ void load_kc_conv(Stage& st, const float* __restrict__ X,
+                                             const PatchGeom& g, const ConvRows& cr, int k0) {
+  const int tap = k0 / g.C;
+  const int c = k0 - tap * g.C + (threadIdx.x & 7) * 4;
+  const int i = tap / g.kw, j = tap - i * g.kw;
+  bool ok[4];
+  int64_t off[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int hi = cr.hb[p] + i, wi = cr.wb[p] + j;
+    ok[p] = (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
+    off[p] = ok[p] ? ((int64_t)(cr.pix[p] + hi * g.W + wi)) * g.C + c : 0;
+  }
+  float4 v[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) v[p] = gload4(X + off[p]);
+#pragma unroll
+  for (int p = 0; p < 4; ++p) st.r[p] = ok[p] ? v[p] : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
 // fragment: lane l gets X[row = base + (l & 31)][k = kk + 8 (l >> 5) + 0..7]
 __device__ __forceinline__ v8bf16 frag_kc(const short* L, int base, int kk) {
   const int l = threadIdx.x & 63;
@@ -314,8 +368,11 @@ __device__ __forceinline__ int gemm3_tile_of_block() {
 }
 
 // one 128 x 128 output tile t of the GEMM described by d
-template <bool A_KC, bool B_KC>
-__device__ __forceinline__ void gemm3_tile(const GemmDesc& d, int t) {
+// k-tiles [kt_begin, kt_begin + kt_count) of the reduction (split-K
+// callers; kt_count < 0: to the end)
+template <bool A_KC, bool B_KC, bool CONV = false>
+__device__ __forceinline__ void gemm3_tile(const GemmDesc& d, int t, const PatchGeom& g = {},
+                                           int kt_begin = 0, int kt_count = -1) {
   constexpr int A_SZ = A_KC ? GT * LDK : GK * LDM;
   constexpr int B_SZ = B_KC ? GT * LDK : GK * LDM;
   constexpr int BUF = 2 * A_SZ + 2 * B_SZ;
@@ -353,6 +410,8 @@ __device__ __forceinline__ void gemm3_tile(const GemmDesc& d, int t) {
   // k-tile kt is multiplied, so each load has two k-tiles of MFMA time
   // (plus the co-resident block's) to land before it is split and stored
   Stage sa0, sb0, sa1, sb1;
+  ConvRows cr;
+  if constexpr (CONV) conv_rows(cr, g, d.M, m0);
   auto load = [&](Stage& sa, Stage& sb, int k0) {
     if constexpr (GEMM3_DIAG == 1) {
 #pragma unroll
@@ -362,7 +421,9 @@ __device__ __forceinline__ void gemm3_tile(const GemmDesc& d, int t) {
       }
       return;
     }
-    if constexpr (A_KC) {
+    if constexpr (CONV) {
+      load_kc_conv(sa, d.A, g, cr, k0);
+    } else if constexpr (A_KC) {
       if (a_hl) load_kc_hl(sa, (const float*)d.Ah, d.lda, d.M, m0, d.Kmain, k0);
       else load_kc(sa, d.A, d.A_extra, d.lda, d.M, m0, d.Kmain, k0, avec);
     } else {
@@ -442,16 +503,18 @@ __device__ __forceinline__ void gemm3_tile(const GemmDesc& d, int t) {
   };
   // iteration kt: LDS buf[kt&1] holds tile kt, stage (kt+1)&1 holds tile
   // kt+1 (in flight), stage kt&1 is free for tile kt+2
+  const int kb = kt_begin * GK;
   auto step = [&](int kt, int nt, Stage& fa, Stage& fb, Stage& na, Stage& nb) {
-    if (kt + 2 < nt) load(fa, fb, (kt + 2) * GK);
+    if (kt + 2 < nt) load(fa, fb, kb + (kt + 2) * GK);
     compute(lds + (kt & 1) * BUF);
     if (kt + 1 < nt) store(na, nb, lds + ((kt + 1) & 1) * BUF);
     __syncthreads();
   };
 
-  const int ntiles = (d.K + GK - 1) / GK;
-  load(sa0, sb0, 0);
-  if (ntiles > 1) load(sa1, sb1, GK);
+  const int kt_all = (d.K + GK - 1) / GK - kt_begin;
+  const int ntiles = kt_count < 0 ? kt_all : min(kt_count, kt_all);
+  load(sa0, sb0, kb);
+  if (ntiles > 1) load(sa1, sb1, kb + GK);
   store(sa0, sb0, lds);
   __syncthreads();
   for (int kt = 0; kt < ntiles; kt += 2) {
@@ -500,6 +563,21 @@ gemm3_single_kernel(const GemmDesc d, int total_tiles) {
   gemm3_tile<A_KC, B_KC>(d, t);
 }
 
+// implicit-GEMM convolution: C[N*Ho*Wo][Cout] = patches(x) . w^T, the
+// descriptor and the geometry by value
+// split-K: block b covers tile (b' % tiles) of split (b' / tiles) and
+// writes its partial sum to C + split * split_stride (the host sums them)
+__global__ void __launch_bounds__(GNT, 2)
+gemm3_conv_kernel(const GemmDesc d, const PatchGeom g, int tiles, int splits, int kt_per,
+                  int64_t split_stride) {
+  const int b = gemm3_tile_of_block();
+  if (b >= tiles * splits) return;
+  const int z = b / tiles;
+  GemmDesc dz = d;
+  dz.C = d.C + (int64_t)z * split_stride;
+  gemm3_tile<true, true, true>(dz, b - z * tiles, g, z * kt_per, kt_per);
+}
+
 }  // namespace
 
 int gemm3_tile_edge() { return GT; }
@@ -527,6 +605,47 @@ void gemm3_single(const GemmDesc& d, bool a_kc, bool b_kc, hipStream_t s) {
   else if (a_kc) gemm3_single_kernel<true, false><<<grid, dim3(GNT), 0, s>>>(d, tiles);
   else if (b_kc) gemm3_single_kernel<false, true><<<grid, dim3(GNT), 0, s>>>(d, tiles);
   else gemm3_single_kernel<false, false><<<grid, dim3(GNT), 0, s>>>(d, tiles);
+}
+
+int gemm3_conv_splits(int N, int H, int W, int C, int Cout, int kh, int kw, int stride, int pad) {
+  const int Ho = (H + 2 * pad - kh) / stride + 1;
+  const int Wo = (W + 2 * pad - kw) / stride + 1;
+  const int tiles = ((N * Ho * Wo + GT - 1) / GT) * ((Cout + GT - 1) / GT);
+  const int kts = (kh * kw * C + GK - 1) / GK;
+  // fill 256 CUs, keeping >= 8 k-tiles per split
+  int sp = (256 + tiles - 1) / tiles;
+  if (sp > kts / 8) sp = kts / 8;
+  if (sp < 1) sp = 1;
+  // equal k-tile counts: every split non-empty
+  const int per = (kts + sp - 1) / sp;
+  return (kts + per - 1) / per;
+}
+
+// y: [splits][N*Ho*Wo][Cout] partials when splits > 1
+void gemm3_conv(const float* x, const float* w, float* y, int N, int H, int W, int C, int Cout,
+                int kh, int kw, int stride, int pad, int splits, hipStream_t s) {
+  const int Ho = (H + 2 * pad - kh) / stride + 1;
+  const int Wo = (W + 2 * pad - kw) / stride + 1;
+  GemmDesc d{};
+  d.A = x;
+  d.B = w;
+  d.C = y;
+  d.lda = C;
+  d.ldb = (int64_t)kh * kw * C;
+  d.ldc = Cout;
+  d.M = N * Ho * Wo;
+  d.N = Cout;
+  d.K = kh * kw * C;
+  d.Kmain = d.K;
+  d.tiles_n = (Cout + GT - 1) / GT;
+  d.vec = 3;
+  const PatchGeom g{H, W, C, Ho, Wo, kw, stride, pad};
+  const int tiles = ((d.M + GT - 1) / GT) * d.tiles_n;
+  if (tiles <= 0) return;
+  const int kts = (d.K + GK - 1) / GK;
+  const int per = (kts + splits - 1) / splits;
+  gemm3_conv_kernel<<<dim3((unsigned)gemm3_grid(tiles * splits)), dim3(GNT), 0, s>>>(
+      d, g, tiles, splits, per, (int64_t)d.M * Cout);
 }
 
 }  // namespace kfac

@@ -45,7 +45,8 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
-__all__ = ['StridedConv1x1', 'GemmConv1x1', 'make_graph_safe', 'is_strided_1x1', 'use_gemm_conv1x1']
+__all__ = ['StridedConv1x1', 'GemmConv1x1', 'ImplicitGemmConv2d', 'make_graph_safe',
+           'is_strided_1x1', 'use_gemm_conv1x1', 'use_implicit_gemm_conv']
 
 
 def is_strided_1x1(m: nn.Module) -> bool:
@@ -137,9 +138,11 @@ def conv1x1_math() -> str:
     return os.environ.get('KFAC_CONV1X1_MATH', 'bf16x3').lower()
 
 
-def _gemm3_lib(*ts: torch.Tensor):  # type: ignore[no-untyped-def]
-    """The native library when the bf16x3 path applies to these operands."""
-    if not all(t.is_cuda and t.dtype == torch.float32 for t in ts) or conv1x1_math() != 'bf16x3':
+def _gemm3_lib(*ts: torch.Tensor, math: str | None = None):  # type: ignore[no-untyped-def]
+    """The native library when the bf16x3 path (``math``, default
+    ``conv1x1_math()``) applies to these operands."""
+    if (not all(t.is_cuda and t.dtype == torch.float32 for t in ts)
+            or (math or conv1x1_math()) != 'bf16x3'):
         return None
     from distributed_kfac_pytorch_amd.ops._native import native
 
@@ -274,3 +277,102 @@ def use_gemm_conv1x1(model: nn.Module) -> int:
             m.__class__ = GemmConv1x1
             n += 1
     return n
+
+
+def conv_kxk_math() -> str:
+    """``KFAC_CONV_KXK_MATH``: bf16x3 (default) or fp32 -- how an fp32
+    ``ImplicitGemmConv2d`` computes its forward and (stride 1) input
+    gradient: the native implicit-GEMM convolution of csrc/gemm3.hip
+    (patches gathered from the NHWC input on their way into LDS, bf16x3
+    MFMA, ~5e-6 relative against float64) or MIOpen fp32."""
+    return os.environ.get('KFAC_CONV_KXK_MATH', 'bf16x3').lower()
+
+
+class _ConvImplicit(torch.autograd.Function):
+    """``y = conv2d(x, w, b, stride, pad)`` with the forward -- and, at
+    stride 1, the input gradient as the convolution of ``dy`` with the
+    flipped, transposed kernel -- on the native implicit GEMM; the weight
+    gradient (and a strided input gradient) through MIOpen's
+    ``convolution_backward``."""
+
+    @staticmethod
+    def forward(  # type: ignore[override]
+        ctx, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None, stride: int, pad: int,
+        lib,  # type: ignore[no-untyped-def]
+    ) -> torch.Tensor:
+        ctx.save_for_backward(x, w)
+        ctx.conf = (stride, pad, b is not None, lib)
+        y = lib.gemm3_conv(x, w.contiguous(memory_format=torch.channels_last), stride, pad)
+        if b is not None:
+            y.add_(b.view(1, -1, 1, 1))
+        return y
+
+    @staticmethod
+    def backward(ctx, gy: torch.Tensor) -> tuple:  # type: ignore[override]
+        x, w = ctx.saved_tensors
+        stride, pad, has_bias, lib = ctx.conf
+        gy = gy.contiguous(memory_format=torch.channels_last)
+        k = w.shape[2]
+        gx = gw = gb = None
+        native_dx = (ctx.needs_input_grad[0] and stride == 1 and k - 1 - pad >= 0
+                     and w.shape[0] % 32 == 0)
+        if native_dx:
+            wf = w.flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last)
+            gx = lib.gemm3_conv(gy, wf, 1, k - 1 - pad)
+        mask = [ctx.needs_input_grad[0] and not native_dx, ctx.needs_input_grad[1], False]
+        if any(mask):
+            r = torch.ops.aten.convolution_backward(
+                gy, x, w, None, [stride, stride], [pad, pad], [1, 1], False, [0, 0], 1, mask)
+            if mask[0]:
+                gx = r[0]
+            gw = r[1]
+        if has_bias and ctx.needs_input_grad[2]:
+            gb = gy.sum((0, 2, 3))
+        return gx, gw, gb, None, None, None
+
+
+def _implicit_ok(m: nn.Conv2d) -> bool:
+    kh, kw = m.kernel_size
+    return (m.groups == 1 and tuple(m.dilation) == (1, 1) and m.padding_mode == 'zeros'
+            and kh == kw and kh > 1 and isinstance(m.padding, tuple)
+            and m.padding[0] == m.padding[1] and m.stride[0] == m.stride[1]
+            and m.in_channels % 32 == 0 and min(m.in_channels, m.out_channels) >= 128)
+
+
+class ImplicitGemmConv2d(nn.Conv2d):
+    """``nn.Conv2d`` (square kernel > 1, symmetric stride / padding, no
+    groups or dilation, ``in_channels % 32 == 0``: ResNet's 3x3
+    convolutions) whose fp32 channels_last forward and stride-1 input
+    gradient run on the native implicit-GEMM kernel (``_ConvImplicit``,
+    ``conv_kxk_math``; split-K over the 9 x C reduction when the image is
+    too small to fill the chip).  ResNet-50 batch 32, per convolution:
+    forward 59-73 us vs MIOpen fp32's 105-179 us at 128-512 channels, the
+    64-channel stage stays on MIOpen (a 128-wide tile would be half empty,
+    ``use_implicit_gemm_conv`` skips it) -- profiles/r5/conv3x3_probe.jsonl,
+    bench 1760 -> 1835 img/s.  Same module,
+    parameters and state-dict keys (K-FAC sees an ``nn.Conv2d``); bf16
+    autocast, other layouts and the CPU take ``nn.Conv2d``'s path."""
+
+    def _conv_forward(  # type: ignore[override]
+        self,
+        input: torch.Tensor,
+        weight: torch.Tensor,
+        bias: torch.Tensor | None,
+    ) -> torch.Tensor:
+        lib = _gemm3_lib(input, weight, math=conv_kxk_math())
+        if (lib is None or torch.is_autocast_enabled(input.device.type)
+                or not input.is_contiguous(memory_format=torch.channels_last)):
+            return super()._conv_forward(input, weight, bias)
+        return _ConvImplicit.apply(input, weight, bias, self.stride[0], self.padding[0], lib)
+
+
+def use_implicit_gemm_conv(model: nn.Module) -> int:
+    """Switch every eligible non-1x1 ``nn.Conv2d`` of ``model`` (in place)
+    to ``ImplicitGemmConv2d``.  Returns the number switched."""
+    n = 0
+    for m in model.modules():
+        if type(m) is nn.Conv2d and _implicit_ok(m):
+            m.__class__ = ImplicitGemmConv2d
+            n += 1
+    return n
+

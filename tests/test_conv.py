@@ -176,3 +176,56 @@ def test_gemm_conv1x1_fp32_native_matches_float64(cuda, shape, stride, monkeypat
     assert rel(y, yd) < 2e-5, rel(y, yd)
     assert rel(x.grad, xd.grad) < 2e-5, rel(x.grad, xd.grad)
     assert rel(gem.weight.grad, wd.grad) < 2e-5, rel(gem.weight.grad, wd.grad)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('shape,stride', [((8, 64, 56, 56, 64), 1), ((8, 128, 56, 56, 128), 2),
+                                          ((32, 512, 7, 7, 512), 1), ((2, 96, 11, 13, 40), 1)])
+def test_implicit_gemm_conv_matches_float64(cuda, shape, stride, monkeypatch) -> None:
+    """fp32 ``ImplicitGemmConv2d`` (3x3, pad 1): forward on the native
+    implicit GEMM (split-K on small images), stride-1 input gradient as the
+    native convolution of dy with the flipped kernel, weight gradient from
+    MIOpen -- output and both gradients match float64 to fp32-class
+    accuracy, and the native kernel runs."""
+    from distributed_kfac_pytorch_amd.ops import _native
+    from distributed_kfac_pytorch_amd.ops.conv import ImplicitGemmConv2d
+
+    lib = _native.native()
+    assert lib is not None, _native.load_error()
+    calls = []
+    real = lib.gemm3_conv
+
+    class Spy:
+        def __getattr__(self, name):  # type: ignore[no-untyped-def]
+            return getattr(lib, name)
+
+        def gemm3_conv(self, *a):  # type: ignore[no-untyped-def]
+            calls.append(tuple(a[0].shape))
+            return real(*a)
+
+    monkeypatch.setattr(_native, 'native', lambda: Spy())
+    monkeypatch.setenv('KFAC_CONV_KXK_MATH', 'bf16x3')
+    n, c, h, w, co = shape
+    torch.manual_seed(0)
+    conv = nn.Conv2d(c, co, 3, stride=stride, padding=1, bias=True).to(cuda)
+    conv = conv.to(memory_format=torch.channels_last)
+    conv.__class__ = ImplicitGemmConv2d
+    x = torch.randn(n, c, h, w, device=cuda).contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    y = conv(x)
+    g = torch.randn_like(y)
+    y.backward(g)
+    assert len(calls) == 1 + (stride == 1 and co % 32 == 0), calls
+    xd = x.detach().double().requires_grad_(True)
+    wd = conv.weight.detach().double().requires_grad_(True)
+    bd = conv.bias.detach().double().requires_grad_(True)
+    yd = torch.nn.functional.conv2d(xd, wd, bd, stride=stride, padding=1)
+    yd.backward(g.double())
+
+    def rel(a: torch.Tensor, b: torch.Tensor) -> float:
+        return float((a.double() - b).norm() / b.norm())
+
+    assert rel(y, yd) < 2e-5, rel(y, yd)
+    assert rel(x.grad, xd.grad) < 2e-5, rel(x.grad, xd.grad)
+    assert rel(conv.weight.grad, wd.grad) < 2e-5, rel(conv.weight.grad, wd.grad)
+    assert rel(conv.bias.grad, bd.grad) < 2e-5, rel(conv.bias.grad, bd.grad)
