@@ -80,7 +80,7 @@ int gemm3_grid(int total_tiles);
 void gemm3_single(const GemmDesc& d, bool a_kc, bool b_kc, hipStream_t s);
 int gemm3_conv_splits(int N, int H, int W, int C, int Cout, int kh, int kw, int stride, int pad);
 void gemm3_conv(const float* x, const float* w, float* y, int N, int H, int W, int C, int Cout,
-                int kh, int kw, int stride, int pad, int splits, hipStream_t s);
+                int kh, int kw, int stride, int pad, int splits, bool flipw, hipStream_t s);
 void gemm3_grouped(const GemmDesc* table, int nlayers, int total_tiles,
                    bool a_kc, bool b_kc, hipStream_t s);
 // gemm3s.hip
@@ -1089,7 +1089,11 @@ void gemm3_mm(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, boo
 // Implicit-GEMM convolution on bf16x3 MFMA (csrc/gemm3.hip): x [N, C, H, W]
 // and w [Cout, C, kh, kw] both channels_last fp32, C % 32 == 0, no
 // dilation or groups; returns y [N, Cout, Ho, Wo] channels_last.
-at::Tensor gemm3_conv(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad) {
+// flipw: w is a stride-1 forward weight [Cf, Cout, kh, kw] (Cf = x's C) and
+// the convolution applied is its flipped transpose -- the input gradient of
+// that convolution when x is dy (pad = kh - 1 - forward pad).
+at::Tensor gemm3_conv(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad,
+                      bool flipw) {
   check_cuda(x, "gemm3_conv x");
   check_cuda(w, "gemm3_conv w");
   TORCH_CHECK(x.scalar_type() == at::kFloat && w.scalar_type() == at::kFloat && x.dim() == 4 &&
@@ -1098,8 +1102,10 @@ at::Tensor gemm3_conv(const at::Tensor& x, const at::Tensor& w, int64_t stride, 
                   w.is_contiguous(at::MemoryFormat::ChannelsLast),
               "gemm3_conv: channels_last operands");
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
-  const int64_t Co = w.size(0), kh = w.size(2), kw = w.size(3);
-  TORCH_CHECK(w.size(1) == C && C % 32 == 0, "gemm3_conv: C must match and be a multiple of 32");
+  const int64_t Co = flipw ? w.size(1) : w.size(0), kh = w.size(2), kw = w.size(3);
+  TORCH_CHECK((flipw ? w.size(0) : w.size(1)) == C && C % 32 == 0,
+              "gemm3_conv: C must match and be a multiple of 32");
+  TORCH_CHECK(!flipw || (stride == 1 && Co % 4 == 0), "gemm3_conv: flipw needs stride 1");
   TORCH_CHECK(stride >= 1 && pad >= 0 && kh >= 1 && kw >= 1, "gemm3_conv: geometry");
   const int64_t Ho = (H + 2 * pad - kh) / stride + 1, Wo = (W + 2 * pad - kw) / stride + 1;
   TORCH_CHECK(Ho > 0 && Wo > 0, "gemm3_conv: empty output");
@@ -1116,7 +1122,7 @@ at::Tensor gemm3_conv(const at::Tensor& x, const at::Tensor& w, int64_t stride, 
   at::Tensor part = sp > 1 ? at::empty({sp, N * Ho * Wo, Co}, x.options()) : y;
   kfac::gemm3_conv(x.data_ptr<float>(), w.data_ptr<float>(), part.data_ptr<float>(), (int)N,
                    (int)H, (int)W, (int)C, (int)Co, (int)kh, (int)kw, (int)stride, (int)pad, sp,
-                   cur_stream());
+                   flipw, cur_stream());
   if (sp > 1) {
     auto yv = y.permute({0, 2, 3, 1}).view({N * Ho * Wo, Co});
     at::sum_out(yv, part, {0});
@@ -1378,7 +1384,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("A_hls") = std::vector<c10::optional<at::Tensor>>(),
         py::arg("B_hls") = std::vector<c10::optional<at::Tensor>>());
   m.def("gemm3_grouped", &gemm3_grouped);
-  m.def("gemm3_conv", &gemm3_conv, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"));
+  m.def("gemm3_conv", &gemm3_conv, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"),
+        py::arg("flipw") = false);
   m.def("gemm3_mm", &gemm3_mm, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("a_kc"),
         py::arg("b_kc"));
   m.def("gemm3s_align", &kfac::gemm3s_align);

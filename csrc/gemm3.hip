@@ -292,7 +292,7 @@ __device__ __forceinline__ void store_mc_hl(const Stage& st, short* Lh, short* L
 // issued at a clamped in-bounds address and zeroed afterwards (padding and
 // rows past M), so a thread's four row loads stay in flight together.
 struct PatchGeom {
-  int32_t H, W, C, Ho, Wo, kw, stride, pad;
+  int32_t H, W, C, Ho, Wo, kw, stride, pad, kh;
 };
 
 struct ConvRows {
@@ -337,6 +337,30 @@ __device__ __forceinline__ void load_kc_conv(Stage& st, const float* __restrict_
   for (int p = 0; p < 4; ++p) st.r[p] = ok[p] ? v[p] : make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
+// B of the stride-1 input gradient: the flipped, transposed kernel read in
+// place from the channels_last weight w[Co][kh][kw][Ci] (no flipped copy):
+// B[k = (i, j, co)][n = ci] = w[co][kh-1-i][kw-1-j][ci], n-contiguous rows.
+// The patches' C is Co, so a 32-row k-tile lies inside one tap.
+__device__ __forceinline__ void load_mc_flipw(Stage& st, const float* __restrict__ Wt,
+                                              const PatchGeom& g, int ncols, int n0, int k0) {
+  const int t = threadIdx.x;
+  const int n = n0 + (t & 31) * 4;
+  const int tap = k0 / g.C;
+  const int i = tap / g.kw, j = tap - i * g.kw;
+  const int co0 = k0 - tap * g.C + (t >> 5);
+  const int64_t tapoff = (int64_t)((g.kh - 1 - i) * g.kw + (g.kw - 1 - j)) * ncols;
+  const bool ok = n < ncols;  // ncols % 4 == 0 (host check)
+  float4 v[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int co = co0 + 8 * p;
+    const int64_t off = ok ? (int64_t)co * g.kh * g.kw * ncols + tapoff + n : 0;
+    v[p] = gload4(Wt + off);
+  }
+#pragma unroll
+  for (int p = 0; p < 4; ++p) st.r[p] = ok ? v[p] : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
 // fragment: lane l gets X[row = base + (l & 31)][k = kk + 8 (l >> 5) + 0..7]
 __device__ __forceinline__ v8bf16 frag_kc(const short* L, int base, int kk) {
   const int l = threadIdx.x & 63;
@@ -370,7 +394,7 @@ __device__ __forceinline__ int gemm3_tile_of_block() {
 // one 128 x 128 output tile t of the GEMM described by d
 // k-tiles [kt_begin, kt_begin + kt_count) of the reduction (split-K
 // callers; kt_count < 0: to the end)
-template <bool A_KC, bool B_KC, bool CONV = false>
+template <bool A_KC, bool B_KC, bool CONV = false, bool FLIPW = false>
 __device__ __forceinline__ void gemm3_tile(const GemmDesc& d, int t, const PatchGeom& g = {},
                                            int kt_begin = 0, int kt_count = -1) {
   constexpr int A_SZ = A_KC ? GT * LDK : GK * LDM;
@@ -430,7 +454,9 @@ __device__ __forceinline__ void gemm3_tile(const GemmDesc& d, int t, const Patch
       if (a_hl) load_mc_hl(sa, (const float*)d.Ah, d.lda, d.M, m0, d.K, k0);
       else load_mc(sa, d.A, d.lda, d.M, m0, d.K, k0, avec);
     }
-    if constexpr (B_KC) {
+    if constexpr (FLIPW) {
+      load_mc_flipw(sb, d.B, g, d.N, n0, k0);
+    } else if constexpr (B_KC) {
       if (b_hl) load_kc_hl(sb, (const float*)d.Bh, d.ldb, d.N, n0, d.K, k0);
       else load_kc(sb, d.B, nullptr, d.ldb, d.N, n0, d.K, k0, bvec);
     } else {
@@ -567,6 +593,7 @@ gemm3_single_kernel(const GemmDesc d, int total_tiles) {
 // descriptor and the geometry by value
 // split-K: block b covers tile (b' % tiles) of split (b' / tiles) and
 // writes its partial sum to C + split * split_stride (the host sums them)
+template <bool FLIPW>
 __global__ void __launch_bounds__(GNT, 2)
 gemm3_conv_kernel(const GemmDesc d, const PatchGeom g, int tiles, int splits, int kt_per,
                   int64_t split_stride) {
@@ -575,7 +602,7 @@ gemm3_conv_kernel(const GemmDesc d, const PatchGeom g, int tiles, int splits, in
   const int z = b / tiles;
   GemmDesc dz = d;
   dz.C = d.C + (int64_t)z * split_stride;
-  gemm3_tile<true, true, true>(dz, b - z * tiles, g, z * kt_per, kt_per);
+  gemm3_tile<true, !FLIPW, true, FLIPW>(dz, b - z * tiles, g, z * kt_per, kt_per);
 }
 
 }  // namespace
@@ -621,9 +648,12 @@ int gemm3_conv_splits(int N, int H, int W, int C, int Cout, int kh, int kw, int 
   return (kts + per - 1) / per;
 }
 
-// y: [splits][N*Ho*Wo][Cout] partials when splits > 1
+// y: [splits][N*Ho*Wo][Cout] partials when splits > 1.  flipw: w is the
+// forward weight [Cout_fwd = C][kh][kw][Cout] of a stride-1 convolution and
+// the kernel applied is its flipped transpose (the input gradient of x is
+// gemm3_conv(dy, w, flipw) with pad kh - 1 - pad)
 void gemm3_conv(const float* x, const float* w, float* y, int N, int H, int W, int C, int Cout,
-                int kh, int kw, int stride, int pad, int splits, hipStream_t s) {
+                int kh, int kw, int stride, int pad, int splits, bool flipw, hipStream_t s) {
   const int Ho = (H + 2 * pad - kh) / stride + 1;
   const int Wo = (W + 2 * pad - kw) / stride + 1;
   GemmDesc d{};
@@ -639,13 +669,19 @@ void gemm3_conv(const float* x, const float* w, float* y, int N, int H, int W, i
   d.Kmain = d.K;
   d.tiles_n = (Cout + GT - 1) / GT;
   d.vec = 3;
-  const PatchGeom g{H, W, C, Ho, Wo, kw, stride, pad};
+  const PatchGeom g{H, W, C, Ho, Wo, kw, stride, pad, kh};
   const int tiles = ((d.M + GT - 1) / GT) * d.tiles_n;
   if (tiles <= 0) return;
   const int kts = (d.K + GK - 1) / GK;
   const int per = (kts + splits - 1) / splits;
-  gemm3_conv_kernel<<<dim3((unsigned)gemm3_grid(tiles * splits)), dim3(GNT), 0, s>>>(
-      d, g, tiles, splits, per, (int64_t)d.M * Cout);
+  if (flipw) {
+    d.ldb = Cout;
+    gemm3_conv_kernel<true><<<dim3((unsigned)gemm3_grid(tiles * splits)), dim3(GNT), 0, s>>>(
+        d, g, tiles, splits, per, (int64_t)d.M * Cout);
+  } else {
+    gemm3_conv_kernel<false><<<dim3((unsigned)gemm3_grid(tiles * splits)), dim3(GNT), 0, s>>>(
+        d, g, tiles, splits, per, (int64_t)d.M * Cout);
+  }
 }
 
 }  // namespace kfac

@@ -61,6 +61,34 @@ def is_strided_1x1(m: nn.Module) -> bool:
     )
 
 
+class _Subsample(torch.autograd.Function):
+    """``x[:, :, ::sh, ::sw]`` as a channels_last tensor whose backward is
+    ONE zero-fill + strided copy into a channels_last gradient.  Autograd's
+    own slice backward builds two NCHW-contiguous zero tensors (one per
+    sliced dim); the residual branch's channels_last gradient is then added
+    to them by an unvectorised mixed-layout add -- 190 us for ResNet-50's
+    layer2 input alone, ~0.5 ms per step over the three projection
+    shortcuts (profiles/r5/prof_fp32_r6o/)."""
+
+    @staticmethod
+    def forward(ctx, x: torch.Tensor, sh: int, sw: int) -> torch.Tensor:  # type: ignore[override]
+        ctx.conf = (x.shape, sh, sw)
+        return x[:, :, ::sh, ::sw].contiguous(memory_format=torch.channels_last)
+
+    @staticmethod
+    def backward(ctx, g: torch.Tensor) -> tuple:  # type: ignore[override]
+        shape, sh, sw = ctx.conf
+        gx = g.new_zeros(shape).contiguous(memory_format=torch.channels_last)
+        gx[:, :, ::sh, ::sw] = g
+        return gx, None, None
+
+
+def _subsample(x: torch.Tensor, sh: int, sw: int) -> torch.Tensor:
+    if x.is_contiguous(memory_format=torch.channels_last):
+        return _Subsample.apply(x, sh, sw)
+    return x[:, :, ::sh, ::sw]
+
+
 class StridedConv1x1(nn.Conv2d):
     """``nn.Conv2d`` (1x1, stride > 1) evaluated as subsample + stride-1
     conv (see the module docstring)."""
@@ -72,9 +100,7 @@ class StridedConv1x1(nn.Conv2d):
         bias: torch.Tensor | None,
     ) -> torch.Tensor:
         sh, sw = self.stride
-        sub = input[:, :, ::sh, ::sw]
-        if input.is_contiguous(memory_format=torch.channels_last):
-            sub = sub.contiguous(memory_format=torch.channels_last)
+        sub = _subsample(input, sh, sw)
         return F.conv2d(sub, weight, bias, 1, 0, 1, self.groups)
 
 
@@ -252,7 +278,7 @@ class GemmConv1x1(StridedConv1x1):
         sh, sw = self.stride
         x = input
         if (sh, sw) != (1, 1):
-            x = input[:, :, ::sh, ::sw].contiguous(memory_format=torch.channels_last)
+            x = _subsample(input, sh, sw)
         n, c, h, w = x.shape
         x2 = x.permute(0, 2, 3, 1).reshape(n * h * w, c)
         w2 = weight.view(weight.shape[0], c)
@@ -317,8 +343,9 @@ class _ConvImplicit(torch.autograd.Function):
         native_dx = (ctx.needs_input_grad[0] and stride == 1 and k - 1 - pad >= 0
                      and w.shape[0] % 32 == 0)
         if native_dx:
-            wf = w.flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last)
-            gx = lib.gemm3_conv(gy, wf, 1, k - 1 - pad)
+            # the flipped, transposed kernel is read in place (flipw)
+            gx = lib.gemm3_conv(gy, w.contiguous(memory_format=torch.channels_last), 1,
+                                k - 1 - pad, True)
         mask = [ctx.needs_input_grad[0] and not native_dx, ctx.needs_input_grad[1], False]
         if any(mask):
             r = torch.ops.aten.convolution_backward(

@@ -83,9 +83,7 @@ def main() -> None:
             nat['fwd_us'] = round(timed(lambda: lib.gemm3_conv(x, wc, s, p)), 1)
             if s == 1 and co % 32 == 0:
                 def nat_dgrad() -> torch.Tensor:
-                    wf = wt.flip(2, 3).transpose(0, 1).contiguous(
-                        memory_format=torch.channels_last)
-                    return lib.gemm3_conv(gy, wf, 1, k - 1 - p)
+                    return lib.gemm3_conv(gy, wc, 1, k - 1 - p, True)
                 dx = nat_dgrad()
                 refx = torch.ops.aten.convolution_backward(
                     gy.double(), x.double(), wt.double(), None, [s, s], [p, p], [1, 1], False,

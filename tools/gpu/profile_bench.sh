@@ -21,4 +21,5 @@ csv=$(find "$raw" -name '*kernel_trace.csv' | head -n 1)
 python3 tools/trace_summary.py "$csv" "$out/window.txt" identity_kernel "${STEPS:-20}"
 python3 tools/trace_gaps_csv.py "$csv" "$out/gaps.txt" 20
 python3 tools/step_kernel_diff.py "$csv" > "$out/step_diff.txt"
+[ -z "$KEEP_CSV" ] || gzip -c "$csv" > "$out/kernel_trace.csv.gz"
 head -n 30 "$out/window.txt"

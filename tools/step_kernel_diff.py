@@ -42,7 +42,7 @@ def main(path: str, marker: str = 'max_pool_forward') -> None:
             return 'inverse'
         if 'syrk_kernel' in names:
             return 'factor'
-        if 'gemm3' in names:
+        if 'gemm3s_kernel' in names:
             return 'plain'
         return 'sgd'
 
@@ -68,6 +68,11 @@ def main(path: str, marker: str = 'max_pool_forward') -> None:
         print('\nper-step kernel time, factor-update minus plain K-FAC step (us):')
         for dt, n in diff[:20]:
             print(f'{dt:9.1f}  factor {f.get(n, 0):8.1f}  plain {p.get(n, 0):8.1f}  {n}')
+    if 'sgd' in by:
+        s = agg(by['sgd'])
+        print('\nper-step kernel time of an SGD step, top 30 (us):')
+        for n, t in sorted(s.items(), key=lambda kv: -kv[1])[:30]:
+            print(f'{t:9.1f}  {n}')
     if 'plain' in by and 'sgd' in by:
         p, s = agg(by['plain']), agg(by['sgd'])
         diff = sorted(((p.get(n, 0) - s.get(n, 0), n) for n in set(p) | set(s)), reverse=True)
