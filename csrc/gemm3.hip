@@ -108,7 +108,16 @@ __device__ __forceinline__ void split4(const float4 v, v4i16& hi, v4i16& lo) {
 // one operand's staging registers: 4 float4 per thread per k-tile
 struct Stage {
   float4 r[4];
+  // bit p set: row group p is valid.  Loads land raw in r[] and the zeroing
+  // of out-of-range rows waits until the split (stage_get): a select right
+  // after the load made the compiler wait for the load there, before the
+  // MFMAs of the current k-tile, and the prefetch never overlapped them.
+  uint32_t ok;
 };
+
+__device__ __forceinline__ float4 stage_get(const Stage& st, int p) {
+  return ((st.ok >> p) & 1u) ? st.r[p] : make_float4(0.f, 0.f, 0.f, 0.f);
+}
 
 // Pointers come out of the descriptor table, so the compiler cannot infer
 // their address space and would emit FLAT loads (which also count on
@@ -127,43 +136,98 @@ __device__ __forceinline__ float gload(const float* p) {
 
 // k-contiguous operand: rows [r0, r0+128) of a [rows][ld] matrix, columns
 // [k0, k0+32).  Thread t: chunk = t & 7 (4 columns), row = (t >> 3) + 32p.
-// `full` (uniform per block and k-tile): the tile is interior and float4
-// loads are legal -> no per-element checks.
+// Edge tiles load at clamped in-bounds addresses and zero afterwards: a
+// load inside a per-row bounds branch made the compiler wait for each one
+// before the next (194 `s_waitcnt vmcnt(0)` for 356 loads in the 1x1
+// convolution kernel), so a partial tile -- every tile of a 64-wide
+// operand -- ran one memory round trip per row.
 __device__ __forceinline__ void load_kc(Stage& st, const float* __restrict__ P,
                                         const float* __restrict__ extra,
                                         int64_t ld, int rows, int r0,
                                         int kmain, int k0, bool vec) {
   const int t = threadIdx.x;
   const int c = k0 + (t & 7) * 4;
-  const bool full = vec && (r0 + GT <= rows) && (k0 + GK <= kmain);
-  if (full) {
+  if (vec && k0 + GK <= kmain) {
+    // whole k-tile inside the matrix: float4 loads at clamped rows
+    uint32_t ok = 0;
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const int r = r0 + (t >> 3) + 32 * p;
-      st.r[p] = gload4(P + (int64_t)r * ld + c);
+      ok |= (r < rows ? 1u : 0u) << p;
+      st.r[p] = gload4(P + (int64_t)(r < rows ? r : rows - 1) * ld + c);
     }
+    st.ok = ok;
     return;
   }
+  // k tail (or unaligned rows): scalar loads at clamped (row, k), the
+  // optional extra column k == kmain from its own vector
+  float tmp[4][4];
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
     const int r = r0 + (t >> 3) + 32 * p;
-    float tmp[4] = {0.f, 0.f, 0.f, 0.f};
-    if (r < rows) {
-      const float* row = P + (int64_t)r * ld;
-      if (vec && c + 3 < kmain) {
-        const float4 v = gload4(row + c);
-        tmp[0] = v.x; tmp[1] = v.y; tmp[2] = v.z; tmp[3] = v.w;
-      } else {
+    const int rc = r < rows ? r : rows - 1;
+    const float* row = P + (int64_t)rc * ld;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int k = c + e;
-          if (k < kmain) tmp[e] = gload(row + k);
-          else if (extra != nullptr && k == kmain) tmp[e] = gload(extra + r);
-        }
-      }
+    for (int e = 0; e < 4; ++e) {
+      const int k = c + e;
+      tmp[p][e] = gload(row + (k < kmain ? k : kmain - 1));
     }
-    st.r[p] = make_float4(tmp[0], tmp[1], tmp[2], tmp[3]);
   }
+  float ex[4] = {0.f, 0.f, 0.f, 0.f};
+  const bool has_extra = extra != nullptr && kmain >= c && kmain < c + 4;
+  if (has_extra) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int r = r0 + (t >> 3) + 32 * p;
+      ex[p] = gload(extra + (r < rows ? r : rows - 1));
+    }
+  }
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const bool rok = r0 + (t >> 3) + 32 * p < rows;
+    float o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = c + e;
+      o[e] = !rok ? 0.f : k < kmain ? tmp[p][e] : (has_extra && k == kmain) ? ex[p] : 0.f;
+    }
+    st.r[p] = make_float4(o[0], o[1], o[2], o[3]);
+  }
+  st.ok = 0xFu;
+}
+
+// The same loads for operands whose k-tiles are all whole and float4-able
+// (K % 32 == 0, 16-byte rows: every convolution GEMM): no scalar tail path
+// in the loop, whose register merge with the float4 path made the compiler
+// wait for the prefetch before the current k-tile's MFMAs.
+__device__ __forceinline__ void load_kc_v(Stage& st, const float* __restrict__ P, int64_t ld,
+                                          int rows, int r0, int k0) {
+  const int t = threadIdx.x;
+  const int c = k0 + (t & 7) * 4;
+  uint32_t ok = 0;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int r = r0 + (t >> 3) + 32 * p;
+    ok |= (r < rows ? 1u : 0u) << p;
+    st.r[p] = gload4(P + (int64_t)(r < rows ? r : rows - 1) * ld + c);
+  }
+  st.ok = ok;
+}
+
+__device__ __forceinline__ void load_mc_v(Stage& st, const float* __restrict__ P, int64_t ld,
+                                          int cols, int m0, int K, int k0) {
+  const int t = threadIdx.x;
+  const int m = m0 + (t & 31) * 4;
+  const bool cok = m < cols;
+  const int mc = cok ? m : cols - 4;
+  uint32_t ok = 0;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int k = k0 + (t >> 5) + 8 * p;
+    ok |= (cok && k < K ? 1u : 0u) << p;
+    st.r[p] = gload4(P + (int64_t)(k < K ? k : K - 1) * ld + mc);
+  }
+  st.ok = ok;
 }
 
 __device__ __forceinline__ void store_kc(const Stage& st, short* Lh, short* Ll) {
@@ -172,7 +236,7 @@ __device__ __forceinline__ void store_kc(const Stage& st, short* Lh, short* Ll) 
   for (int p = 0; p < 4; ++p) {
     const int r = (t >> 3) + 32 * p;
     v4i16 h, l;
-    split4(st.r[p], h, l);
+    split4(stage_get(st, p), h, l);
     *reinterpret_cast<v4i16*>(Lh + r * LDK + (t & 7) * 4) = h;
     *reinterpret_cast<v4i16*>(Ll + r * LDK + (t & 7) * 4) = l;
   }
@@ -180,37 +244,42 @@ __device__ __forceinline__ void store_kc(const Stage& st, short* Lh, short* Ll) 
 
 // m-contiguous operand: k-rows [k0, k0+32) of a [K][ld] matrix, columns
 // [m0, m0+128).  Thread t: chunk = t & 31 (4 columns), krow = (t >> 5) + 8p.
+// Clamped loads, masked afterwards (see load_kc).
 __device__ __forceinline__ void load_mc(Stage& st, const float* __restrict__ P,
                                         int64_t ld, int cols, int m0, int K,
                                         int k0, bool vec) {
   const int t = threadIdx.x;
   const int m = m0 + (t & 31) * 4;
-  const bool full = vec && (m0 + GT <= cols) && (k0 + GK <= K);
-  if (full) {
+  if (vec && (cols & 3) == 0) {
+    // columns come in whole float4 groups: a group is in or out
+    const bool cok = m < cols;
+    const int mc = cok ? m : cols - 4;
+    uint32_t ok = 0;
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const int k = k0 + (t >> 5) + 8 * p;
-      st.r[p] = gload4(P + (int64_t)k * ld + m);
+      ok |= (cok && k < K ? 1u : 0u) << p;
+      st.r[p] = gload4(P + (int64_t)(k < K ? k : K - 1) * ld + mc);
     }
+    st.ok = ok;
     return;
   }
+  float tmp[4][4];
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
     const int k = k0 + (t >> 5) + 8 * p;
-    float tmp[4] = {0.f, 0.f, 0.f, 0.f};
-    if (k < K) {
-      const float* row = P + (int64_t)k * ld;
-      if (vec && m + 3 < cols) {
-        const float4 v = gload4(row + m);
-        tmp[0] = v.x; tmp[1] = v.y; tmp[2] = v.z; tmp[3] = v.w;
-      } else {
+    const float* row = P + (int64_t)(k < K ? k : K - 1) * ld;
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (m + e < cols) tmp[e] = gload(row + m + e);
-      }
-    }
-    st.r[p] = make_float4(tmp[0], tmp[1], tmp[2], tmp[3]);
+    for (int e = 0; e < 4; ++e) tmp[p][e] = gload(row + (m + e < cols ? m + e : cols - 1));
   }
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const bool kok = k0 + (t >> 5) + 8 * p < K;
+    st.r[p] = make_float4(kok && m < cols ? tmp[p][0] : 0.f, kok && m + 1 < cols ? tmp[p][1] : 0.f,
+                          kok && m + 2 < cols ? tmp[p][2] : 0.f,
+                          kok && m + 3 < cols ? tmp[p][3] : 0.f);
+  }
+  st.ok = 0xFu;
 }
 
 __device__ __forceinline__ void store_mc(const Stage& st, short* Lh, short* Ll) {
@@ -219,7 +288,7 @@ __device__ __forceinline__ void store_mc(const Stage& st, short* Lh, short* Ll) 
   for (int p = 0; p < 4; ++p) {
     const int k = (t >> 5) + 8 * p;
     v4i16 h, l;
-    split4(st.r[p], h, l);
+    split4(stage_get(st, p), h, l);
     *reinterpret_cast<v4i16*>(Lh + k * LDM + (t & 31) * 4) = h;
     *reinterpret_cast<v4i16*>(Ll + k * LDM + (t & 31) * 4) = l;
   }
@@ -240,6 +309,7 @@ __device__ __forceinline__ void load_kc_hl(Stage& st, const float* __restrict__ 
     st.r[p] = (r < rows && c < kmain) ? gload4(P + (int64_t)r * ld + c)
                                       : make_float4(0.f, 0.f, 0.f, 0.f);
   }
+  st.ok = 0xFu;
 }
 
 __device__ __forceinline__ void load_mc_hl(Stage& st, const float* __restrict__ P, int64_t ld,
@@ -252,6 +322,7 @@ __device__ __forceinline__ void load_mc_hl(Stage& st, const float* __restrict__ 
     st.r[p] = (k < K && m < cols) ? gload4(P + (int64_t)k * ld + m)
                                   : make_float4(0.f, 0.f, 0.f, 0.f);
   }
+  st.ok = 0xFu;
 }
 
 __device__ __forceinline__ void unpack_hl(const float4 v, v4i16& hi, v4i16& lo) {
@@ -322,19 +393,15 @@ __device__ __forceinline__ void load_kc_conv(Stage& st, const float* __restrict_
   const int tap = k0 / g.C;
   const int c = k0 - tap * g.C + (threadIdx.x & 7) * 4;
   const int i = tap / g.kw, j = tap - i * g.kw;
-  bool ok[4];
-  int64_t off[4];
+  uint32_t ok = 0;
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
     const int hi = cr.hb[p] + i, wi = cr.wb[p] + j;
-    ok[p] = (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
-    off[p] = ok[p] ? ((int64_t)(cr.pix[p] + hi * g.W + wi)) * g.C + c : 0;
+    const bool in = (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
+    ok |= (in ? 1u : 0u) << p;
+    st.r[p] = gload4(X + (in ? ((int64_t)(cr.pix[p] + hi * g.W + wi)) * g.C + c : 0));
   }
-  float4 v[4];
-#pragma unroll
-  for (int p = 0; p < 4; ++p) v[p] = gload4(X + off[p]);
-#pragma unroll
-  for (int p = 0; p < 4; ++p) st.r[p] = ok[p] ? v[p] : make_float4(0.f, 0.f, 0.f, 0.f);
+  st.ok = ok;
 }
 
 // B of the stride-1 input gradient: the flipped, transposed kernel read in
@@ -350,15 +417,13 @@ __device__ __forceinline__ void load_mc_flipw(Stage& st, const float* __restrict
   const int co0 = k0 - tap * g.C + (t >> 5);
   const int64_t tapoff = (int64_t)((g.kh - 1 - i) * g.kw + (g.kw - 1 - j)) * ncols;
   const bool ok = n < ncols;  // ncols % 4 == 0 (host check)
-  float4 v[4];
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
     const int co = co0 + 8 * p;
     const int64_t off = ok ? (int64_t)co * g.kh * g.kw * ncols + tapoff + n : 0;
-    v[p] = gload4(Wt + off);
+    st.r[p] = gload4(Wt + off);
   }
-#pragma unroll
-  for (int p = 0; p < 4; ++p) st.r[p] = ok ? v[p] : make_float4(0.f, 0.f, 0.f, 0.f);
+  st.ok = ok ? 0xFu : 0u;
 }
 
 // fragment: lane l gets X[row = base + (l & 31)][k = kk + 8 (l >> 5) + 0..7]
@@ -394,7 +459,7 @@ __device__ __forceinline__ int gemm3_tile_of_block() {
 // one 128 x 128 output tile t of the GEMM described by d
 // k-tiles [kt_begin, kt_begin + kt_count) of the reduction (split-K
 // callers; kt_count < 0: to the end)
-template <bool A_KC, bool B_KC, bool CONV = false, bool FLIPW = false>
+template <bool A_KC, bool B_KC, bool CONV = false, bool FLIPW = false, bool FASTLD = false>
 __device__ __forceinline__ void gemm3_tile(const GemmDesc& d, int t, const PatchGeom& g = {},
                                            int kt_begin = 0, int kt_count = -1) {
   constexpr int A_SZ = A_KC ? GT * LDK : GK * LDM;
@@ -443,10 +508,15 @@ __device__ __forceinline__ void gemm3_tile(const GemmDesc& d, int t, const Patch
         sa.r[p] = make_float4(k0, 1.f, 2.f, 3.f);
         sb.r[p] = make_float4(k0, 1.f, 2.f, 3.f);
       }
+      sa.ok = sb.ok = 0xFu;
       return;
     }
     if constexpr (CONV) {
       load_kc_conv(sa, d.A, g, cr, k0);
+    } else if constexpr (FASTLD && A_KC) {
+      load_kc_v(sa, d.A, d.lda, d.M, m0, k0);
+    } else if constexpr (FASTLD) {
+      load_mc_v(sa, d.A, d.lda, d.M, m0, d.K, k0);
     } else if constexpr (A_KC) {
       if (a_hl) load_kc_hl(sa, (const float*)d.Ah, d.lda, d.M, m0, d.Kmain, k0);
       else load_kc(sa, d.A, d.A_extra, d.lda, d.M, m0, d.Kmain, k0, avec);
@@ -456,6 +526,10 @@ __device__ __forceinline__ void gemm3_tile(const GemmDesc& d, int t, const Patch
     }
     if constexpr (FLIPW) {
       load_mc_flipw(sb, d.B, g, d.N, n0, k0);
+    } else if constexpr (FASTLD && B_KC) {
+      load_kc_v(sb, d.B, d.ldb, d.N, n0, k0);
+    } else if constexpr (FASTLD) {
+      load_mc_v(sb, d.B, d.ldb, d.N, n0, d.K, k0);
     } else if constexpr (B_KC) {
       if (b_hl) load_kc_hl(sb, (const float*)d.Bh, d.ldb, d.N, n0, d.K, k0);
       else load_kc(sb, d.B, nullptr, d.ldb, d.N, n0, d.K, k0, bvec);
@@ -581,12 +655,12 @@ gemm3_kernel(const GemmDesc* __restrict__ descs, int nlayers, int total_tiles) {
 // one GEMM whose descriptor travels in the kernel arguments: no device
 // table to upload, so a launch is one graph-capturable kernel node (the
 // fp32 1x1 convolutions, ops/conv.py)
-template <bool A_KC, bool B_KC>
+template <bool A_KC, bool B_KC, bool FASTLD>
 __global__ void __launch_bounds__(GNT, 2)
 gemm3_single_kernel(const GemmDesc d, int total_tiles) {
   const int t = gemm3_tile_of_block();
   if (t >= total_tiles) return;
-  gemm3_tile<A_KC, B_KC>(d, t);
+  gemm3_tile<A_KC, B_KC, false, false, FASTLD>(d, t);
 }
 
 // implicit-GEMM convolution: C[N*Ho*Wo][Cout] = patches(x) . w^T, the
@@ -602,7 +676,7 @@ gemm3_conv_kernel(const GemmDesc d, const PatchGeom g, int tiles, int splits, in
   const int z = b / tiles;
   GemmDesc dz = d;
   dz.C = d.C + (int64_t)z * split_stride;
-  gemm3_tile<true, !FLIPW, true, FLIPW>(dz, b - z * tiles, g, z * kt_per, kt_per);
+  gemm3_tile<true, !FLIPW, true, FLIPW, true>(dz, b - z * tiles, g, z * kt_per, kt_per);
 }
 
 }  // namespace
@@ -628,10 +702,18 @@ void gemm3_single(const GemmDesc& d, bool a_kc, bool b_kc, hipStream_t s) {
   const int tiles = ((d.M + GT - 1) / GT) * d.tiles_n;
   if (tiles <= 0 || d.K <= 0) return;
   const dim3 grid((unsigned)gemm3_grid(tiles));
-  if (a_kc && b_kc) gemm3_single_kernel<true, true><<<grid, dim3(GNT), 0, s>>>(d, tiles);
-  else if (a_kc) gemm3_single_kernel<true, false><<<grid, dim3(GNT), 0, s>>>(d, tiles);
-  else if (b_kc) gemm3_single_kernel<false, true><<<grid, dim3(GNT), 0, s>>>(d, tiles);
-  else gemm3_single_kernel<false, false><<<grid, dim3(GNT), 0, s>>>(d, tiles);
+  // whole float4-able k-tiles and 4-aligned m-contiguous extents: the
+  // tail-free loaders
+  const bool fast = d.K % GK == 0 && d.vec == 3 && d.A_extra == nullptr &&
+                    (a_kc || d.M % 4 == 0) && (b_kc || d.N % 4 == 0);
+#define G3S(A, B)                                                                    \
+  (fast ? gemm3_single_kernel<A, B, true><<<grid, dim3(GNT), 0, s>>>(d, tiles)       \
+        : gemm3_single_kernel<A, B, false><<<grid, dim3(GNT), 0, s>>>(d, tiles))
+  if (a_kc && b_kc) G3S(true, true);
+  else if (a_kc) G3S(true, false);
+  else if (b_kc) G3S(false, true);
+  else G3S(false, false);
+#undef G3S
 }
 
 int gemm3_conv_splits(int N, int H, int W, int C, int Cout, int kh, int kw, int stride, int pad) {

@@ -363,7 +363,7 @@ def _implicit_ok(m: nn.Conv2d) -> bool:
     return (m.groups == 1 and tuple(m.dilation) == (1, 1) and m.padding_mode == 'zeros'
             and kh == kw and kh > 1 and isinstance(m.padding, tuple)
             and m.padding[0] == m.padding[1] and m.stride[0] == m.stride[1]
-            and m.in_channels % 32 == 0 and min(m.in_channels, m.out_channels) >= 128)
+            and m.in_channels % 32 == 0)
 
 
 class ImplicitGemmConv2d(nn.Conv2d):
@@ -373,10 +373,9 @@ class ImplicitGemmConv2d(nn.Conv2d):
     gradient run on the native implicit-GEMM kernel (``_ConvImplicit``,
     ``conv_kxk_math``; split-K over the 9 x C reduction when the image is
     too small to fill the chip).  ResNet-50 batch 32, per convolution:
-    forward 59-73 us vs MIOpen fp32's 105-179 us at 128-512 channels, the
-    64-channel stage stays on MIOpen (a 128-wide tile would be half empty,
-    ``use_implicit_gemm_conv`` skips it) -- profiles/r5/conv3x3_probe.jsonl,
-    bench 1760 -> 1835 img/s.  Same module,
+    forward 58-71 us vs MIOpen fp32's 105-178 us at 128-512 channels, 84 vs
+    90 us at 64 (profiles/r5/conv3x3_probe.jsonl); bench 1760 -> 1835 img/s
+    with the 3x3 convolutions native.  Same module,
     parameters and state-dict keys (K-FAC sees an ``nn.Conv2d``); bf16
     autocast, other layouts and the CPU take ``nn.Conv2d``'s path."""
 
