@@ -545,7 +545,8 @@ def main() -> None:
         kxk = conv_kxk_math() if args.conv_kxk == 'gemm' else 'fp32'
         line['model_math'] = {
             'conv1x1_fwd_dgrad': conv1x1_math() if args.dtype == 'fp32' else args.dtype,
-            'conv1x1_wgrad': 'fp32',
+            'conv1x1_wgrad': (conv1x1_math() if args.dtype == 'fp32' else args.dtype) +
+                             ' from 256x128 weights up, fp32 below',
             'conv3x3_fwd_dgrad_stride1': kxk if args.dtype == 'fp32' else args.dtype,
             'conv3x3_wgrad_and_strided_dgrad': 'fp32 (MIOpen)'}
     line['host_issue_ms'] = res['host_issue_ms']

@@ -77,7 +77,8 @@ void apply_multi(const LayerDesc* descs, int nlayers, int64_t total_blocks,
                  const float* scale, hipStream_t s);
 // gemm3.hip
 int gemm3_grid(int total_tiles);
-void gemm3_single(const GemmDesc& d, bool a_kc, bool b_kc, hipStream_t s);
+void gemm3_single(const GemmDesc& d, bool a_kc, bool b_kc, int splits, int64_t split_stride,
+                  hipStream_t s);
 int gemm3_conv_splits(int N, int H, int W, int C, int Cout, int kh, int kw, int stride, int pad);
 void gemm3_conv(const float* x, const float* w, float* y, int N, int H, int W, int C, int Cout,
                 int kh, int kw, int stride, int pad, int splits, bool flipw, hipStream_t s);
@@ -1047,19 +1048,41 @@ std::tuple<at::Tensor, int64_t, at::Tensor> build_gemm_table(
   return {dev_t, tiles, cpu};
 }
 
+// The split count gemm3_single actually uses for a K-long reduction asked
+// for `want` splits: equal whole-k-tile shares, none empty.
+int64_t gemm3_mm_splits_for(int64_t K, int64_t want) {
+  const int64_t kts = (K + 31) / 32;
+  int64_t sp = want < 1 ? 1 : (want > kts ? kts : want);
+  const int64_t per = (kts + sp - 1) / sp;
+  return (kts + per - 1) / per;
+}
+
 // One fp32 GEMM C[M,N] = A . B on bf16x3 MFMA (csrc/gemm3.hip), the
 // descriptor passed by value (no table upload: capturable as a single
 // kernel node).  a_kc: A is [M, K], else the stored [K, M]; b_kc: B is the
-// stored [N, K], else [K, N].  C is overwritten.
+// stored [N, K], else [K, N].  C is overwritten.  splits > 1: split-K, C is
+// [splits, M, N] and receives one partial product per split (the caller
+// sums them; k-tiles are shared out equally, see gemm3_mm_splits).
 void gemm3_mm(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, bool a_kc,
-              bool b_kc) {
-  for (const at::Tensor* t : {&A, &B, &C}) {
+              bool b_kc, int64_t splits) {
+  TORCH_CHECK(splits >= 1, "gemm3_mm: splits >= 1");
+  if (splits > 1) {
+    check_cuda(C, "gemm3_mm partials");
+    TORCH_CHECK(C.dim() == 3 && C.size(0) == splits && C.is_contiguous() &&
+                    C.scalar_type() == at::kFloat,
+                "gemm3_mm: split-K output must be a contiguous fp32 [splits, M, N]");
+    const int64_t kk = a_kc ? A.size(1) : A.size(0);
+    TORCH_CHECK(splits == gemm3_mm_splits_for(kk, splits),
+                "gemm3_mm: splits must come from gemm3_mm_splits");
+  }
+  const at::Tensor C2 = splits > 1 ? C[0] : C;
+  for (const at::Tensor* t : {&A, &B, &C2}) {
     check_cuda(*t, "gemm3_mm operand");
     TORCH_CHECK(t->scalar_type() == at::kFloat && t->dim() == 2 && t->stride(1) == 1,
                 "gemm3_mm: operands must be fp32 2-D with unit column stride");
   }
   TORCH_CHECK(A.device() == B.device() && A.device() == C.device(), "gemm3_mm: one device");
-  const int64_t M = C.size(0), N = C.size(1);
+  const int64_t M = C2.size(0), N = C2.size(1);
   const int64_t K = a_kc ? A.size(1) : A.size(0);
   TORCH_CHECK((a_kc ? A.size(0) : A.size(1)) == M, "gemm3_mm: A shape");
   TORCH_CHECK(b_kc ? (B.size(0) == N && B.size(1) == K) : (B.size(0) == K && B.size(1) == N),
@@ -1068,10 +1091,10 @@ void gemm3_mm(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, boo
   kfac::GemmDesc d{};
   d.A = A.data_ptr<float>();
   d.B = B.data_ptr<float>();
-  d.C = C.data_ptr<float>();
+  d.C = C2.data_ptr<float>();
   d.lda = A.stride(0);
   d.ldb = B.stride(0);
-  d.ldc = C.stride(0);
+  d.ldc = C2.stride(0);
   d.M = (int32_t)M;
   d.N = (int32_t)N;
   d.K = (int32_t)K;
@@ -1083,7 +1106,7 @@ void gemm3_mm(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, boo
     C.zero_();
     return;
   }
-  kfac::gemm3_single(d, a_kc, b_kc, cur_stream());
+  kfac::gemm3_single(d, a_kc, b_kc, (int)splits, M * N, cur_stream());
 }
 
 // Implicit-GEMM convolution on bf16x3 MFMA (csrc/gemm3.hip): x [N, C, H, W]
@@ -1387,7 +1410,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm3_conv", &gemm3_conv, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"),
         py::arg("flipw") = false);
   m.def("gemm3_mm", &gemm3_mm, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("a_kc"),
-        py::arg("b_kc"));
+        py::arg("b_kc"), py::arg("splits") = 1);
+  m.def("gemm3_mm_splits", &gemm3_mm_splits_for, py::arg("k"), py::arg("want"));
   m.def("gemm3s_align", &kfac::gemm3s_align);
   m.def("build_gemm3s_table", &build_gemm3s_table);
   m.def("gemm3s_grouped", &gemm3s_grouped);

@@ -655,12 +655,21 @@ gemm3_kernel(const GemmDesc* __restrict__ descs, int nlayers, int total_tiles) {
 // one GEMM whose descriptor travels in the kernel arguments: no device
 // table to upload, so a launch is one graph-capturable kernel node (the
 // fp32 1x1 convolutions, ops/conv.py)
+// split-K as gemm3_conv_kernel: block b covers tile b % tiles of split
+// b / tiles, whose partial goes to C + split * split_stride
 template <bool A_KC, bool B_KC, bool FASTLD>
 __global__ void __launch_bounds__(GNT, 2)
-gemm3_single_kernel(const GemmDesc d, int total_tiles) {
-  const int t = gemm3_tile_of_block();
-  if (t >= total_tiles) return;
-  gemm3_tile<A_KC, B_KC, false, false, FASTLD>(d, t);
+gemm3_single_kernel(const GemmDesc d, int tiles, int splits, int kt_per, int64_t split_stride) {
+  const int b = gemm3_tile_of_block();
+  if (b >= tiles * splits) return;
+  if (splits == 1) {
+    gemm3_tile<A_KC, B_KC, false, false, FASTLD>(d, b);
+    return;
+  }
+  const int z = b / tiles;
+  GemmDesc dz = d;
+  dz.C = d.C + (int64_t)z * split_stride;
+  gemm3_tile<A_KC, B_KC, false, false, FASTLD>(dz, b - z * tiles, {}, z * kt_per, kt_per);
 }
 
 // implicit-GEMM convolution: C[N*Ho*Wo][Cout] = patches(x) . w^T, the
@@ -698,17 +707,28 @@ void gemm3_grouped(const GemmDesc* table, int nlayers, int total_tiles,
   else gemm3_kernel<false, false><<<grid, dim3(GNT), 0, s>>>(table, nlayers, total_tiles);
 }
 
-void gemm3_single(const GemmDesc& d, bool a_kc, bool b_kc, hipStream_t s) {
+// splits > 1: d.C holds `splits` partial [M][ldc] outputs, split_stride
+// elements apart, each over an equal share of whole k-tiles (every split
+// non-empty: the host passes splits <= the k-tile count)
+void gemm3_single(const GemmDesc& d, bool a_kc, bool b_kc, int splits, int64_t split_stride,
+                  hipStream_t s) {
   const int tiles = ((d.M + GT - 1) / GT) * d.tiles_n;
   if (tiles <= 0 || d.K <= 0) return;
-  const dim3 grid((unsigned)gemm3_grid(tiles));
+  const int kts = (d.K + GK - 1) / GK;
+  if (splits < 1) splits = 1;
+  if (splits > kts) splits = kts;
+  const int per = (kts + splits - 1) / splits;
+  splits = (kts + per - 1) / per;
+  const dim3 grid((unsigned)gemm3_grid(tiles * splits));
   // whole float4-able k-tiles and 4-aligned m-contiguous extents: the
   // tail-free loaders
   const bool fast = d.K % GK == 0 && d.vec == 3 && d.A_extra == nullptr &&
                     (a_kc || d.M % 4 == 0) && (b_kc || d.N % 4 == 0);
 #define G3S(A, B)                                                                    \
-  (fast ? gemm3_single_kernel<A, B, true><<<grid, dim3(GNT), 0, s>>>(d, tiles)       \
-        : gemm3_single_kernel<A, B, false><<<grid, dim3(GNT), 0, s>>>(d, tiles))
+  (fast ? gemm3_single_kernel<A, B, true><<<grid, dim3(GNT), 0, s>>>(d, tiles, splits, per,  \
+                                                                       split_stride)        \
+        : gemm3_single_kernel<A, B, false><<<grid, dim3(GNT), 0, s>>>(d, tiles, splits, per, \
+                                                                        split_stride))
   if (a_kc && b_kc) G3S(true, true);
   else if (a_kc) G3S(true, false);
   else if (b_kc) G3S(false, true);

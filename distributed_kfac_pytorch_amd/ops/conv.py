@@ -159,7 +159,8 @@ def conv1x1_math() -> str:
     against 4.97 ms for fp32 hipBLASLt (profiles/r5/conv1x1_gemm3_probe.jsonl),
     except where K >= 1024 leaves fewer than 128 output tiles (hipBLASLt's
     split-K wins there, and keeps those).  The weight gradient (K = N*H*W)
-    stays hipBLASLt's slab-reduced fp32 GEMM either way.  ``fp32``:
+    runs split-K on the same kernel from 256 x 128 weights up
+    (``_wgrad_native``, ``KFAC_CONV1X1_WGRAD=lib`` for hipBLASLt's slabs).  ``fp32``:
     hipBLASLt for everything (exact fp32 products, the A/B setting)."""
     return os.environ.get('KFAC_CONV1X1_MATH', 'bf16x3').lower()
 
@@ -214,6 +215,24 @@ def _splitk(m: int, rows: int | None = None) -> int:
     return s
 
 
+def _wgrad_native(lib, gy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:  # type: ignore[no-untyped-def]
+    """``dW = dY^T X`` (fp32 [m, co] x [m, ci]) on the native bf16x3 GEMM
+    with split-K over the m = N*H*W rows: ~512 blocks of >= 8 k-tiles
+    each write fp32 partials, one fixed-order sum (deterministic)."""
+    m, co = gy.shape
+    ci = x.shape[1]
+    tiles = -(-co // 128) * -(-ci // 128)
+    want = max(1, min(-(-512 // tiles), (m // 32) // 8))
+    sp = int(lib.gemm3_mm_splits(m, want))
+    if sp == 1:
+        gw = torch.empty(co, ci, device=gy.device, dtype=gy.dtype)
+        lib.gemm3_mm(gy, x, gw, False, False)
+        return gw
+    part = torch.empty(sp, co, ci, device=gy.device, dtype=gy.dtype)
+    lib.gemm3_mm(gy, x, part, False, False, sp)
+    return part.sum(0)
+
+
 class _Conv1x1Gemm(torch.autograd.Function):
     """``Y = X W^T (+ b)`` on the NHWC activation matrix, with the weight
     gradient ``dW = dY^T X`` reduced in slabs: one GEMM with K = N*H*W
@@ -238,7 +257,14 @@ class _Conv1x1Gemm(torch.autograd.Function):
         gy = gy.contiguous()
         gx = _mm_nn(gy, w.contiguous()) if ctx.needs_input_grad[0] else None
         gw = None
-        if ctx.needs_input_grad[1]:
+        lib = _gemm3_lib(gy, x) if ctx.needs_input_grad[1] else None
+        # native split-K from 256 x 128 weights up (51 vs 61 us there, 44 vs
+        # 56-58 at 512 x 256 / 1024 x 512); hipBLASLt's slabs keep the small
+        # 64-channel weights (37 vs 48 us): profiles/r5/conv1x1_gemm3_probe.jsonl
+        if (lib is not None and os.environ.get('KFAC_CONV1X1_WGRAD', 'native') == 'native'
+                and gy.shape[1] * x.shape[1] >= 32768):
+            gw = _wgrad_native(lib, gy, x)
+        elif ctx.needs_input_grad[1]:
             m = gy.shape[0]
             s = _splitk(m)
             if s > 1:

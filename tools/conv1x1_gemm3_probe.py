@@ -23,6 +23,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from distributed_kfac_pytorch_amd.ops._native import native  # noqa: E402
 from distributed_kfac_pytorch_amd.ops.conv import _splitk  # noqa: E402
+from distributed_kfac_pytorch_amd.ops.conv import _wgrad_native  # noqa: E402
 from tools.conv1x1_probe import shapes  # noqa: E402
 from tools.conv1x1_probe import timed  # noqa: E402
 
@@ -81,9 +82,8 @@ def main() -> None:
         def g3_x() -> None:
             lib.gemm3_mm(gy, wt, dx3, True, False)
 
-        def g3_w() -> None:
-            g3(tw)
-            part.sum(0)
+        def g3_w() -> None:  # split-K native weight gradient (ops/conv.py)
+            _wgrad_native(lib, gy, x)
 
         g3_f(), g3_x(), g3(tw)
         torch.cuda.synchronize()
@@ -92,7 +92,7 @@ def main() -> None:
         err_lib = [rel(F.linear(x, wt), ref[0]), rel(gy @ wt, ref[1]),
                    rel(torch.bmm(gy.view(s, rows, co).transpose(1, 2),
                                  x.view(s, rows, ci)).sum(0), ref[2])]
-        err_g3 = [rel(y3, ref[0]), rel(dx3, ref[1]), rel(part.sum(0), ref[2])]
+        err_g3 = [rel(y3, ref[0]), rel(dx3, ref[1]), rel(_wgrad_native(lib, gy, x), ref[2])]
         t_lib = [timed(f) for f in (lib_f, lib_x, lib_w)]
         t_g3 = [timed(f) for f in (g3_f, g3_x, g3_w)]
         tot['lib'] += cnt * sum(t_lib)
