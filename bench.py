@@ -547,8 +547,8 @@ def main() -> None:
             'conv1x1_fwd_dgrad': conv1x1_math() if args.dtype == 'fp32' else args.dtype,
             'conv1x1_wgrad': (conv1x1_math() if args.dtype == 'fp32' else args.dtype) +
                              ' from 256x128 weights up, fp32 below',
-            'conv3x3_fwd_dgrad_stride1': kxk if args.dtype == 'fp32' else args.dtype,
-            'conv3x3_wgrad_and_strided_dgrad': 'fp32 (MIOpen)'}
+            'conv3x3_fwd_dgrad_stride1_wgrad_ge128ch': kxk if args.dtype == 'fp32' else args.dtype,
+            'conv3x3_strided_dgrad_64ch_wgrad_stem': 'fp32 (MIOpen)'}
     line['host_issue_ms'] = res['host_issue_ms']
     if base is not None:
         line['sgd_host_issue_ms'] = base['host_issue_ms']

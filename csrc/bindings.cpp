@@ -80,6 +80,9 @@ int gemm3_grid(int total_tiles);
 void gemm3_single(const GemmDesc& d, bool a_kc, bool b_kc, int splits, int64_t split_stride,
                   hipStream_t s);
 int gemm3_conv_splits(int N, int H, int W, int C, int Cout, int kh, int kw, int stride, int pad);
+int gemm3_wgrad_splits(int pixels, int Cout, int kcols);
+void gemm3_conv_wgrad(const float* x, const float* dy, float* dw, int N, int H, int W, int C,
+                      int Cout, int kh, int kw, int stride, int pad, int splits, hipStream_t s);
 void gemm3_conv(const float* x, const float* w, float* y, int N, int H, int W, int C, int Cout,
                 int kh, int kw, int stride, int pad, int splits, bool flipw, hipStream_t s);
 void gemm3_grouped(const GemmDesc* table, int nlayers, int total_tiles,
@@ -1153,6 +1156,35 @@ at::Tensor gemm3_conv(const at::Tensor& x, const at::Tensor& w, int64_t stride, 
   return y;
 }
 
+// Weight gradient of gemm3_conv: x [N, C, H, W] and dy [N, Cout, Ho, Wo]
+// channels_last fp32 (C % 4 == 0, Cout % 4 == 0); returns dw [Cout, C, kh,
+// kw] channels_last (split-K partials summed in fixed order).
+at::Tensor gemm3_conv_wgrad(const at::Tensor& x, const at::Tensor& dy, int64_t kh, int64_t kw,
+                            int64_t stride, int64_t pad) {
+  check_cuda(x, "gemm3_conv_wgrad x");
+  check_cuda(dy, "gemm3_conv_wgrad dy");
+  TORCH_CHECK(x.scalar_type() == at::kFloat && dy.scalar_type() == at::kFloat && x.dim() == 4 &&
+                  dy.dim() == 4, "gemm3_conv_wgrad: fp32 4-D operands");
+  TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  dy.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "gemm3_conv_wgrad: channels_last operands");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int64_t Co = dy.size(1), Ho = dy.size(2), Wo = dy.size(3);
+  TORCH_CHECK(dy.size(0) == N && Ho == (H + 2 * pad - kh) / stride + 1 &&
+                  Wo == (W + 2 * pad - kw) / stride + 1, "gemm3_conv_wgrad: geometry");
+  TORCH_CHECK(C % 4 == 0 && Co % 4 == 0, "gemm3_conv_wgrad: channels must be multiples of 4");
+  TORCH_CHECK(N * Ho * Wo < (1 << 22) && N * H * W * C < (1LL << 31),
+              "gemm3_conv_wgrad: too large");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  const int sp = kfac::gemm3_wgrad_splits((int)(N * Ho * Wo), (int)Co, (int)(kh * kw * C));
+  auto part = at::empty({sp, Co, kh * kw * C}, x.options());
+  kfac::gemm3_conv_wgrad(x.data_ptr<float>(), dy.data_ptr<float>(), part.data_ptr<float>(),
+                         (int)N, (int)H, (int)W, (int)C, (int)Co, (int)kh, (int)kw, (int)stride,
+                         (int)pad, sp, cur_stream());
+  auto dw = sp > 1 ? part.sum(0) : part[0];
+  return dw.view({Co, kh, kw, C}).permute({0, 3, 1, 2});
+}
+
 void gemm3_grouped(const at::Tensor& table, int64_t nlayers, int64_t total_tiles,
                    bool a_kc, bool b_kc) {
   check_cuda(table, "table");
@@ -1407,6 +1439,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("A_hls") = std::vector<c10::optional<at::Tensor>>(),
         py::arg("B_hls") = std::vector<c10::optional<at::Tensor>>());
   m.def("gemm3_grouped", &gemm3_grouped);
+  m.def("gemm3_conv_wgrad", &gemm3_conv_wgrad, py::arg("x"), py::arg("dy"), py::arg("kh"),
+        py::arg("kw"), py::arg("stride"), py::arg("pad"));
   m.def("gemm3_conv", &gemm3_conv, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"),
         py::arg("flipw") = false);
   m.def("gemm3_mm", &gemm3_mm, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("a_kc"),

@@ -426,6 +426,46 @@ __device__ __forceinline__ void load_mc_flipw(Stage& st, const float* __restrict
   st.ok = ok ? 0xFu : 0u;
 }
 
+// B of a weight gradient: the patch matrix as [K = N*Ho*Wo pixels][n =
+// (tap, c)] rows (n-contiguous), gathered from the NHWC input.  Each k-row
+// is decoded to (image, ho, wo) by a float reciprocal with an exact integer
+// fix-up (pixel counts < 2^22); c % 4 == 0, so a thread's 4 columns share
+// one tap.
+__device__ __forceinline__ int fdivmod(int a, int b, float inv, int& r) {
+  int q = __float2int_rz((float)a * inv);
+  r = a - q * b;
+  if (r < 0) { --q; r += b; }
+  else if (r >= b) { ++q; r -= b; }
+  return q;
+}
+
+__device__ __forceinline__ void load_mc_patch(Stage& st, const float* __restrict__ X,
+                                              const PatchGeom& g, int ncols, int n0, int K,
+                                              int k0) {
+  const int t = threadIdx.x;
+  const int n = n0 + (t & 31) * 4;
+  const bool cok = n < ncols;
+  const int nn = cok ? n : 0;
+  const int tap = nn / g.C;
+  const int c = nn - tap * g.C;
+  const int i = tap / g.kw, j = tap - i * g.kw;
+  const float inv_wo = 1.f / (float)g.Wo, inv_ho = 1.f / (float)g.Ho;
+  uint32_t ok = 0;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int k = k0 + (t >> 5) + 8 * p;
+    const int kc = k < K ? k : K - 1;
+    int wo, ho;
+    const int q = fdivmod(kc, g.Wo, inv_wo, wo);
+    const int img = fdivmod(q, g.Ho, inv_ho, ho);
+    const int hi = ho * g.stride - g.pad + i, wi = wo * g.stride - g.pad + j;
+    const bool in = cok && k < K && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
+    ok |= (in ? 1u : 0u) << p;
+    st.r[p] = gload4(X + (in ? ((int64_t)((img * g.H + hi) * g.W + wi)) * g.C + c : 0));
+  }
+  st.ok = ok;
+}
+
 // fragment: lane l gets X[row = base + (l & 31)][k = kk + 8 (l >> 5) + 0..7]
 __device__ __forceinline__ v8bf16 frag_kc(const short* L, int base, int kk) {
   const int l = threadIdx.x & 63;
@@ -459,7 +499,8 @@ __device__ __forceinline__ int gemm3_tile_of_block() {
 // one 128 x 128 output tile t of the GEMM described by d
 // k-tiles [kt_begin, kt_begin + kt_count) of the reduction (split-K
 // callers; kt_count < 0: to the end)
-template <bool A_KC, bool B_KC, bool CONV = false, bool FLIPW = false, bool FASTLD = false>
+template <bool A_KC, bool B_KC, bool CONV = false, bool FLIPW = false, bool FASTLD = false,
+          bool PATCHB = false>
 __device__ __forceinline__ void gemm3_tile(const GemmDesc& d, int t, const PatchGeom& g = {},
                                            int kt_begin = 0, int kt_count = -1) {
   constexpr int A_SZ = A_KC ? GT * LDK : GK * LDM;
@@ -524,7 +565,9 @@ __device__ __forceinline__ void gemm3_tile(const GemmDesc& d, int t, const Patch
       if (a_hl) load_mc_hl(sa, (const float*)d.Ah, d.lda, d.M, m0, d.K, k0);
       else load_mc(sa, d.A, d.lda, d.M, m0, d.K, k0, avec);
     }
-    if constexpr (FLIPW) {
+    if constexpr (PATCHB) {
+      load_mc_patch(sb, d.B, g, d.N, n0, d.K, k0);
+    } else if constexpr (FLIPW) {
       load_mc_flipw(sb, d.B, g, d.N, n0, k0);
     } else if constexpr (FASTLD && B_KC) {
       load_kc_v(sb, d.B, d.ldb, d.N, n0, k0);
@@ -688,6 +731,19 @@ gemm3_conv_kernel(const GemmDesc d, const PatchGeom g, int tiles, int splits, in
   gemm3_tile<true, !FLIPW, true, FLIPW, true>(dz, b - z * tiles, g, z * kt_per, kt_per);
 }
 
+// weight gradient of the implicit-GEMM convolution: dW[Co][(tap, c)] =
+// dy^T . patches(x), split-K over the pixels
+__global__ void __launch_bounds__(GNT, 2)
+gemm3_wgrad_kernel(const GemmDesc d, const PatchGeom g, int tiles, int splits, int kt_per,
+                   int64_t split_stride) {
+  const int b = gemm3_tile_of_block();
+  if (b >= tiles * splits) return;
+  const int z = b / tiles;
+  GemmDesc dz = d;
+  dz.C = d.C + (int64_t)z * split_stride;
+  gemm3_tile<false, false, false, false, true, true>(dz, b - z * tiles, g, z * kt_per, kt_per);
+}
+
 }  // namespace
 
 int gemm3_tile_edge() { return GT; }
@@ -784,6 +840,42 @@ void gemm3_conv(const float* x, const float* w, float* y, int N, int H, int W, i
     gemm3_conv_kernel<false><<<dim3((unsigned)gemm3_grid(tiles * splits)), dim3(GNT), 0, s>>>(
         d, g, tiles, splits, per, (int64_t)d.M * Cout);
   }
+}
+
+int gemm3_wgrad_splits(int pixels, int Cout, int kcols) {
+  const int tiles = ((Cout + GT - 1) / GT) * ((kcols + GT - 1) / GT);
+  const int kts = (pixels + GK - 1) / GK;
+  int sp = (512 + tiles - 1) / tiles;
+  if (sp > kts / 8) sp = kts / 8;
+  if (sp < 1) sp = 1;
+  const int per = (kts + sp - 1) / sp;
+  return (kts + per - 1) / per;
+}
+
+// dw: [splits][Cout][kh*kw*C] partials (splits from gemm3_wgrad_splits)
+void gemm3_conv_wgrad(const float* x, const float* dy, float* dw, int N, int H, int W, int C,
+                      int Cout, int kh, int kw, int stride, int pad, int splits, hipStream_t s) {
+  const int Ho = (H + 2 * pad - kh) / stride + 1;
+  const int Wo = (W + 2 * pad - kw) / stride + 1;
+  GemmDesc d{};
+  d.A = dy;
+  d.B = x;
+  d.C = dw;
+  d.lda = Cout;
+  d.ldb = 0;
+  d.ldc = (int64_t)kh * kw * C;
+  d.M = Cout;
+  d.N = kh * kw * C;
+  d.K = N * Ho * Wo;
+  d.Kmain = d.K;
+  d.tiles_n = (d.N + GT - 1) / GT;
+  d.vec = 3;
+  const PatchGeom g{H, W, C, Ho, Wo, kw, stride, pad, kh};
+  const int tiles = ((d.M + GT - 1) / GT) * d.tiles_n;
+  const int kts = (d.K + GK - 1) / GK;
+  const int per = (kts + splits - 1) / splits;
+  gemm3_wgrad_kernel<<<dim3((unsigned)gemm3_grid(tiles * splits)), dim3(GNT), 0, s>>>(
+      d, g, tiles, splits, per, (int64_t)d.M * d.N);
 }
 
 }  // namespace kfac

@@ -341,10 +341,11 @@ def conv_kxk_math() -> str:
 
 
 class _ConvImplicit(torch.autograd.Function):
-    """``y = conv2d(x, w, b, stride, pad)`` with the forward -- and, at
-    stride 1, the input gradient as the convolution of ``dy`` with the
-    flipped, transposed kernel -- on the native implicit GEMM; the weight
-    gradient (and a strided input gradient) through MIOpen's
+    """``y = conv2d(x, w, b, stride, pad)`` with the forward, the input
+    gradient at stride 1 (the convolution of ``dy`` with the flipped,
+    transposed kernel, read in place) and the weight gradient
+    (``dy^T . patches(x)``, split-K) on the native implicit GEMM; strided
+    input gradients (and 64-channel weight gradients) through MIOpen's
     ``convolution_backward``."""
 
     @staticmethod
@@ -372,13 +373,23 @@ class _ConvImplicit(torch.autograd.Function):
             # the flipped, transposed kernel is read in place (flipw)
             gx = lib.gemm3_conv(gy, w.contiguous(memory_format=torch.channels_last), 1,
                                 k - 1 - pad, True)
-        mask = [ctx.needs_input_grad[0] and not native_dx, ctx.needs_input_grad[1], False]
+        # native weight gradient (split-K over the pixels) from 128 input
+        # channels up: 54-71 us vs MIOpen's 85-87; at 64 MIOpen's 85 beats
+        # 96 (profiles/r5/conv3x3_probe.jsonl)
+        native_dw = (ctx.needs_input_grad[1] and x.shape[1] >= 128 and x.shape[1] % 4 == 0
+                     and w.shape[0] % 4 == 0
+                     and os.environ.get('KFAC_CONV_KXK_WGRAD', 'native') == 'native')
+        if native_dw:
+            gw = lib.gemm3_conv_wgrad(x, gy, k, w.shape[3], stride, pad)
+        mask = [ctx.needs_input_grad[0] and not native_dx,
+                ctx.needs_input_grad[1] and not native_dw, False]
         if any(mask):
             r = torch.ops.aten.convolution_backward(
                 gy, x, w, None, [stride, stride], [pad, pad], [1, 1], False, [0, 0], 1, mask)
             if mask[0]:
                 gx = r[0]
-            gw = r[1]
+            if mask[1]:
+                gw = r[1]
         if has_bias and ctx.needs_input_grad[2]:
             gb = gy.sum((0, 2, 3))
         return gx, gw, gb, None, None, None

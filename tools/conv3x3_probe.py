@@ -81,6 +81,12 @@ def main() -> None:
             nat['fwd_err'] = f'{float((yn.double() - ref).norm() / ref.norm()):.1e}'
             nat['fwd_err_miopen'] = f'{float((y.double() - ref).norm() / ref.norm()):.1e}'
             nat['fwd_us'] = round(timed(lambda: lib.gemm3_conv(x, wc, s, p)), 1)
+            dw = lib.gemm3_conv_wgrad(x, gy, k, k, s, p)
+            refw = torch.ops.aten.convolution_backward(
+                gy.double(), x.double(), wt.double(), None, [s, s], [p, p], [1, 1], False,
+                [0, 0], 1, [False, True, False])[1]
+            nat['wgrad_err'] = f'{float((dw.double() - refw).norm() / refw.norm()):.1e}'
+            nat['wgrad_us'] = round(timed(lambda: lib.gemm3_conv_wgrad(x, gy, k, k, s, p)), 1)
             if s == 1 and co % 32 == 0:
                 def nat_dgrad() -> torch.Tensor:
                     return lib.gemm3_conv(gy, wc, 1, k - 1 - p, True)
