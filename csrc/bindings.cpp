@@ -1113,8 +1113,8 @@ void gemm3_mm(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, boo
 }
 
 // Implicit-GEMM convolution on bf16x3 MFMA (csrc/gemm3.hip): x [N, C, H, W]
-// and w [Cout, C, kh, kw] both channels_last fp32, C % 32 == 0, no
-// dilation or groups; returns y [N, Cout, Ho, Wo] channels_last.
+// and w [Cout, C, kh, kw] both channels_last fp32, C % 4 == 0 (% 32 with
+// flipw), no dilation or groups; returns y [N, Cout, Ho, Wo] channels_last.
 // flipw: w is a stride-1 forward weight [Cf, Cout, kh, kw] (Cf = x's C) and
 // the convolution applied is its flipped transpose -- the input gradient of
 // that convolution when x is dy (pad = kh - 1 - forward pad).
@@ -1129,8 +1129,8 @@ at::Tensor gemm3_conv(const at::Tensor& x, const at::Tensor& w, int64_t stride, 
               "gemm3_conv: channels_last operands");
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
   const int64_t Co = flipw ? w.size(1) : w.size(0), kh = w.size(2), kw = w.size(3);
-  TORCH_CHECK((flipw ? w.size(0) : w.size(1)) == C && C % 32 == 0,
-              "gemm3_conv: C must match and be a multiple of 32");
+  TORCH_CHECK((flipw ? w.size(0) : w.size(1)) == C && C % 4 == 0 && (!flipw || C % 32 == 0),
+              "gemm3_conv: C must match and be a multiple of 4 (32 with flipw)");
   TORCH_CHECK(!flipw || (stride == 1 && Co % 4 == 0), "gemm3_conv: flipw needs stride 1");
   TORCH_CHECK(stride >= 1 && pad >= 0 && kh >= 1 && kw >= 1, "gemm3_conv: geometry");
   const int64_t Ho = (H + 2 * pad - kh) / stride + 1, Wo = (W + 2 * pad - kw) / stride + 1;

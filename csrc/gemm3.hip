@@ -388,16 +388,22 @@ __device__ __forceinline__ void conv_rows(ConvRows& cr, const PatchGeom& g, int 
   }
 }
 
+// (C % 4 == 0 in general: a thread's 4 channels lie in one tap; with C %
+// 32 != 0 -- the 4-channel padded stem -- a k-tile spans several taps and
+// k may run past K in the last tile)
 __device__ __forceinline__ void load_kc_conv(Stage& st, const float* __restrict__ X,
-                                             const PatchGeom& g, const ConvRows& cr, int k0) {
-  const int tap = k0 / g.C;
-  const int c = k0 - tap * g.C + (threadIdx.x & 7) * 4;
+                                             const PatchGeom& g, const ConvRows& cr, int k0,
+                                             int K) {
+  const int kk = k0 + (threadIdx.x & 7) * 4;
+  const int tap = kk / g.C;
+  const int c = kk - tap * g.C;
   const int i = tap / g.kw, j = tap - i * g.kw;
+  const bool kok = kk < K;
   uint32_t ok = 0;
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
     const int hi = cr.hb[p] + i, wi = cr.wb[p] + j;
-    const bool in = (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
+    const bool in = kok && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
     ok |= (in ? 1u : 0u) << p;
     st.r[p] = gload4(X + (in ? ((int64_t)(cr.pix[p] + hi * g.W + wi)) * g.C + c : 0));
   }
@@ -553,7 +559,7 @@ __device__ __forceinline__ void gemm3_tile(const GemmDesc& d, int t, const Patch
       return;
     }
     if constexpr (CONV) {
-      load_kc_conv(sa, d.A, g, cr, k0);
+      load_kc_conv(sa, d.A, g, cr, k0, d.K);
     } else if constexpr (FASTLD && A_KC) {
       load_kc_v(sa, d.A, d.lda, d.M, m0, k0);
     } else if constexpr (FASTLD) {
@@ -719,7 +725,7 @@ gemm3_single_kernel(const GemmDesc d, int tiles, int splits, int kt_per, int64_t
 // descriptor and the geometry by value
 // split-K: block b covers tile (b' % tiles) of split (b' / tiles) and
 // writes its partial sum to C + split * split_stride (the host sums them)
-template <bool FLIPW>
+template <bool FLIPW, bool FASTB>
 __global__ void __launch_bounds__(GNT, 2)
 gemm3_conv_kernel(const GemmDesc d, const PatchGeom g, int tiles, int splits, int kt_per,
                   int64_t split_stride) {
@@ -728,7 +734,7 @@ gemm3_conv_kernel(const GemmDesc d, const PatchGeom g, int tiles, int splits, in
   const int z = b / tiles;
   GemmDesc dz = d;
   dz.C = d.C + (int64_t)z * split_stride;
-  gemm3_tile<true, !FLIPW, true, FLIPW, true>(dz, b - z * tiles, g, z * kt_per, kt_per);
+  gemm3_tile<true, !FLIPW, true, FLIPW, FASTB>(dz, b - z * tiles, g, z * kt_per, kt_per);
 }
 
 // weight gradient of the implicit-GEMM convolution: dW[Co][(tap, c)] =
@@ -832,13 +838,17 @@ void gemm3_conv(const float* x, const float* w, float* y, int N, int H, int W, i
   if (tiles <= 0) return;
   const int kts = (d.K + GK - 1) / GK;
   const int per = (kts + splits - 1) / splits;
-  if (flipw) {
+  const dim3 grid((unsigned)gemm3_grid(tiles * splits));
+  if (flipw) {  // host: C % 32 == 0 (whole taps per k-tile)
     d.ldb = Cout;
-    gemm3_conv_kernel<true><<<dim3((unsigned)gemm3_grid(tiles * splits)), dim3(GNT), 0, s>>>(
-        d, g, tiles, splits, per, (int64_t)d.M * Cout);
+    gemm3_conv_kernel<true, true><<<grid, dim3(GNT), 0, s>>>(d, g, tiles, splits, per,
+                                                             (int64_t)d.M * Cout);
+  } else if (d.K % GK == 0) {
+    gemm3_conv_kernel<false, true><<<grid, dim3(GNT), 0, s>>>(d, g, tiles, splits, per,
+                                                              (int64_t)d.M * Cout);
   } else {
-    gemm3_conv_kernel<false><<<dim3((unsigned)gemm3_grid(tiles * splits)), dim3(GNT), 0, s>>>(
-        d, g, tiles, splits, per, (int64_t)d.M * Cout);
+    gemm3_conv_kernel<false, false><<<grid, dim3(GNT), 0, s>>>(d, g, tiles, splits, per,
+                                                               (int64_t)d.M * Cout);
   }
 }
 

@@ -355,7 +355,8 @@ class _ConvImplicit(torch.autograd.Function):
     ) -> torch.Tensor:
         ctx.save_for_backward(x, w)
         ctx.conf = (stride, pad, b is not None, lib)
-        y = lib.gemm3_conv(x, w.contiguous(memory_format=torch.channels_last), stride, pad)
+        y = lib.gemm3_conv(_pad4(x), _pad4(w).contiguous(memory_format=torch.channels_last),
+                           stride, pad)
         if b is not None:
             y.add_(b.view(1, -1, 1, 1))
         return y
@@ -368,7 +369,7 @@ class _ConvImplicit(torch.autograd.Function):
         k = w.shape[2]
         gx = gw = gb = None
         native_dx = (ctx.needs_input_grad[0] and stride == 1 and k - 1 - pad >= 0
-                     and w.shape[0] % 32 == 0)
+                     and w.shape[0] % 32 == 0 and x.shape[1] % 4 == 0)
         if native_dx:
             # the flipped, transposed kernel is read in place (flipw)
             gx = lib.gemm3_conv(gy, w.contiguous(memory_format=torch.channels_last), 1,
@@ -376,11 +377,12 @@ class _ConvImplicit(torch.autograd.Function):
         # native weight gradient (split-K over the pixels) from 128 input
         # channels up: 54-71 us vs MIOpen's 85-87; at 64 MIOpen's 85 beats
         # 96 (profiles/r5/conv3x3_probe.jsonl)
-        native_dw = (ctx.needs_input_grad[1] and x.shape[1] >= 128 and x.shape[1] % 4 == 0
+        native_dw = (ctx.needs_input_grad[1] and (x.shape[1] >= 128 or x.shape[1] < 4)
                      and w.shape[0] % 4 == 0
                      and os.environ.get('KFAC_CONV_KXK_WGRAD', 'native') == 'native')
         if native_dw:
-            gw = lib.gemm3_conv_wgrad(x, gy, k, w.shape[3], stride, pad)
+            gw = lib.gemm3_conv_wgrad(_pad4(x), gy, k, w.shape[3], stride, pad)
+            gw = gw[:, :x.shape[1]]
         mask = [ctx.needs_input_grad[0] and not native_dx,
                 ctx.needs_input_grad[1] and not native_dw, False]
         if any(mask):
@@ -395,18 +397,32 @@ class _ConvImplicit(torch.autograd.Function):
         return gx, gw, gb, None, None, None
 
 
+def _pad4(t: torch.Tensor) -> torch.Tensor:
+    """Zero-pad dim 1 (channels) of an NCHW-shaped tensor to a multiple of 4
+    (the 3-channel stem: one pixel's channels = one float4), channels_last."""
+    c = t.shape[1]
+    if c % 4 == 0:
+        return t
+    z = t.new_zeros(t.shape[0], 4 - c % 4, *t.shape[2:])
+    return torch.cat([t, z], 1).contiguous(memory_format=torch.channels_last)
+
+
 def _implicit_ok(m: nn.Conv2d) -> bool:
     kh, kw = m.kernel_size
     return (m.groups == 1 and tuple(m.dilation) == (1, 1) and m.padding_mode == 'zeros'
             and kh == kw and kh > 1 and isinstance(m.padding, tuple)
             and m.padding[0] == m.padding[1] and m.stride[0] == m.stride[1]
-            and m.in_channels % 32 == 0)
+            # the 3-channel stem runs (4-channel padded) but slower than
+            # MIOpen's: bench 1932 vs 1942-1950 img/s with it switched
+            and m.in_channels % 4 == 0)
 
 
 class ImplicitGemmConv2d(nn.Conv2d):
     """``nn.Conv2d`` (square kernel > 1, symmetric stride / padding, no
-    groups or dilation, ``in_channels % 32 == 0``: ResNet's 3x3
-    convolutions) whose fp32 channels_last forward and stride-1 input
+    groups or dilation: ResNet's 3x3 convolutions; a channel count that is
+    not a multiple of 4 is zero-padded, but ``use_implicit_gemm_conv`` leaves
+    the 3-channel stem to MIOpen, which is faster there) whose fp32
+    channels_last forward and stride-1 input
     gradient run on the native implicit-GEMM kernel (``_ConvImplicit``,
     ``conv_kxk_math``; split-K over the 9 x C reduction when the image is
     too small to fill the chip).  ResNet-50 batch 32, per convolution:

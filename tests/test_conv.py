@@ -179,14 +179,19 @@ def test_gemm_conv1x1_fp32_native_matches_float64(cuda, shape, stride, monkeypat
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('shape,stride', [((8, 64, 56, 56, 64), 1), ((8, 128, 56, 56, 128), 2),
-                                          ((32, 512, 7, 7, 512), 1), ((2, 96, 11, 13, 40), 1)])
-def test_implicit_gemm_conv_matches_float64(cuda, shape, stride, monkeypatch) -> None:
-    """fp32 ``ImplicitGemmConv2d`` (3x3, pad 1): forward on the native
-    implicit GEMM (split-K on small images), stride-1 input gradient as the
-    native convolution of dy with the flipped kernel, weight gradient from
-    MIOpen -- output and both gradients match float64 to fp32-class
-    accuracy, and the native kernel runs."""
+@pytest.mark.parametrize('shape,stride,k', [((8, 64, 56, 56, 64), 1, 3), ((8, 128, 56, 56, 128), 2, 3),
+                                            ((32, 512, 7, 7, 512), 1, 3),
+                                            ((2, 96, 11, 13, 40), 1, 3),
+                                            ((4, 3, 64, 64, 64), 2, 7),
+                                            ((4, 256, 14, 14, 256), 1, 3)])
+def test_implicit_gemm_conv_matches_float64(cuda, shape, stride, k, monkeypatch) -> None:
+    """fp32 ``ImplicitGemmConv2d`` (3x3 pad 1, and the 7x7 stride-2 stem
+    with its 3 channels padded to 4): forward on the native implicit GEMM
+    (split-K on small images), stride-1 input gradient as the native
+    convolution of dy with the flipped kernel, weight gradient native from
+    128 channels (and for the stem), MIOpen otherwise -- output and both
+    gradients match float64 to fp32-class accuracy, and the native kernel
+    runs."""
     from distributed_kfac_pytorch_amd.ops import _native
     from distributed_kfac_pytorch_amd.ops.conv import ImplicitGemmConv2d
 
@@ -207,7 +212,7 @@ def test_implicit_gemm_conv_matches_float64(cuda, shape, stride, monkeypatch) ->
     monkeypatch.setenv('KFAC_CONV_KXK_MATH', 'bf16x3')
     n, c, h, w, co = shape
     torch.manual_seed(0)
-    conv = nn.Conv2d(c, co, 3, stride=stride, padding=1, bias=True).to(cuda)
+    conv = nn.Conv2d(c, co, k, stride=stride, padding=k // 2, bias=True).to(cuda)
     conv = conv.to(memory_format=torch.channels_last)
     conv.__class__ = ImplicitGemmConv2d
     x = torch.randn(n, c, h, w, device=cuda).contiguous(memory_format=torch.channels_last)
@@ -215,11 +220,11 @@ def test_implicit_gemm_conv_matches_float64(cuda, shape, stride, monkeypatch) ->
     y = conv(x)
     g = torch.randn_like(y)
     y.backward(g)
-    assert len(calls) == 1 + (stride == 1 and co % 32 == 0), calls
+    assert len(calls) == 1 + (stride == 1 and co % 32 == 0 and c % 4 == 0), calls
     xd = x.detach().double().requires_grad_(True)
     wd = conv.weight.detach().double().requires_grad_(True)
     bd = conv.bias.detach().double().requires_grad_(True)
-    yd = torch.nn.functional.conv2d(xd, wd, bd, stride=stride, padding=1)
+    yd = torch.nn.functional.conv2d(xd, wd, bd, stride=stride, padding=k // 2)
     yd.backward(g.double())
 
     def rel(a: torch.Tensor, b: torch.Tensor) -> float:
