@@ -40,6 +40,8 @@
 //   m-contiguous in memory ([k][m]): LDS [k][160] bf16, fragment = two
 //     ds_read_b64_tr_b16 (transposing read).
 #include "common.h"
+
+#include <cstdlib>
 #include "descs.h"
 
 namespace kfac {
@@ -855,7 +857,14 @@ void gemm3_conv(const float* x, const float* w, float* y, int N, int H, int W, i
 int gemm3_wgrad_splits(int pixels, int Cout, int kcols) {
   const int tiles = ((Cout + GT - 1) / GT) * ((kcols + GT - 1) / GT);
   const int kts = (pixels + GK - 1) / GK;
-  int sp = (512 + tiles - 1) / tiles;
+  // KFAC_WGRAD_SPLIT_BLOCKS (default 512): blocks the split-K aims for --
+  // more splits fill the chip, fewer shrink the partial-sum pass
+  static const int target = [] {
+    const char* e = std::getenv("KFAC_WGRAD_SPLIT_BLOCKS");
+    const int v = e != nullptr ? std::atoi(e) : 0;
+    return v > 0 ? v : 512;
+  }();
+  int sp = (target + tiles - 1) / tiles;
   if (sp > kts / 8) sp = kts / 8;
   if (sp < 1) sp = 1;
   const int per = (kts + sp - 1) / sp;
