@@ -79,6 +79,10 @@ void apply_multi(const LayerDesc* descs, int nlayers, int64_t total_blocks,
 int gemm3_grid(int total_tiles);
 void gemm3_single(const GemmDesc& d, bool a_kc, bool b_kc, int splits, int64_t split_stride,
                   hipStream_t s);
+void subsample_fwd(const float* x, float* y, int N, int H, int W, int C, int sh, int sw,
+                   hipStream_t s);
+void subsample_bwd(const float* g, float* gx, int N, int H, int W, int C, int sh, int sw,
+                   hipStream_t s);
 int gemm3_conv_splits(int N, int H, int W, int C, int Cout, int kh, int kw, int stride, int pad);
 int gemm3_wgrad_splits(int pixels, int Cout, int kcols);
 void gemm3_conv_wgrad(const float* x, const float* dy, float* dw, int N, int H, int W, int C,
@@ -1185,6 +1189,41 @@ at::Tensor gemm3_conv_wgrad(const at::Tensor& x, const at::Tensor& dy, int64_t k
   return dw.view({Co, kh, kw, C}).permute({0, 3, 1, 2});
 }
 
+// x[:, :, ::sh, ::sw] of a channels_last fp32 tensor (C % 4 == 0), and the
+// adjoint: the gradient scattered to every kept pixel of a zero tensor of
+// the input's shape (csrc/subsample.hip)
+static void check_nhwc4(const at::Tensor& t, const char* what) {
+  check_cuda(t, what);
+  TORCH_CHECK(t.scalar_type() == at::kFloat && t.dim() == 4 &&
+                  t.is_contiguous(at::MemoryFormat::ChannelsLast) && t.size(1) % 4 == 0 &&
+                  (reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0,
+              what, ": expected a 16-byte aligned channels_last fp32 tensor with C % 4 == 0");
+}
+
+at::Tensor subsample_fwd(const at::Tensor& x, int64_t sh, int64_t sw) {
+  check_nhwc4(x, "subsample x");
+  TORCH_CHECK(sh >= 1 && sw >= 1, "subsample: strides");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  auto y = at::empty({N, C, (H + sh - 1) / sh, (W + sw - 1) / sw},
+                     x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  kfac::subsample_fwd(x.data_ptr<float>(), y.data_ptr<float>(), (int)N, (int)H, (int)W, (int)C,
+                      (int)sh, (int)sw, cur_stream());
+  return y;
+}
+
+at::Tensor subsample_bwd(const at::Tensor& gy, int64_t H, int64_t W, int64_t sh, int64_t sw) {
+  check_nhwc4(gy, "subsample gradient");
+  const int64_t N = gy.size(0), C = gy.size(1);
+  TORCH_CHECK(gy.size(2) == (H + sh - 1) / sh && gy.size(3) == (W + sw - 1) / sw,
+              "subsample_bwd: gradient shape");
+  auto gx = at::empty({N, C, H, W}, gy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  c10::hip::HIPGuardMasqueradingAsCUDA g(gy.device());
+  kfac::subsample_bwd(gy.data_ptr<float>(), gx.data_ptr<float>(), (int)N, (int)H, (int)W, (int)C,
+                      (int)sh, (int)sw, cur_stream());
+  return gx;
+}
+
 void gemm3_grouped(const at::Tensor& table, int64_t nlayers, int64_t total_tiles,
                    bool a_kc, bool b_kc) {
   check_cuda(table, "table");
@@ -1439,6 +1478,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("A_hls") = std::vector<c10::optional<at::Tensor>>(),
         py::arg("B_hls") = std::vector<c10::optional<at::Tensor>>());
   m.def("gemm3_grouped", &gemm3_grouped);
+  m.def("subsample_fwd", &subsample_fwd, py::arg("x"), py::arg("sh"), py::arg("sw"));
+  m.def("subsample_bwd", &subsample_bwd, py::arg("gy"), py::arg("h"), py::arg("w"),
+        py::arg("sh"), py::arg("sw"));
   m.def("gemm3_conv_wgrad", &gemm3_conv_wgrad, py::arg("x"), py::arg("dy"), py::arg("kh"),
         py::arg("kw"), py::arg("stride"), py::arg("pad"));
   m.def("gemm3_conv", &gemm3_conv, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"),

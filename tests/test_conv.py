@@ -234,3 +234,25 @@ def test_implicit_gemm_conv_matches_float64(cuda, shape, stride, k, monkeypatch)
     assert rel(x.grad, xd.grad) < 2e-5, rel(x.grad, xd.grad)
     assert rel(conv.weight.grad, wd.grad) < 2e-5, rel(conv.weight.grad, wd.grad)
     assert rel(conv.bias.grad, bd.grad) < 2e-5, rel(conv.bias.grad, bd.grad)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('shape,s', [((32, 256, 56, 56), 2), ((3, 12, 7, 9), 2), ((2, 8, 10, 10), 3)])
+def test_subsample_native_exact(cuda, shape, s) -> None:
+    """The strided 1x1 convolutions' subsample and its adjoint on the native
+    kernels (csrc/subsample.hip) equal the slicing reference bit for bit."""
+    from distributed_kfac_pytorch_amd.ops import _native
+    from distributed_kfac_pytorch_amd.ops.conv import _subsample
+
+    assert _native.native() is not None, _native.load_error()
+    x = torch.randn(*shape, device=cuda).contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    y = _subsample(x, s, s)
+    ref = x.detach()[:, :, ::s, ::s]
+    assert torch.equal(y, ref) and y.is_contiguous(memory_format=torch.channels_last)
+    g = torch.randn_like(y)
+    y.backward(g)
+    gx = torch.zeros_like(x)
+    gx[:, :, ::s, ::s] = g
+    assert torch.equal(x.grad, gx)
+    assert x.grad.is_contiguous(memory_format=torch.channels_last)
