@@ -61,7 +61,7 @@ Two safety nets guard every capture (round 5):
   saved state the step runs eagerly twice and is replayed three times -- the
   second replay after an eager step of the other kind, the third straight
   after it -- and every parameter and gradient must agree per tensor within
-  10x the eager-vs-eager noise (capped at 25 %, floored at the step's
+  10x the eager-vs-eager noise (capped at 25 %, floored at twice the step's
   largest eager noise: ``verify_tolerance``); otherwise the graphs are
   dropped and the runner stays eager.
 
@@ -163,20 +163,22 @@ def verify_tolerance(noise: torch.Tensor) -> torch.Tensor:
 
     ``min(10 x n, max(2 x n, 0.25))`` of the tensor's own noise ``n`` -- a
     replay may be ten times as noisy as one eager pair, but not 25 % off when
-    the eager pair agrees to within 12.5 % -- plus a floor of the step's
-    largest eager noise (itself capped at 25 %) and 1e-3.  The floor: one
+    the eager pair agrees to within 12.5 % -- plus a floor of twice the
+    step's largest eager noise (capped at 25 %) and 1e-3.  The floor: one
     eager pair under-samples the noise of a tensor fed by atomic reductions
-    (MIOpen's bf16 solvers).  In the ImageNet CLI's bf16 batch-8 steps six
+    (MIOpen's bf16 solvers), and replays reorder those atomics more than two
+    back-to-back eager steps do.  In the ImageNet CLI's bf16 batch-8 steps six
     eager steps from one state spread by up to 14 % in BatchNorm gradients,
-    six replays by the same 10-15 % around the eager step AND around each
-    other, yet single eager pairs put some of those tensors at 1e-4 and the
-    check dropped sound graphs in half the runs
-    (profiles/r5/graph_verify_probe/).  The hazards the check exists for
+    six replays by 10-16 % around the eager step AND around each other, yet
+    single eager pairs put some of those tensors at 0 - 1e-4 and the check
+    dropped sound graphs in half the runs (profiles/r5/graph_verify_probe/;
+    with a floor of 1x the largest noise, one run in ~10 still failed: 12 %
+    against a 6.9 % step noise, profiles/r5/pytest_gpu_final/).  The hazards the check exists for
     (memory a graph reads outside its pool, accumulation the graph never
     re-zeroes) move a gradient by O(1) or make it non-finite; a deterministic
     fp32 step keeps a floor of ~1e-3.  A non-finite noise entry makes every
     tolerance NaN (the check fails)."""
-    floor = torch.clamp(noise.max(), max=0.25) if noise.numel() else noise.new_zeros(())
+    floor = torch.clamp(2.0 * noise.max(), max=0.25) if noise.numel() else noise.new_zeros(())
     return torch.minimum(10.0 * noise, torch.clamp(2.0 * noise, min=0.25)) + floor + 1e-3
 
 

@@ -62,8 +62,8 @@ def test_verify_tolerance() -> None:
     # bf16 step: a tensor whose single eager pair agreed to 1e-4 may still
     # differ by the 4.6 % seen across replays and eager steps
     noisy = verify_tolerance(torch.tensor([1e-4, 0.02, 0.09], dtype=torch.float64))
-    assert noisy[0] > 0.046 and noisy[1] > 0.2
-    assert torch.all(noisy < 0.5)
+    assert noisy[0] > 0.12 and noisy[1] > 0.2
+    assert torch.all(noisy < 0.7)
     # a model whose noise exceeds 25 %: the floor stops at 25 %, so a
     # quiet tensor off by 100 % still fails
     big = verify_tolerance(torch.tensor([0.0, 0.6], dtype=torch.float64))
