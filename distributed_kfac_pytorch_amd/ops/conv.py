@@ -45,6 +45,8 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
+from distributed_kfac_pytorch_amd.ops import _native as _nat
+
 __all__ = ['StridedConv1x1', 'GemmConv1x1', 'ImplicitGemmConv2d', 'make_graph_safe',
            'is_strided_1x1', 'use_gemm_conv1x1', 'use_implicit_gemm_conv']
 
@@ -96,9 +98,7 @@ def _subsample_lib(x: torch.Tensor):  # type: ignore[no-untyped-def]
     if not (x.is_cuda and x.dtype == torch.float32 and x.shape[1] % 4 == 0
             and x.data_ptr() % 16 == 0):
         return None
-    from distributed_kfac_pytorch_amd.ops._native import native
-
-    return native()
+    return _nat.native()
 
 
 def _subsample(x: torch.Tensor, sh: int, sw: int) -> torch.Tensor:
@@ -161,6 +161,13 @@ def make_graph_safe(model: nn.Module, mode: str | None = None) -> int:
 
 
 _SLAB_ROWS = int(os.environ.get('KFAC_CONV1X1_SLAB_ROWS', '2048'))
+# read once: the eager (multi-GPU) step runs these paths ~100 times per step
+# and is within a millisecond of host-bound (host issue 13.1 vs 13.7 ms GPU,
+# profiles/r5/bench_eager_r7f.json)
+_MATH_1X1 = os.environ.get('KFAC_CONV1X1_MATH', 'bf16x3').lower()
+_WGRAD_1X1 = os.environ.get('KFAC_CONV1X1_WGRAD', 'native')
+_MATH_KXK = os.environ.get('KFAC_CONV_KXK_MATH', 'bf16x3').lower()
+_WGRAD_KXK = os.environ.get('KFAC_CONV_KXK_WGRAD', 'native')
 
 
 def conv1x1_math() -> str:
@@ -180,18 +187,16 @@ def conv1x1_math() -> str:
     runs split-K on the same kernel from 256 x 128 weights up
     (``_wgrad_native``, ``KFAC_CONV1X1_WGRAD=lib`` for hipBLASLt's slabs).  ``fp32``:
     hipBLASLt for everything (exact fp32 products, the A/B setting)."""
-    return os.environ.get('KFAC_CONV1X1_MATH', 'bf16x3').lower()
+    return _MATH_1X1
 
 
 def _gemm3_lib(*ts: torch.Tensor, math: str | None = None):  # type: ignore[no-untyped-def]
     """The native library when the bf16x3 path (``math``, default
     ``conv1x1_math()``) applies to these operands."""
     if (not all(t.is_cuda and t.dtype == torch.float32 for t in ts)
-            or (math or conv1x1_math()) != 'bf16x3'):
+            or (math or _MATH_1X1) != 'bf16x3'):
         return None
-    from distributed_kfac_pytorch_amd.ops._native import native
-
-    return native()
+    return _nat.native()
 
 
 def _gemm3_pays(m: int, n: int, k: int) -> bool:
@@ -285,7 +290,7 @@ class _Conv1x1Gemm(torch.autograd.Function):
         # native split-K from 256 x 128 weights up (51 vs 61 us there, 44 vs
         # 56-58 at 512 x 256 / 1024 x 512); hipBLASLt's slabs keep the small
         # 64-channel weights (37 vs 48 us): profiles/r5/conv1x1_gemm3_probe.jsonl
-        if (lib is not None and os.environ.get('KFAC_CONV1X1_WGRAD', 'native') == 'native'
+        if (lib is not None and _WGRAD_1X1 == 'native'
                 and gy.shape[1] * x.shape[1] >= 32768):
             gw = _wgrad_native(lib, gy, x)
         elif ctx.needs_input_grad[1]:
@@ -361,7 +366,7 @@ def conv_kxk_math() -> str:
     gradient: the native implicit-GEMM convolution of csrc/gemm3.hip
     (patches gathered from the NHWC input on their way into LDS, bf16x3
     MFMA, ~5e-6 relative against float64) or MIOpen fp32."""
-    return os.environ.get('KFAC_CONV_KXK_MATH', 'bf16x3').lower()
+    return _MATH_KXK
 
 
 class _ConvImplicit(torch.autograd.Function):
@@ -403,7 +408,7 @@ class _ConvImplicit(torch.autograd.Function):
         # 96 (profiles/r5/conv3x3_probe.jsonl)
         native_dw = (ctx.needs_input_grad[1] and (x.shape[1] >= 128 or x.shape[1] < 4)
                      and w.shape[0] % 4 == 0
-                     and os.environ.get('KFAC_CONV_KXK_WGRAD', 'native') == 'native')
+                     and _WGRAD_KXK == 'native')
         if native_dw:
             gw = lib.gemm3_conv_wgrad(_pad4(x), gy, k, w.shape[3], stride, pad)
             gw = gw[:, :x.shape[1]]
