@@ -207,24 +207,42 @@ def _gemm3_pays(m: int, n: int, k: int) -> bool:
     return k < 1024 or tiles >= 128
 
 
+_SPLITK_FEW_TILES = os.environ.get('KFAC_CONV1X1_SPLITK', '0') == '1'
+
+
+def _mm3(lib, a: torch.Tensor, b: torch.Tensor, n: int, b_kc: bool) -> torch.Tensor:  # type: ignore[no-untyped-def]
+    """C[m, n] = a . B on gemm3_mm; split-K (fixed-order partial sum) when a
+    long reduction leaves fewer than 128 tiles (``KFAC_CONV1X1_SPLITK=1``)."""
+    m, k = a.shape
+    tiles = -(-m // 128) * -(-n // 128)
+    sp = 1
+    if _SPLITK_FEW_TILES and tiles < 128 and k >= 1024:
+        sp = int(lib.gemm3_mm_splits(k, max(1, min(-(-256 // tiles), (k // 32) // 8))))
+    if sp == 1:
+        y = torch.empty(m, n, device=a.device, dtype=a.dtype)
+        lib.gemm3_mm(a, b, y, True, b_kc)
+        return y
+    part = torch.empty(sp, m, n, device=a.device, dtype=a.dtype)
+    lib.gemm3_mm(a, b, part, True, b_kc, sp)
+    return part.sum(0)
+
+
 def _mm_nt(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """``x @ w.T`` for fp32 [m, k] x [n, k]."""
     lib = _gemm3_lib(x, w)
-    if lib is None or not _gemm3_pays(x.shape[0], w.shape[0], x.shape[1]):
+    if lib is None or (not _SPLITK_FEW_TILES
+                       and not _gemm3_pays(x.shape[0], w.shape[0], x.shape[1])):
         return x @ w.t()
-    y = torch.empty(x.shape[0], w.shape[0], device=x.device, dtype=x.dtype)
-    lib.gemm3_mm(x, w, y, True, True)
-    return y
+    return _mm3(lib, x, w, w.shape[0], True)
 
 
 def _mm_nn(g: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """``g @ w`` for fp32 [m, k] x [k, n]."""
     lib = _gemm3_lib(g, w)
-    if lib is None or not _gemm3_pays(g.shape[0], w.shape[1], g.shape[1]):
+    if lib is None or (not _SPLITK_FEW_TILES
+                       and not _gemm3_pays(g.shape[0], w.shape[1], g.shape[1])):
         return g @ w
-    y = torch.empty(g.shape[0], w.shape[1], device=g.device, dtype=g.dtype)
-    lib.gemm3_mm(g, w, y, True, False)
-    return y
+    return _mm3(lib, g, w, w.shape[1], False)
 
 
 def _splitk(m: int, rows: int | None = None) -> int:
