@@ -44,7 +44,12 @@ def main() -> None:
     args = ap.parse_args()
     dev = torch.device('cuda', 0)
     torch.manual_seed(0)
-    model = get_model('resnet50').to(dev).to(memory_format=torch.channels_last)
+    model = get_model('resnet50')
+    # the bench's model conversions (bench.py --conv1x1 gemm --conv-kxk gemm)
+    from distributed_kfac_pytorch_amd.ops.conv import use_gemm_conv1x1, use_implicit_gemm_conv
+    use_gemm_conv1x1(model)
+    use_implicit_gemm_conv(model)
+    model = model.to(dev).to(memory_format=torch.channels_last)
     if args.bf16:
         enable_fused_weight_cast(model)
     opt = torch.optim.SGD(model.parameters(), lr=0.0125, momentum=0.9, weight_decay=5e-5,
