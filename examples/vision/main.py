@@ -65,6 +65,11 @@ def add_common_args(p: argparse.ArgumentParser, *, batch_size: int, epochs: int,
                    help='gemm: 1x1 convolutions as GEMMs on the NHWC activation matrix '
                         '(distributed_kfac_pytorch_amd.ops.conv.GemmConv1x1, same values; '
                         "the bench's default, channels_last CUDA only)")
+    p.add_argument('--conv-kxk', default='miopen', choices=['miopen', 'gemm'],
+                   help='gemm: fp32 3x3 convolutions on the native implicit-GEMM kernel '
+                        '(distributed_kfac_pytorch_amd.ops.conv.ImplicitGemmConv2d, bf16x3 '
+                        "math ~5e-6 relative; the bench's default, channels_last CUDA only; "
+                        'bf16 autocast steps keep MIOpen)')
     p.add_argument('--no-resume', dest='resume', action='store_false', default=True)
 
 
@@ -87,6 +92,9 @@ def run(args: argparse.Namespace,
         if getattr(args, 'conv1x1', 'miopen') == 'gemm':
             from distributed_kfac_pytorch_amd.ops.conv import use_gemm_conv1x1
             use_gemm_conv1x1(model)
+        if getattr(args, 'conv_kxk', 'miopen') == 'gemm':
+            from distributed_kfac_pytorch_amd.ops.conv import use_implicit_gemm_conv
+            use_implicit_gemm_conv(model)
     if args.world_size > 1:
         ctx = contextlib.nullcontext()
         if getattr(args, 'graphs', 0) and args.cuda:
