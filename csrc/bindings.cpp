@@ -81,6 +81,7 @@ void gemm3_single(const GemmDesc& d, bool a_kc, bool b_kc, int splits, int64_t s
                   hipStream_t s);
 void subsample_fwd(const float* x, float* y, int N, int H, int W, int C, int sh, int sw,
                    hipStream_t s);
+void sum_splits(const float* part, float* out, int S, int64_t T, hipStream_t s);
 void subsample_bwd(const float* g, float* gx, int N, int H, int W, int C, int sh, int sw,
                    hipStream_t s);
 int gemm3_conv_splits(int N, int H, int W, int C, int Cout, int kh, int kw, int stride, int pad);
@@ -1122,6 +1123,8 @@ void gemm3_mm(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, boo
 // flipw: w is a stride-1 forward weight [Cf, Cout, kh, kw] (Cf = x's C) and
 // the convolution applied is its flipped transpose -- the input gradient of
 // that convolution when x is dy (pad = kh - 1 - forward pad).
+at::Tensor sum_splits(const at::Tensor& part, const c10::optional<at::Tensor>& out_opt);
+
 at::Tensor gemm3_conv(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad,
                       bool flipw) {
   check_cuda(x, "gemm3_conv x");
@@ -1153,10 +1156,7 @@ at::Tensor gemm3_conv(const at::Tensor& x, const at::Tensor& w, int64_t stride, 
   kfac::gemm3_conv(x.data_ptr<float>(), w.data_ptr<float>(), part.data_ptr<float>(), (int)N,
                    (int)H, (int)W, (int)C, (int)Co, (int)kh, (int)kw, (int)stride, (int)pad, sp,
                    flipw, cur_stream());
-  if (sp > 1) {
-    auto yv = y.permute({0, 2, 3, 1}).view({N * Ho * Wo, Co});
-    at::sum_out(yv, part, {0});
-  }
+  if (sp > 1) sum_splits(part, y.permute({0, 2, 3, 1}).view({N * Ho * Wo, Co}));
   return y;
 }
 
@@ -1185,7 +1185,7 @@ at::Tensor gemm3_conv_wgrad(const at::Tensor& x, const at::Tensor& dy, int64_t k
   kfac::gemm3_conv_wgrad(x.data_ptr<float>(), dy.data_ptr<float>(), part.data_ptr<float>(),
                          (int)N, (int)H, (int)W, (int)C, (int)Co, (int)kh, (int)kw, (int)stride,
                          (int)pad, sp, cur_stream());
-  auto dw = sp > 1 ? part.sum(0) : part[0];
+  auto dw = sp > 1 ? sum_splits(part, c10::nullopt) : part[0];
   return dw.view({Co, kh, kw, C}).permute({0, 3, 1, 2});
 }
 
@@ -1198,6 +1198,28 @@ static void check_nhwc4(const at::Tensor& t, const char* what) {
                   t.is_contiguous(at::MemoryFormat::ChannelsLast) && t.size(1) % 4 == 0 &&
                   (reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0,
               what, ": expected a 16-byte aligned channels_last fp32 tensor with C % 4 == 0");
+}
+
+// out = part.sum(0) for a contiguous fp32 [S, ...] partial stack (split-K);
+// `out` contiguous with part[0]'s element count, or undefined (allocated)
+at::Tensor sum_splits(const at::Tensor& part, const c10::optional<at::Tensor>& out_opt) {
+  check_cuda(part, "sum_splits partials");
+  TORCH_CHECK(part.scalar_type() == at::kFloat && part.is_contiguous() && part.dim() >= 2,
+              "sum_splits: contiguous fp32 [S, ...] partials");
+  const int64_t S = part.size(0), T = part.numel() / (S > 0 ? S : 1);
+  at::Tensor out = out_opt.has_value() ? *out_opt : at::empty(part.sizes().slice(1), part.options());
+  TORCH_CHECK(out.scalar_type() == at::kFloat && out.is_contiguous() && out.numel() == T,
+              "sum_splits: output must be contiguous fp32 with one partial's elements");
+  const bool vec = T % 4 == 0 && (reinterpret_cast<uintptr_t>(part.data_ptr()) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(out.data_ptr()) & 15) == 0;
+  if (!vec) {
+    auto flat = out.view({T});
+    at::sum_out(flat, part.view({S, T}), {0});
+    return out;
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA g(part.device());
+  kfac::sum_splits(part.data_ptr<float>(), out.data_ptr<float>(), (int)S, T, cur_stream());
+  return out;
 }
 
 at::Tensor subsample_fwd(const at::Tensor& x, int64_t sh, int64_t sw) {
@@ -1479,6 +1501,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("B_hls") = std::vector<c10::optional<at::Tensor>>());
   m.def("gemm3_grouped", &gemm3_grouped);
   m.def("subsample_fwd", &subsample_fwd, py::arg("x"), py::arg("sh"), py::arg("sw"));
+  m.def("sum_splits", &sum_splits, py::arg("part"), py::arg("out") = py::none());
   m.def("subsample_bwd", &subsample_bwd, py::arg("gy"), py::arg("h"), py::arg("w"),
         py::arg("sh"), py::arg("sw"));
   m.def("gemm3_conv_wgrad", &gemm3_conv_wgrad, py::arg("x"), py::arg("dy"), py::arg("kh"),

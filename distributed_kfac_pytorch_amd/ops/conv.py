@@ -224,7 +224,7 @@ def _mm3(lib, a: torch.Tensor, b: torch.Tensor, n: int, b_kc: bool) -> torch.Ten
         return y
     part = torch.empty(sp, m, n, device=a.device, dtype=a.dtype)
     lib.gemm3_mm(a, b, part, True, b_kc, sp)
-    return part.sum(0)
+    return lib.sum_splits(part)
 
 
 def _mm_nt(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
@@ -277,7 +277,7 @@ def _wgrad_native(lib, gy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:  # ty
         return gw
     part = torch.empty(sp, co, ci, device=gy.device, dtype=gy.dtype)
     lib.gemm3_mm(gy, x, part, False, False, sp)
-    return part.sum(0)
+    return lib.sum_splits(part)
 
 
 class _Conv1x1Gemm(torch.autograd.Function):

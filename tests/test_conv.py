@@ -256,3 +256,23 @@ def test_subsample_native_exact(cuda, shape, s) -> None:
     gx[:, :, ::s, ::s] = g
     assert torch.equal(x.grad, gx)
     assert x.grad.is_contiguous(memory_format=torch.channels_last)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('shape', [(7, 256, 64), (256, 64, 256), (3, 5, 7), (1, 8, 4)])
+def test_sum_splits_matches_torch(cuda, shape) -> None:
+    """The split-K partial sum kernel (csrc/subsample.hip ``sum_splits``,
+    fixed order) equals ``part.sum(0)`` to fp32 rounding, with the torch
+    fallback for element counts that are not a multiple of 4."""
+    from distributed_kfac_pytorch_amd.ops import _native
+
+    lib = _native.native()
+    assert lib is not None, _native.load_error()
+    part = torch.randn(*shape, device=cuda)
+    got = lib.sum_splits(part)
+    ref = part.double().sum(0)
+    assert got.shape == ref.shape
+    assert float((got.double() - ref).abs().max() / ref.abs().max().clamp_min(1e-30)) < 1e-5
+    out = torch.empty(shape[1:], device=cuda)
+    assert lib.sum_splits(part, out).data_ptr() == out.data_ptr()
+    torch.testing.assert_close(out, got)
