@@ -25,7 +25,6 @@ from __future__ import annotations
 
 import logging
 import math
-import os
 import warnings
 from collections import defaultdict
 from typing import Any
@@ -46,6 +45,7 @@ from distributed_kfac_pytorch_amd.parallel.comm import get_world_size
 from distributed_kfac_pytorch_amd.parallel.comm import (
     TorchDistributedCommunicator,
 )
+from distributed_kfac_pytorch_amd.utils.env import getenv
 
 logger = logging.getLogger(__name__)
 # diagnostics only: compute P but leave the raw gradients in place
@@ -100,7 +100,7 @@ class StepGraphs:
         """Split the layers into ``KFAC_PRECOND_STREAMS`` (default 4)
         cost-balanced lanes (greedy LPT on the precondition GEMM flops
         ``g*a*(g+a)``); each lane keeps model order."""
-        n = max(1, min(int(os.environ.get('KFAC_PRECOND_STREAMS', '4')), len(workers)))
+        n = max(1, min(int(getenv('KFAC_PRECOND_STREAMS', '4')), len(workers)))
         if n == 1:
             return [list(workers)]
 
@@ -393,7 +393,7 @@ class BaseKFACPreconditioner:
         # tree: profiles/r5/eager_stepgraphs/), while the grouped kernels
         # launched eagerly are only 4 + 3 launches.  Whole-step graphs
         # (graphs.GraphedTrainStep) capture the phase anyway.
-        if os.environ.get('KFAC_GRAPHS', '0') == '1':
+        if getenv('KFAC_GRAPHS', '0') == '1':
             self._graphs = StepGraphs()
         # factor SYRKs (+ their all-reduce) run on a side stream forked from
         # the hook's stream, so they overlap the rest of forward / backward;
@@ -632,7 +632,7 @@ class BaseKFACPreconditioner:
         ``memory_usage``, graph capture.  Single process only: with a process
         group the buckets / packed chunks still unlaunched at ``step()`` are
         all-reduced from the compute stream and need the full join."""
-        if os.environ.get('KFAC_FACTOR_JOIN', 'lazy') != 'lazy':
+        if getenv('KFAC_FACTOR_JOIN', 'lazy') != 'lazy':
             return False
         if self.steps % self.inv_update_steps == 0:
             return False
@@ -742,7 +742,7 @@ class BaseKFACPreconditioner:
         ``g*a*(g+a)`` moved into the early group.  Never on second-order
         update steps (the bases change in ``step()``)."""
         self._early = {'names': [], 'count': 0, 'total': 0, 'pending': False}
-        if os.environ.get('KFAC_PRECOND_OVERLAP', '0') == '0':
+        if getenv('KFAC_PRECOND_OVERLAP', '0') == '0':
             return
         if self._accumulation_steps != 1 or get_world_size() > 1:
             return
@@ -760,7 +760,7 @@ class BaseKFACPreconditioner:
             g, a = l.module.g_factor_shape[0], l.module.a_factor_shape[0]
             return float(g) * a * (g + a)
 
-        frac = float(os.environ.get('KFAC_PRECOND_OVERLAP_FRAC', '0.5'))
+        frac = float(getenv('KFAC_PRECOND_OVERLAP_FRAC', '0.5'))
         total = sum(cost(l) for _, l in workers)
         names, acc = [], 0.0
         for n, l in workers[:-1]:
@@ -997,7 +997,7 @@ class BaseKFACPreconditioner:
     def _factor_stream(self, t: torch.Tensor) -> torch.cuda.Stream | None:
         # KFAC_FACTOR_STREAM: 1 force on, 0 force off, unset = on for
         # single-process jobs and RCCL process groups
-        mode = os.environ.get('KFAC_FACTOR_STREAM', 'auto')
+        mode = getenv('KFAC_FACTOR_STREAM', 'auto')
         if not t.is_cuda or self._factor_stream_off or mode == '0':
             return None
         if mode != '1' and not self._stream_friendly_backend():

@@ -22,7 +22,6 @@ MI355X-specific behaviour:
 """
 from __future__ import annotations
 
-import os
 
 from typing import Callable
 
@@ -41,6 +40,7 @@ from distributed_kfac_pytorch_amd.parallel.comm import get_world_size
 from distributed_kfac_pytorch_amd.parallel.comm import (
     TorchDistributedCommunicator,
 )
+from distributed_kfac_pytorch_amd.utils.env import getenv
 
 
 def _resolve(value: torch.Tensor | FutureType | None) -> torch.Tensor | None:
@@ -314,10 +314,10 @@ class KFACBaseLayer:
         emulation used by the gloo tests, 0 = off).  The slot bookkeeping is
         host-side, so auto stays off under the opt-in multi-rank step graphs
         (``KFAC_STEP_GRAPHS_MULTI=1``), whose replays would skip it."""
-        mode = os.environ.get('KFAC_PACKED_FACTORS', 'auto')
+        mode = getenv('KFAC_PACKED_FACTORS', 'auto')
         if mode == '0' or not self._pack_factors() or get_world_size(group) == 1:
             return False
-        if mode == 'auto' and os.environ.get('KFAC_STEP_GRAPHS_MULTI', '0') == '1':
+        if mode == 'auto' and getenv('KFAC_STEP_GRAPHS_MULTI', '0') == '1':
             return False
         if self.factor_dtype not in (None, torch.float32):
             return False
@@ -401,7 +401,7 @@ class KFACBaseLayer:
         """
         if not self.symmetric_factors:
             return False
-        if os.environ.get('KFAC_PACK_FACTORS', '1') == '0':
+        if getenv('KFAC_PACK_FACTORS', '1') == '0':
             return self.symmetry_aware
         return True
 

@@ -14,7 +14,6 @@ identical semantics.  ``KFAC_FUSED_BN=0`` disables the kernels,
 """
 from __future__ import annotations
 
-import os
 from typing import Any
 
 import torch
@@ -22,17 +21,18 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from distributed_kfac_pytorch_amd.ops._native import native
+from distributed_kfac_pytorch_amd.utils.env import getenv
 
 __all__ = ['BatchNormAct2d', 'bn_act']
 
 
 def _enabled() -> bool:
-    return os.environ.get('KFAC_FUSED_BN', '1') != '0'
+    return getenv('KFAC_FUSED_BN', '1') != '0'
 
 
 def _dtypes() -> tuple[torch.dtype, ...]:
     # KFAC_FUSED_BN_FP32=0 keeps fp32 activations on the PyTorch / MIOpen path
-    if os.environ.get('KFAC_FUSED_BN_FP32', '1') == '0':
+    if getenv('KFAC_FUSED_BN_FP32', '1') == '0':
         return (torch.bfloat16,)
     return (torch.bfloat16, torch.float32)
 

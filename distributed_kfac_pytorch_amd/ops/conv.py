@@ -46,6 +46,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from distributed_kfac_pytorch_amd.ops import _native as _nat
+from distributed_kfac_pytorch_amd.utils.env import getenv
 
 __all__ = ['StridedConv1x1', 'GemmConv1x1', 'ImplicitGemmConv2d', 'make_graph_safe',
            'is_strided_1x1', 'use_gemm_conv1x1', 'use_implicit_gemm_conv']
@@ -145,7 +146,7 @@ def make_graph_safe(model: nn.Module, mode: str | None = None) -> int:
       GEMMs, no MIOpen 1x1 solver in the graph at all) -- slower than MIOpen
       at the 56x56 stages (profiles/conv1x1_probe_r4.jsonl).
     """
-    mode = mode or os.environ.get('KFAC_GRAPH_SAFE_CONV', 'strided')
+    mode = mode or getenv('KFAC_GRAPH_SAFE_CONV', 'strided')
     if mode == 'gemm':
         return use_gemm_conv1x1(model)
     if mode != 'strided':

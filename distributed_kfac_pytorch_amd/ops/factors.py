@@ -18,12 +18,12 @@ symmetric fp32 result with the EMA / averaging weights folded into
 from __future__ import annotations
 
 import math
-import os
 
 import torch
 
 from distributed_kfac_pytorch_amd.ops._native import native
 from distributed_kfac_pytorch_amd.ops._native import use_native
+from distributed_kfac_pytorch_amd.utils.env import getenv
 
 
 def _torch_cov_accumulate_(
@@ -50,13 +50,13 @@ def _torch_cov_accumulate_(
 def fp32_exact() -> bool:
     """fp32 SYRK inputs: exact-product fp32 MFMA (``KFAC_SYRK_FP32=exact``)
     instead of the default three-term bf16 split (csrc/syrk.hip)."""
-    return os.environ.get('KFAC_SYRK_FP32', 'bf16x3').lower() == 'exact'
+    return getenv('KFAC_SYRK_FP32', 'bf16x3').lower() == 'exact'
 
 
 def _splits() -> int:
     """Split-K slab count of the SYRK (``KFAC_SYRK_SPLITS``; 0 = the
     kernel's own choice, 1 = no split-K workspace)."""
-    return int(os.environ.get('KFAC_SYRK_SPLITS', '0'))
+    return int(getenv('KFAC_SYRK_SPLITS', '0'))
 
 
 def packed_dim(out: torch.Tensor) -> int:

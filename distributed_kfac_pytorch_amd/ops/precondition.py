@@ -19,7 +19,6 @@ step performs no host synchronisation:
 from __future__ import annotations
 
 import math
-import os
 from typing import Any
 from typing import Callable
 
@@ -27,6 +26,7 @@ import torch
 
 from distributed_kfac_pytorch_amd.ops._native import native
 from distributed_kfac_pytorch_amd.ops._native import use_native
+from distributed_kfac_pytorch_amd.utils.env import getenv
 
 
 def eigen_scale_(
@@ -432,13 +432,13 @@ class MultiLayerApply:
 
 
 def presplit_enabled() -> bool:
-    return os.environ.get('KFAC_GEMM3_PRESPLIT', '0') == '1'
+    return getenv('KFAC_GEMM3_PRESPLIT', '0') == '1'
 
 
 def grouped_gemm_enabled() -> bool:
     """``KFAC_PRECOND_GEMM=torch`` keeps the per-layer hipBLASLt fp32 chain;
     otherwise a grouped bf16x3 MFMA kernel runs (``grouped_gemm_mode``)."""
-    return os.environ.get('KFAC_PRECOND_GEMM', 'bf16x3').lower() != 'torch'
+    return getenv('KFAC_PRECOND_GEMM', 'bf16x3').lower() != 'torch'
 
 
 class GroupedPrecondition:
@@ -790,7 +790,7 @@ def grouped_gemm_mode() -> str:
     torch (per-layer hipBLASLt fp32).  Same box, alternating runs: ResNet-50
     2183 / 2190 vs 2170 / 2172 img/s, GPT-NeoX-125M 246.2k / 247.0k vs
     238.4k / 238.8k tokens/s (profiles/gemm3s_integration_ab_r2.txt)."""
-    return os.environ.get('KFAC_PRECOND_GEMM', 'split').lower()
+    return getenv('KFAC_PRECOND_GEMM', 'split').lower()
 
 
 def make_grouped() -> GroupedPrecondition:
