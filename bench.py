@@ -421,17 +421,49 @@ def run(args: argparse.Namespace, use_kfac: bool, rank: int, world: int,
     return out
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(('127.0.0.1', 0))
+        return int(s.getsockname()[1])
+
+
+def launcher_argv(argv: list[str], gpus: int, port: int) -> list[str]:
+    """torchrun command that starts ``gpus`` ranks of this script with the
+    same arguments: one process per GPU on this node, rendezvous on
+    127.0.0.1 (reference launcher: ``scripts/run_imagenet.sh:54-60``)."""
+    return [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
+            f'--nproc-per-node={gpus}', '--master-addr=127.0.0.1',
+            f'--master-port={port}', '--max-restarts=0',
+            os.path.abspath(__file__)] + list(argv)
+
+
+def check_world(world: int, gpus: int) -> None:
+    """The job must have exactly ``--gpus`` ranks: a mismatch would time a
+    different configuration than the one the JSON line names."""
+    if world != gpus:
+        raise SystemExit(f'[bench] --gpus {gpus} but the job has {world} rank(s) '
+                         f'(WORLD_SIZE={os.environ.get("WORLD_SIZE")}); launch N ranks with '
+                         'torchrun or run `python bench.py --gpus N` without WORLD_SIZE set')
+
+
 def main() -> None:
     args = parse_args()
+    if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        # `python bench.py --gpus N`: start the N ranks as a fresh child
+        # process (nothing in this process has touched the GPU), relay its
+        # output (rank 0 prints the JSON line) and exit with its status
+        import subprocess
+        cmd = launcher_argv(sys.argv[1:], args.gpus, _free_port())
+        print('[bench] launching: ' + ' '.join(cmd), file=sys.stderr, flush=True)
+        sys.exit(subprocess.call(cmd))
     if args.bf16:
         args.dtype = 'bf16'
     if args.fp32:
         args.dtype = 'fp32'
     amp = args.dtype == 'bf16'
+    check_world(int(os.environ.get('WORLD_SIZE', '1')), args.gpus)
     rank, world, dev = setup(args)
-    if world != args.gpus and rank == 0:
-        print(f'[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}',
-              file=sys.stderr)
     res = run(args, not args.no_kfac, rank, world, dev, amp)
     base = None
     if args.baseline and not args.no_kfac:

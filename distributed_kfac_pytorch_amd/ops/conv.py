@@ -161,14 +161,23 @@ def make_graph_safe(model: nn.Module, mode: str | None = None) -> int:
 
 
 
-_SLAB_ROWS = int(os.environ.get('KFAC_CONV1X1_SLAB_ROWS', '2048'))
-# read once: the eager (multi-GPU) step runs these paths ~100 times per step
-# and is within a millisecond of host-bound (host issue 13.1 vs 13.7 ms GPU,
-# profiles/r5/bench_eager_r7f.json)
-_MATH_1X1 = os.environ.get('KFAC_CONV1X1_MATH', 'bf16x3').lower()
-_WGRAD_1X1 = os.environ.get('KFAC_CONV1X1_WGRAD', 'native')
-_MATH_KXK = os.environ.get('KFAC_CONV_KXK_MATH', 'bf16x3').lower()
-_WGRAD_KXK = os.environ.get('KFAC_CONV_KXK_WGRAD', 'native')
+# Knobs are read at call time through utils.env.getenv (~0.2 us a read, the
+# eager step runs these paths ~100 times): a change of the environment takes
+# effect on the next call, and two models in one process can differ.
+def _slab_rows() -> int:
+    return int(getenv('KFAC_CONV1X1_SLAB_ROWS', '2048'))
+
+
+def _wgrad_1x1() -> str:
+    return getenv('KFAC_CONV1X1_WGRAD', 'native')
+
+
+def _wgrad_kxk() -> str:
+    return getenv('KFAC_CONV_KXK_WGRAD', 'native')
+
+
+def _splitk_few_tiles() -> bool:
+    return getenv('KFAC_CONV1X1_SPLITK', '0') == '1'
 
 
 def conv1x1_math() -> str:
@@ -188,14 +197,14 @@ def conv1x1_math() -> str:
     runs split-K on the same kernel from 256 x 128 weights up
     (``_wgrad_native``, ``KFAC_CONV1X1_WGRAD=lib`` for hipBLASLt's slabs).  ``fp32``:
     hipBLASLt for everything (exact fp32 products, the A/B setting)."""
-    return _MATH_1X1
+    return getenv('KFAC_CONV1X1_MATH', 'bf16x3').lower()
 
 
 def _gemm3_lib(*ts: torch.Tensor, math: str | None = None):  # type: ignore[no-untyped-def]
     """The native library when the bf16x3 path (``math``, default
     ``conv1x1_math()``) applies to these operands."""
     if (not all(t.is_cuda and t.dtype == torch.float32 for t in ts)
-            or (math or _MATH_1X1) != 'bf16x3'):
+            or (math or conv1x1_math()) != 'bf16x3'):
         return None
     return _nat.native()
 
@@ -208,16 +217,13 @@ def _gemm3_pays(m: int, n: int, k: int) -> bool:
     return k < 1024 or tiles >= 128
 
 
-_SPLITK_FEW_TILES = os.environ.get('KFAC_CONV1X1_SPLITK', '0') == '1'
-
-
 def _mm3(lib, a: torch.Tensor, b: torch.Tensor, n: int, b_kc: bool) -> torch.Tensor:  # type: ignore[no-untyped-def]
     """C[m, n] = a . B on gemm3_mm; split-K (fixed-order partial sum) when a
     long reduction leaves fewer than 128 tiles (``KFAC_CONV1X1_SPLITK=1``)."""
     m, k = a.shape
     tiles = -(-m // 128) * -(-n // 128)
     sp = 1
-    if _SPLITK_FEW_TILES and tiles < 128 and k >= 1024:
+    if _splitk_few_tiles() and tiles < 128 and k >= 1024:
         sp = int(lib.gemm3_mm_splits(k, max(1, min(-(-256 // tiles), (k // 32) // 8))))
     if sp == 1:
         y = torch.empty(m, n, device=a.device, dtype=a.dtype)
@@ -231,7 +237,7 @@ def _mm3(lib, a: torch.Tensor, b: torch.Tensor, n: int, b_kc: bool) -> torch.Ten
 def _mm_nt(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """``x @ w.T`` for fp32 [m, k] x [n, k]."""
     lib = _gemm3_lib(x, w)
-    if lib is None or (not _SPLITK_FEW_TILES
+    if lib is None or (not _splitk_few_tiles()
                        and not _gemm3_pays(x.shape[0], w.shape[0], x.shape[1])):
         return x @ w.t()
     return _mm3(lib, x, w, w.shape[0], True)
@@ -240,7 +246,7 @@ def _mm_nt(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
 def _mm_nn(g: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """``g @ w`` for fp32 [m, k] x [k, n]."""
     lib = _gemm3_lib(g, w)
-    if lib is None or (not _SPLITK_FEW_TILES
+    if lib is None or (not _splitk_few_tiles()
                        and not _gemm3_pays(g.shape[0], w.shape[1], g.shape[1])):
         return g @ w
     return _mm3(lib, g, w, w.shape[1], False)
@@ -250,7 +256,7 @@ def _splitk(m: int, rows: int | None = None) -> int:
     """Slabs of the weight-gradient reduction over ``m`` = N*H*W rows: the
     largest power of two that divides ``m`` and leaves >= ``rows`` rows each
     (``KFAC_CONV1X1_SLAB_ROWS``, default 2048)."""
-    rows = rows or _SLAB_ROWS
+    rows = rows or _slab_rows()
     s = 1
     while m % (2 * s) == 0 and m // (2 * s) >= rows:
         s *= 2
@@ -309,7 +315,7 @@ class _Conv1x1Gemm(torch.autograd.Function):
         # native split-K from 256 x 128 weights up (51 vs 61 us there, 44 vs
         # 56-58 at 512 x 256 / 1024 x 512); hipBLASLt's slabs keep the small
         # 64-channel weights (37 vs 48 us): profiles/r5/conv1x1_gemm3_probe.jsonl
-        if (lib is not None and _WGRAD_1X1 == 'native'
+        if (lib is not None and _wgrad_1x1() == 'native'
                 and gy.shape[1] * x.shape[1] >= 32768):
             gw = _wgrad_native(lib, gy, x)
         elif ctx.needs_input_grad[1]:
@@ -385,7 +391,7 @@ def conv_kxk_math() -> str:
     gradient: the native implicit-GEMM convolution of csrc/gemm3.hip
     (patches gathered from the NHWC input on their way into LDS, bf16x3
     MFMA, ~5e-6 relative against float64) or MIOpen fp32."""
-    return _MATH_KXK
+    return getenv('KFAC_CONV_KXK_MATH', 'bf16x3').lower()
 
 
 class _ConvImplicit(torch.autograd.Function):
@@ -425,9 +431,13 @@ class _ConvImplicit(torch.autograd.Function):
         # native weight gradient (split-K over the pixels) from 128 input
         # channels up: 54-71 us vs MIOpen's 85-87; at 64 MIOpen's 85 beats
         # 96 (profiles/r5/conv3x3_probe.jsonl)
+        # (the kernel indexes output pixels in 22 bits: larger inputs, e.g.
+        # 128 channels at 512x512 from batch 16, go to MIOpen)
         native_dw = (ctx.needs_input_grad[1] and (x.shape[1] >= 128 or x.shape[1] < 4)
                      and w.shape[0] % 4 == 0
-                     and _WGRAD_KXK == 'native')
+                     and gy.shape[0] * gy.shape[2] * gy.shape[3] < (1 << 22)
+                     and x.numel() + 4 * x.shape[0] * x.shape[2] * x.shape[3] < (1 << 31)
+                     and _wgrad_kxk() == 'native')
         if native_dw:
             gw = lib.gemm3_conv_wgrad(_pad4(x), gy, k, w.shape[3], stride, pad)
             gw = gw[:, :x.shape[1]]

@@ -55,8 +55,6 @@ from distributed_kfac_pytorch_amd.ops._native import load_error as _native_error
 from distributed_kfac_pytorch_amd.ops._native import native
 from distributed_kfac_pytorch_amd.ops._native import use_native
 
-JACOBI_SWEEPS = int(os.environ.get('KFAC_JACOBI_SWEEPS', '15'))
-JACOBI_TOL = float(os.environ.get('KFAC_JACOBI_TOL', '1e-7'))
 # largest n sent to the LDS Jacobi kernel (its hard limit is jacobi_max_n());
 # everything above goes to the native tridiagonalisation
 JACOBI_MAX_N = 128
@@ -133,7 +131,8 @@ def _gpu_bucket(stack: torch.Tensor, ts_sizes: set) -> tuple[torch.Tensor, torch
     lib = native()
     if n <= JACOBI_MAX_N:
         _tier('jacobi', n, stack.shape[0])
-        return lib.jacobi_eigh(stack.contiguous(), JACOBI_SWEEPS, JACOBI_TOL)
+        return lib.jacobi_eigh(stack.contiguous(), int(os.environ.get('KFAC_JACOBI_SWEEPS', '15')),
+                               float(os.environ.get('KFAC_JACOBI_TOL', '1e-7')))
     if _use_twostage(n, ts_sizes):
         _tier('twostage', n, stack.shape[0])
         if twostage.graphs_enabled():

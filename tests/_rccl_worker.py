@@ -8,11 +8,16 @@ line with what the test asserts.
 """
 from __future__ import annotations
 
+import faulthandler
+import gc
 import json
 import os
 import sys
 
 os.environ.setdefault('TORCH_NCCL_ASYNC_ERROR_HANDLING', '0')  # captured collectives
+# a fatal signal (SIGABRT from a C++ terminate) prints every thread's Python
+# stack to stderr, which the test keeps in full
+faulthandler.enable(all_threads=True)
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
@@ -68,12 +73,20 @@ def train(dev: torch.device, ddp: bool) -> dict:
         losses.append(loss.detach().clone())
     torch.cuda.synchronize()
     net = model.module if ddp else model
+    replays = runner.replays if runner is not None else 0
+    captures = runner.captures if runner is not None else 0
+    verify = runner.verify_report if runner is not None else {}
+    if runner is not None:
+        # graphs holding captured RCCL work go before the communicator does
+        runner.close()
+    print(f'[worker] ddp={ddp} steps={STEPS} replays={replays} captures={captures}',
+          flush=True)
     return {
         'losses': [float(v) for v in losses],
         'params': [p.detach().clone() for p in net.parameters()],
-        'replays': runner.replays if runner is not None else 0,
-        'captures': runner.captures if runner is not None else 0,
-        'verify': runner.verify_report if runner is not None else {},
+        'replays': replays,
+        'captures': captures,
+        'verify': verify,
         'finite': all(bool(torch.isfinite(p).all()) for p in net.parameters()),
     }
 
@@ -98,7 +111,10 @@ def main() -> None:
     if dist.get_rank() == 0:
         print('RESULT ' + json.dumps(out), flush=True)
     dist.barrier()
+    gc.collect()
+    torch.cuda.synchronize()
     dist.destroy_process_group()
+    print('[worker] process group destroyed', flush=True)
 
 
 if __name__ == '__main__':

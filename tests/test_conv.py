@@ -237,6 +237,44 @@ def test_implicit_gemm_conv_matches_float64(cuda, shape, stride, k, monkeypatch)
 
 
 @pytest.mark.gpu
+def test_implicit_gemm_conv_wgrad_falls_back_past_kernel_limit(cuda, monkeypatch) -> None:
+    """An input with N*Ho*Wo >= 2^22 output pixels (here 16 x 512 x 512)
+    is past the native weight gradient's index range: the backward takes
+    MIOpen's weight gradient instead of failing the binding's check."""
+    from distributed_kfac_pytorch_amd.ops import _native
+    from distributed_kfac_pytorch_amd.ops.conv import ImplicitGemmConv2d
+
+    lib = _native.native()
+    assert lib is not None, _native.load_error()
+    called = []
+
+    class Spy:
+        def __getattr__(self, name):  # type: ignore[no-untyped-def]
+            return getattr(lib, name)
+
+        def gemm3_conv_wgrad(self, *a):  # type: ignore[no-untyped-def]
+            called.append(tuple(a[0].shape))
+            return lib.gemm3_conv_wgrad(*a)
+
+    monkeypatch.setattr(_native, 'native', lambda: Spy())
+    monkeypatch.setenv('KFAC_CONV_KXK_MATH', 'bf16x3')
+    torch.manual_seed(0)
+    conv = nn.Conv2d(3, 8, 3, padding=1, bias=False).to(cuda).to(memory_format=torch.channels_last)
+    conv.__class__ = ImplicitGemmConv2d
+    for n, native in ((15, True), (16, False)):  # 15*512*512 < 2^22 <= 16*512*512
+        x = torch.randn(n, 3, 512, 512, device=cuda).contiguous(memory_format=torch.channels_last)
+        called.clear()
+        conv.weight.grad = None
+        y = conv(x)
+        g = torch.randn_like(y)
+        y.backward(g)
+        assert bool(called) == native, (n, called)
+        wd = torch.nn.grad.conv2d_weight(x.double(), conv.weight.shape, g.double(), padding=1)
+        err = float((conv.weight.grad.double() - wd).norm() / wd.norm())
+        assert err < 2e-5, (n, err)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize('shape,s', [((32, 256, 56, 56), 2), ((3, 12, 7, 9), 2), ((2, 8, 10, 10), 3)])
 def test_subsample_native_exact(cuda, shape, s) -> None:
     """The strided 1x1 convolutions' subsample and its adjoint on the native
