@@ -137,7 +137,6 @@ void sytrd_batched_range(const SytrdDesc* descs_dev, const int* ns, int batch,
 }  // namespace kfac
 
 int64_t sytrd_max_n() { return kfac::sytrd_max_n(); }
-static constexpr int64_t kSytrdCtlBytes = 256;  // >= SY_CTL_WORDS (csrc/sytrd.hip)
 int64_t sytrd_panel() { return kfac::sytrd_nb(); }
 
 // stacks: list of [cnt, n, n] fp32 contiguous symmetric (overwritten).
@@ -158,7 +157,7 @@ static std::vector<at::Tensor> sytrd_setup(std::vector<at::Tensor>& stacks,
     const int64_t cnt = A.size(0), n = A.size(1);
     for (int64_t b = 0; b < cnt; ++b) ns.push_back((int)n);
     scratch += cnt * ((int64_t)NB * n + (int64_t)kfac::sytrd_maxch() * P1 +
-                      kfac::sytrd_maxrowblk() + 4 + 2 * NB + ((n + 63) / 64) * n);
+                      kfac::sytrd_maxrowblk() + 4 + 2 * NB);
   }
   const int batch = (int)ns.size();
   if (batch == 0) return outs;
@@ -186,8 +185,7 @@ static std::vector<at::Tensor> sytrd_setup(std::vector<at::Tensor>& stacks,
       wp += kfac::sytrd_maxrowblk();
       D.sc = wp;
       wp += 4 + 2 * NB;
-      D.P = wp;
-      wp += ((n + 63) / 64) * n;
+      D.P = nullptr;
       D.n = (int)n;
       D.pad = 0;
     }
@@ -195,9 +193,7 @@ static std::vector<at::Tensor> sytrd_setup(std::vector<at::Tensor>& stacks,
     outs.push_back(e);
     outs.push_back(tau);
   }
-  // the table is followed by the chain's control words (persistent panels:
-  // two barrier counters and an error flag, csrc/sytrd.hip), zeroed here
-  auto dev = at::zeros({host.numel() + kSytrdCtlBytes}, opts.dtype(at::kByte));
+  auto dev = at::empty({host.numel()}, opts.dtype(at::kByte));
   dev.narrow(0, 0, host.numel()).copy_(host, /*non_blocking=*/true);
   outs.insert(outs.begin(), work);
   outs.insert(outs.begin(), dev);
@@ -233,7 +229,7 @@ void sytrd_advance(at::Tensor descs, std::vector<int64_t> sizes, int64_t k0, int
   c10::hip::HIPGuardMasqueradingAsCUDA g(descs.device());
   hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
   std::vector<int> ns(sizes.begin(), sizes.end());
-  TORCH_CHECK((int64_t)ns.size() * (int64_t)sizeof(kfac::SytrdDesc) + kSytrdCtlBytes ==
+  TORCH_CHECK((int64_t)ns.size() * (int64_t)sizeof(kfac::SytrdDesc) ==
               descs.numel());
   kfac::sytrd_batched_range(reinterpret_cast<const kfac::SytrdDesc*>(descs.data_ptr()),
                             ns.data(), (int)ns.size(), (int)k0, (int)k1, s, (int)waves);

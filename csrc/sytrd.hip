@@ -89,30 +89,11 @@ __device__ __forceinline__ void pin_desc(const GView& D) {
                "s"(D.part2), "s"(D.sc), "s"(D.P), "s"(D.n));
 }
 
-// Memory another workgroup of the SAME launch wrote (panel rows, W, the
-// partials): inside the persistent panel kernel these go through
-// agent-coherent accesses (sc1: they bypass the per-XCD L2, which is not
-// coherent across XCDs within a kernel); the two-launch form has a kernel
-// boundary between writer and reader and uses plain accesses.  The matrix
-// stream of the symv (rows of A22, never written during a panel) is always
-// plain.
-template <bool COH>
-__device__ __forceinline__ float ldc(const GLOBAL float* p) {
-  if constexpr (COH) {
-    return __hip_atomic_load(const_cast<GLOBAL float*>(p), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-  } else {
-    return *p;
-  }
-}
-template <bool COH>
-__device__ __forceinline__ void stc(GLOBAL float* p, float v) {
-  if constexpr (COH) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else {
-    *p = v;
-  }
-}
+// Plain global accesses: every writer and reader of the chain's shared
+// data (panel rows, W, the partials) sit in different launches, and the
+// kernel boundary orders them.
+__device__ __forceinline__ float ldc(const GLOBAL float* p) { return *p; }
+__device__ __forceinline__ void stc(GLOBAL float* p, float v) { *p = v; }
 
 __device__ __forceinline__ float block_sum(float v, float* red) {
   v = wave_sum_uniform(v);
@@ -135,7 +116,6 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 // of column k) are formed by EVERY wave on its own -- wave reductions and
 // lane broadcasts, no LDS round trip -- so the kernel has one block
 // barrier, before the final cross-wave sums.
-template <bool COH, bool TILE>
 __device__ __forceinline__ void col_body(const GView& D, int bx, int k, int p, int fin_only,
                                          int cnt) {
   const int n = D.n;
@@ -161,13 +141,13 @@ __device__ __forceinline__ void col_body(const GView& D, int bx, int k, int p, i
     vj[j] = 0.f;
     wj[j] = 0.f;
   }
-  if (act && (!fin_only || TILE)) {
-    if (!fin_only) a = ldc<COH>(D.A + (int64_t)k * n + r);
+  if (act && !fin_only) {
+    if (!fin_only) a = ldc(D.A + (int64_t)k * n + r);
 #pragma unroll
     for (int j = 0; j < SY_NB; ++j) {
       const int pj = p + j < n ? p + j : n - 1;
-      vj[j] = ldc<COH>(D.A + (int64_t)pj * n + r);
-      wj[j] = ldc<COH>(D.Wt + (int64_t)j * n + r);
+      vj[j] = ldc(D.A + (int64_t)pj * n + r);
+      wj[j] = ldc(D.Wt + (int64_t)j * n + r);
     }
   }
   float s2 = 0.f;
@@ -178,64 +158,25 @@ __device__ __forceinline__ void col_body(const GView& D, int bx, int k, int p, i
 #pragma unroll
     for (int u = 0; u < SY_MAXROWBLK / 64; ++u) {
       const int t = l + 64 * u;
-      const float v = ldc<COH>(D.part2 + (t < cnt ? t : cnt - 1));
+      const float v = ldc(D.part2 + (t < cnt ? t : cnt - 1));
       s2 += t < cnt ? v : 0.f;
     }
   }
-  const float tp = fin ? ldc<COH>(D.sc) : 0.f;
-  const float sprev = fin ? ldc<COH>(D.sc + 1) : 0.f;
+  const float tp = fin ? ldc(D.sc) : 0.f;
+  const float sprev = fin ? ldc(D.sc + 1) : 0.f;
   // lane j < i of every wave: W[k, j] and V_j[k] of the panel
   float cw_raw = 0.f, cv_raw = 0.f;
   if (l < i && !fin_only) {
-    cw_raw = ldc<COH>(D.Wt + (int64_t)l * n + k);
-    cv_raw = l == i - 1 ? 1.f : ldc<COH>(D.A + (int64_t)(p + l) * n + k);  // V_{i-1}[k] = 1
+    cw_raw = ldc(D.Wt + (int64_t)l * n + k);
+    cv_raw = l == i - 1 ? 1.f : ldc(D.A + (int64_t)(p + l) * n + k);  // V_{i-1}[k] = 1
   }
   float vraw = 0.f, wraw = 0.f;
   if (act && fin) {
-    vraw = r == k ? 1.f : ldc<COH>(D.A + (int64_t)(k - 1) * n + r);
-    if (!TILE) wraw = ldc<COH>(D.Wt + (int64_t)(i - 1) * n + r);
+    vraw = r == k ? 1.f : ldc(D.A + (int64_t)(k - 1) * n + r);
+    wraw = ldc(D.Wt + (int64_t)(i - 1) * n + r);
   }
 
-  float alpha2 = 0.f;
-  if constexpr (TILE) {
-    if (fin) {
-      // the tile symv of column k-1 left, per row, one partial of A22 v per
-      // 64-column tile (P[T][r], T >= k >> 6) and t1 = W^T v, t2 = V^T v,
-      // t1.t2 in sc: w = tau (A22 v - V t1 - W t2), w.v = tau (v^T A22 v -
-      // 2 t1.t2) with v^T A22 v the sum of the symv's block partials
-      const int T0 = k >> 6, nt = (n + 63) >> 6;
-      const float t1l = l < SY_NB ? ldc<COH>(D.sc + 4 + l) : 0.f;
-      const float t2l = l < SY_NB ? ldc<COH>(D.sc + 4 + SY_NB + l) : 0.f;
-      const float t12 = ldc<COH>(D.sc + 2);
-      const int t1i = __builtin_bit_cast(int, t1l), t2i = __builtin_bit_cast(int, t2l);
-      // this thread's row: sum the tile partials, subtract the panel terms
-      float y = 0.f;
-      if (act) {
-        for (int T = T0; T < nt; ++T) y += ldc<COH>(D.P + (int64_t)T * n + r);
-      }
-      float corr = 0.f;
-#pragma unroll
-      for (int j = 0; j < SY_NB; ++j) {
-        if (j < i - 1) {
-          const float t1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(t1i, j));
-          const float t2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(t2i, j));
-          corr += vj[j] * t1 + wj[j] * t2;
-        }
-      }
-      wraw = tp * (y - corr);
-      // row k of the new column (lane i-1's panel entry), formed per wave
-      float yk = 0.f;
-      if (T0 + l < nt) yk += ldc<COH>(D.P + (int64_t)(T0 + l) * n + k);
-      if (T0 + l + 64 < nt) yk += ldc<COH>(D.P + (int64_t)(T0 + l + 64) * n + k);
-      if (!fin_only && l < i - 1) corr = cv_raw * t1l + cw_raw * t2l;
-      else corr = 0.f;
-      const float wk = tp * (wave_sum_uniform(yk) - wave_sum_uniform(corr));
-      if (l == i - 1) cw_raw = wk;
-      alpha2 = -0.5f * tp * tp * (wave_sum_uniform(s2) - 2.f * t12);
-    }
-  } else {
-    if (fin) alpha2 = -0.5f * tp * wave_sum_uniform(s2);
-  }
+  const float alpha2 = fin ? -0.5f * tp * wave_sum_uniform(s2) : 0.f;
   // finalised W[k, i-1] gets the -tau/2 (w.v) v correction
   const float cw = l < i ? cw_raw + (l == i - 1 ? alpha2 : 0.f) : 0.f;
   const float cv = l < i ? cv_raw : 0.f;
@@ -243,12 +184,12 @@ __device__ __forceinline__ void col_body(const GView& D, int bx, int k, int p, i
   float vprev = 0.f, wprev = 0.f;
   if (act && fin) {
     vprev = r == k ? 1.f : vraw * sprev;
-    if (r > k) stc<COH>(D.A + (int64_t)(k - 1) * n + r, vprev);
+    if (r > k) stc(D.A + (int64_t)(k - 1) * n + r, vprev);
     wprev = wraw + alpha2 * vprev;
     // W[k, i-1] is finalised by every block on its own (cw above) and not
     // read again by later col / symv steps: writing it here would race with
     // those reads.  The panel-end trailing update does read it (r = q).
-    if (r > k || fin_only) stc<COH>(D.Wt + (int64_t)(i - 1) * n + r, wprev);
+    if (r > k || fin_only) stc(D.Wt + (int64_t)(i - 1) * n + r, wprev);
   }
   if (fin_only) return;
 
@@ -268,8 +209,8 @@ __device__ __forceinline__ void col_body(const GView& D, int bx, int k, int p, i
     a -= vj[j] * cWj + wj[j] * cVj;
   }
   if (act) {
-    stc<COH>(D.A + (int64_t)k * n + r, a);
-    if (r == k) stc<COH>(D.d + k, a);
+    stc(D.A + (int64_t)k * n + r, a);
+    if (r == k) stc(D.d + k, a);
   }
   if (k == n - 1) return;  // last diagonal entry: no reflector
   // partial sums over the reflector tail x = a[k+2:n]
@@ -297,7 +238,7 @@ __device__ __forceinline__ void col_body(const GView& D, int bx, int k, int p, i
     float s = 0.f;
 #pragma unroll
     for (int q = 0; q < SY_T / 64; ++q) s += wred[q][t];
-    stc<COH>(D.part1 + (int64_t)bx * SY_P1 + t, s);
+    stc(D.part1 + (int64_t)bx * SY_P1 + t, s);
   }
 }
 
@@ -305,14 +246,7 @@ __global__ void __launch_bounds__(SY_T) sytrd_col_kernel(
     const SytrdDesc* __restrict__ descs, int k, int p, int fin_only, int cnt) {
   const GView D = gview(descs[blockIdx.y]);
   pin_desc(D);
-  col_body<false, false>(D, blockIdx.x, k, p, fin_only, cnt);
-}
-
-__global__ void __launch_bounds__(SY_T) sytrd_col_tile_kernel(
-    const SytrdDesc* __restrict__ descs, int k, int p, int fin_only, int cnt) {
-  const GView D = gview(descs[blockIdx.y]);
-  pin_desc(D);
-  col_body<false, true>(D, blockIdx.x, k, p, fin_only, cnt);
+  col_body(D, blockIdx.x, k, p, fin_only, cnt);
 }
 
 // symv step for column k (k <= n-2).  grid (G, batch), G = sytrd_symv_blocks().
@@ -328,7 +262,7 @@ __global__ void __launch_bounds__(SY_T) sytrd_col_tile_kernel(
 // the scalars and its panel correction terms on its own.  Every block
 // writes its partial w.v (0 without rows) to part2[b]; the next col step
 // gets G as an argument.
-template <int SY_SU, bool COH>
+template <int SY_SU>
 __device__ __forceinline__ void symv_body(const GView& D, int bx, int G, int k, int p) {
   const int n = D.n;
   if (k >= n - 1) return;  // this member is done (its col steps stop too)
@@ -365,9 +299,9 @@ __device__ __forceinline__ void symv_body(const GView& D, int bx, int G, int k, 
   // with a full memory wait per trip -- 3-4 dependent round trips at n=4608)
   // lane l < i: W[k+1, l]; lane 32 <= l < 32 + i: V_{l-32}[k+1]
   float wa = 0.f;
-  if (l < i) wa = ldc<COH>(D.Wt + (int64_t)l * n + k + 1);
-  else if (l >= 32 && l - 32 < i) wa = ldc<COH>(D.A + (int64_t)(p + l - 32) * n + k + 1);
-  const float alpha = ldc<COH>(D.A + (int64_t)k * n + k + 1);
+  if (l < i) wa = ldc(D.Wt + (int64_t)l * n + k + 1);
+  else if (l >= 32 && l - 32 < i) wa = ldc(D.A + (int64_t)(p + l - 32) * n + k + 1);
+  const float alpha = ldc(D.A + (int64_t)k * n + k + 1);
   const int nch = (int)ceil_div(n - k, SY_T);
   const int np1 = nch * SY_P1;
   constexpr int PT = (SY_MAXCH * SY_P1 + SY_T - 1) / SY_T;
@@ -375,7 +309,7 @@ __device__ __forceinline__ void symv_body(const GView& D, int bx, int G, int k, 
 #pragma unroll
   for (int u = 0; u < PT; ++u) {
     const int t = threadIdx.x + SY_T * u;
-    pst[u] = ldc<COH>(D.part1 + (t < np1 ? t : np1 - 1));  // clamped: no branch per load
+    pst[u] = ldc(D.part1 + (t < np1 ? t : np1 - 1));  // clamped: no branch per load
   }
   const GLOBAL float* arow = D.A + (int64_t)k * n;
   constexpr int VT = SY_MAXN / SY_T;
@@ -383,7 +317,7 @@ __device__ __forceinline__ void symv_body(const GView& D, int bx, int G, int k, 
 #pragma unroll
   for (int u = 0; u < VT; ++u) {
     const int c = threadIdx.x + SY_T * u;
-    const float v = ldc<COH>(arow + (c < span ? base + c : n - 1));
+    const float v = ldc(arow + (c < span ? base + c : n - 1));
     vst[u] = base + c > k + 1 ? v : 0.f;
   }
 #pragma unroll
@@ -416,10 +350,10 @@ __device__ __forceinline__ void symv_body(const GView& D, int bx, int G, int k, 
     scale = 1.f / (alpha - beta);
   }
   if (bx == 0 && threadIdx.x == 0) {
-    stc<COH>(D.e + k, beta);
-    stc<COH>(D.tau + k, tau_k);
-    stc<COH>(D.sc, tau_k);
-    stc<COH>(D.sc + 1, scale);
+    stc(D.e + k, beta);
+    stc(D.tau + k, tau_k);
+    stc(D.sc, tau_k);
+    stc(D.sc + 1, scale);
   }
   // t1 = W^T v (lanes < i), t2 = V^T v (lanes 32 .. 32 + i)
   const bool tlive = l < i || (l >= 32 && l - 32 < i);
@@ -436,11 +370,11 @@ __device__ __forceinline__ void symv_body(const GView& D, int bx, int G, int k, 
     // column k+1 entries
     float pv0 = 0.f, pv1 = 0.f;
     if (l < i) {
-      pv0 = ldc<COH>(D.A + (int64_t)(p + l) * n + r0);
-      pv1 = ldc<COH>(D.A + (int64_t)(p + l) * n + r1c);
+      pv0 = ldc(D.A + (int64_t)(p + l) * n + r0);
+      pv1 = ldc(D.A + (int64_t)(p + l) * n + r1c);
     } else if (l >= 32 && l - 32 < i) {
-      pv0 = ldc<COH>(D.Wt + (int64_t)(l - 32) * n + r0);
-      pv1 = ldc<COH>(D.Wt + (int64_t)(l - 32) * n + r1c);
+      pv0 = ldc(D.Wt + (int64_t)(l - 32) * n + r0);
+      pv1 = ldc(D.Wt + (int64_t)(l - 32) * n + r1c);
     }
     const float pk0 = D.A[(int64_t)r0 * n + k + 1];
     const float pk1 = D.A[(int64_t)r1c * n + k + 1];
@@ -486,16 +420,16 @@ __device__ __forceinline__ void symv_body(const GView& D, int bx, int G, int k, 
     const float c1 = wave_sum_uniform(pv1 * tl);
     const float w1 = tau_k * (y1 - c1);
     if (l == 0) {
-      stc<COH>(D.Wt + (int64_t)i * n + r0, w0);
+      stc(D.Wt + (int64_t)i * n + r0, w0);
       pd += w0 * (r0 == k + 1 ? 1.f : scale * sv[r0 - base]);
       if (two) {
-        stc<COH>(D.Wt + (int64_t)i * n + r1, w1);
+        stc(D.Wt + (int64_t)i * n + r1, w1);
         pd += w1 * (r1 == k + 1 ? 1.f : scale * sv[r1 - base]);
       }
     }
   }
   pd = block_sum(pd, red);
-  if (threadIdx.x == 0) stc<COH>(D.part2 + bx, pd);
+  if (threadIdx.x == 0) stc(D.part2 + bx, pd);
 }
 
 template <int SY_SU>
@@ -503,276 +437,7 @@ __global__ void __launch_bounds__(SY_T) sytrd_symv_kernel(
     const SytrdDesc* __restrict__ descs, int k, int p) {
   const GView D = gview(descs[blockIdx.y]);
   pin_desc(D);
-  symv_body<SY_SU, false>(D, blockIdx.x, gridDim.x, k, p);
-}
-
-// ---- tile symv (KFAC_SYTRD_TILE): A22 v from the LOWER triangle only.
-// The trailing matrix is cut into 64 x 64 tiles on a fixed 64-aligned grid;
-// tile (I, J), I >= J, adds A_IJ v_J to the rows of I (slot P[J][row]) and,
-// off the diagonal, A_IJ^T v_I to the rows of J (slot P[I][row]).  Every
-// (slot, row) of the trailing rows is written exactly once, so the next col
-// step sums a row's slots in a fixed order (bitwise reproducible) and forms
-// w = tau (A22 v - V t1 - W t2) itself (col_body<TILE>).  Half the matrix
-// bytes of the row symv, which streams whole rows of the symmetric A22.
-// Each block holds the scaled v in LDS; wave w of a block takes rows
-// 16 w .. 16 w + 15 of the tile, lane c its column c (coalesced 256-B rows).
-template <bool COH>
-__device__ __forceinline__ void symv_tile_body(const GView& D, int bx, int G, int k, int p) {
-  const int n = D.n;
-  if (k >= n - 1) return;
-  const int i = k - p;
-  __shared__ __attribute__((aligned(16))) float sv[SY_MAXN];
-  __shared__ float ptmp[SY_MAXCH * SY_P1];
-  __shared__ float red[SY_T / 64];
-  __shared__ float colp[SY_T / 64][64];
-  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
-  const int base = (k + 1) & ~63;
-  const int span = n - base;
-  // ---- prologue (as symv_body): partials of column k, panel entries of
-  // column k+1, the pivot, the raw reflector row
-  float wa = 0.f;
-  if (l < i) wa = ldc<COH>(D.Wt + (int64_t)l * n + k + 1);
-  else if (l >= 32 && l - 32 < i) wa = ldc<COH>(D.A + (int64_t)(p + l - 32) * n + k + 1);
-  const float alpha = ldc<COH>(D.A + (int64_t)k * n + k + 1);
-  const int nch = (int)ceil_div(n - k, SY_T);
-  const int np1 = nch * SY_P1;
-  constexpr int PT = (SY_MAXCH * SY_P1 + SY_T - 1) / SY_T;
-  float pst[PT];
-#pragma unroll
-  for (int u = 0; u < PT; ++u) {
-    const int t = threadIdx.x + SY_T * u;
-    pst[u] = ldc<COH>(D.part1 + (t < np1 ? t : np1 - 1));
-  }
-  const GLOBAL float* arow = D.A + (int64_t)k * n;
-  constexpr int VT = SY_MAXN / SY_T;
-  float vst[VT];
-#pragma unroll
-  for (int u = 0; u < VT; ++u) {
-    const int c = threadIdx.x + SY_T * u;
-    const float v = ldc<COH>(arow + (c < span ? base + c : n - 1));
-    vst[u] = base + c > k + 1 && c < span ? v : 0.f;
-  }
-#pragma unroll
-  for (int u = 0; u < PT; ++u) {
-    const int t = threadIdx.x + SY_T * u;
-    if (t < np1) ptmp[t] = pst[u];
-  }
-  __syncthreads();
-  float xn2 = 0.f, xl = 0.f;
-  for (int c = 0; c < nch; ++c) {
-    xn2 += ptmp[c * SY_P1];
-    xl += ptmp[c * SY_P1 + 1 + l];
-  }
-  float tau_k, beta, scale;
-  if (xn2 == 0.f) {
-    tau_k = 0.f;
-    beta = alpha;
-    scale = 0.f;
-  } else {
-    beta = -copysignf(sqrtf(alpha * alpha + xn2), alpha);
-    tau_k = (beta - alpha) / beta;
-    scale = 1.f / (alpha - beta);
-  }
-  // t1 = W^T v (lanes < i), t2 = V^T v (lanes 32 .. 32 + i)
-  const bool tlive = l < i || (l >= 32 && l - 32 < i);
-  const float tl = tlive ? wa + scale * xl : 0.f;
-  if (bx == 0 && wv == 0) {
-    const float t2 = __shfl(tl, l + 32 < 64 ? l + 32 : l);
-    const float t12 = wave_sum_uniform(l < i ? tl * t2 : 0.f);
-    if (l < i) stc<COH>(D.sc + 4 + l, tl);
-    else if (l >= 32 && l - 32 < i) stc<COH>(D.sc + 4 + SY_NB + (l - 32), tl);
-    if (l == 0) {
-      stc<COH>(D.e + k, beta);
-      stc<COH>(D.tau + k, tau_k);
-      stc<COH>(D.sc, tau_k);
-      stc<COH>(D.sc + 1, scale);
-      stc<COH>(D.sc + 2, t12);
-    }
-  }
-  // the scaled reflector v (v[k+1] = 1), each thread its own entries
-#pragma unroll
-  for (int u = 0; u < VT; ++u) {
-    const int c = threadIdx.x + SY_T * u;
-    if (c < span) sv[c] = base + c == k + 1 ? 1.f : scale * vst[u];
-  }
-  __syncthreads();
-
-  // ---- lower-triangle tiles of the trailing matrix
-  const int T0 = base >> 6, nt = (n + 63) >> 6, m = nt - T0;
-  const int total = m * (m + 1) / 2;
-  float pd = 0.f;
-  for (int t = bx; t < total; t += G) {
-    int ip = (int)((sqrtf(8.f * (float)t + 1.f) - 1.f) * 0.5f);
-    while ((ip + 1) * (ip + 2) / 2 <= t) ++ip;
-    while (ip * (ip + 1) / 2 > t) --ip;
-    const int jp = t - ip * (ip + 1) / 2;
-    const int I = T0 + ip, J = T0 + jp;
-    const int c = 64 * J + l;
-    const int rb = 64 * I + 16 * wv;
-    const bool cok = c > k && c < n;
-    float av[16];
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int r = rb + e;
-      av[e] = (cok && r > k && r < n) ? D.A[(int64_t)r * n + c] : 0.f;
-    }
-    const float vJ = cok ? sv[c - base] : 0.f;
-    float vI[16];
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int r = rb + e;
-      vI[e] = r < n ? sv[r - base] : 0.f;
-    }
-    float cs = 0.f, mine = 0.f, sct = 0.f;
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      cs += av[e] * vI[e];
-      const float rs = wave_sum_uniform(av[e] * vJ);
-      mine = l == e ? rs : mine;
-      sct += vI[e] * rs;
-    }
-    if (l < 16 && rb + l < n && rb + l > k) stc<COH>(D.P + (int64_t)J * n + rb + l, mine);
-    pd += (I == J ? 1.f : 2.f) * sct;
-    if (I != J) {
-      colp[wv][l] = cs;
-      __syncthreads();
-      if (threadIdx.x < 64) {
-        const float sum = (colp[0][l] + colp[1][l]) + (colp[2][l] + colp[3][l]);
-        if (cok) stc<COH>(D.P + (int64_t)I * n + c, sum);
-      }
-      __syncthreads();
-    }
-  }
-  pd = block_sum(l == 0 ? pd : 0.f, red);
-  if (threadIdx.x == 0) stc<COH>(D.part2 + bx, pd);
-}
-
-__global__ void __launch_bounds__(SY_T) sytrd_symv_tile_kernel(
-    const SytrdDesc* __restrict__ descs, int k, int p) {
-  const GView D = gview(descs[blockIdx.y]);
-  pin_desc(D);
-  symv_tile_body<false>(D, blockIdx.x, gridDim.x, k, p);
-}
-
-// ---- persistent panel kernel -------------------------------------------
-// One launch per panel runs its NB columns (col step, symv, col step, ...)
-// with two device-wide barriers per column instead of two dependent kernel
-// launches per column (a dependent dispatch alone costs ~3 us on MI355X, and
-// a column of the chain ~16 us: profiles/launch_floor_r4.json,
-// profiles/pmc/pmc_eig4608_r4.md).  Every member of the batch runs on the
-// same grid (P blocks per member); blocks that have no work at a step still
-// take part in the barriers.
-//
-// Barrier: each thread drains its own stores (s_waitcnt: the cross-block
-// data are agent-coherent sc1 stores, complete = visible at the coherence
-// point), the block synchronises, and one thread counts its arrival and
-// polls (relaxed agent-scope atomics, no L2 writeback / invalidate: nothing
-// shared goes through the L2).  Two-level by default (KFAC_SYTRD_BARRIER=flat:
-// one counter): a block arrives on one of SY_BAR_GRP group counters and the
-// last arrival of a group on the top counter, so no address takes more than
-// ~G/16 serialised atomics (one counter costs ~17 ns per arrival:
-// tools/grid_barrier_bench.cpp).  Termination is guaranteed: the host sizes
-// the grid to the chip's resident block count (all blocks co-resident), and
-// a poll that exceeds SY_BAR_TIMEOUT ticks of the 100 MHz wall clock (or sees
-// another block's error) sets the chain's sticky error flag and leaves;
-// later panel launches of the chain exit at once and the member's d[0] is
-// poisoned with NaN so the caller's non-finite repair re-solves it.
-// Control words (ctl): top[2] at 0..1 and group counters at 8 + 16 * parity
-// alternate between panel launches (launch j uses parity j & 1 and clears
-// the other set for launch j + 1), the error flag at 2.
-constexpr uint64_t SY_BAR_TIMEOUT = 200ull * 1000 * 1000;  // 2 s at 100 MHz
-constexpr int SY_BAR_GRP = 16;
-constexpr int SY_CTL_WORDS = 8 + 2 * SY_BAR_GRP;
-
-__device__ __forceinline__ bool grid_barrier(unsigned* ctl, int parity, unsigned epoch,
-                                             int tree, unsigned* err, const SytrdDesc* descs) {
-  __builtin_amdgcn_s_waitcnt(0);
-  __syncthreads();
-  __shared__ int s_ok;
-  if (threadIdx.x == 0) {
-    const unsigned G = gridDim.x * gridDim.y;
-    const unsigned me = blockIdx.y * gridDim.x + blockIdx.x;
-    unsigned* top = ctl + parity;
-    unsigned target;
-    if (tree) {
-      const unsigned g = me % SY_BAR_GRP;
-      const unsigned gsize = G / SY_BAR_GRP + (g < G % SY_BAR_GRP ? 1u : 0u);
-      const unsigned ngrp = G < (unsigned)SY_BAR_GRP ? G : (unsigned)SY_BAR_GRP;
-      unsigned* grp = ctl + 8 + SY_BAR_GRP * parity + g;
-      const unsigned old = __hip_atomic_fetch_add(grp, 1u, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-      if (old + 1 == epoch * gsize)
-        __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      target = epoch * ngrp;
-    } else {
-      __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      target = epoch * G;
-    }
-    const uint64_t t0 = wall_clock64();
-    int ok = 1;
-    while (__hip_atomic_load(top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(1);
-      if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
-        ok = 0;
-        break;
-      }
-      if (wall_clock64() - t0 > SY_BAR_TIMEOUT) {
-        __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ok = 0;
-        break;
-      }
-    }
-    if (!ok) {
-      // poison this member's result (every block that leaves does, so every
-      // member of the chain is covered): the caller's finiteness check
-      // re-solves it
-      const float nan = __builtin_nanf("");
-      __hip_atomic_store((float*)descs[blockIdx.y].d, nan, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    }
-    s_ok = ok;
-  }
-  __syncthreads();
-  return s_ok != 0;
-}
-
-// grid (P, batch); columns [p, q) of the panel, then the finalise-only col
-// step of column q when q < maxn (the host follows with the trailing update)
-template <int SY_SU, bool TILE>
-__global__ void __launch_bounds__(SY_T) sytrd_panel_kernel(
-    const SytrdDesc* __restrict__ descs, int p, int q, int maxn, unsigned* ctl, int tree) {
-  const int P = gridDim.x;
-  const int bx = blockIdx.x;
-  unsigned* err = ctl + 2;
-  const int parity = (p / SY_NB) & 1;
-  if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
-    // an earlier panel of this chain failed: keep every member poisoned
-    // (a later col step of the two-launch form may have rewritten d[0])
-    if (threadIdx.x == 0)
-      __hip_atomic_store((float*)descs[blockIdx.y].d, __builtin_nanf(""), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  if (bx == 0 && blockIdx.y == 0 && threadIdx.x <= SY_BAR_GRP) {
-    // the next panel launch's counters (nobody uses them during this launch)
-    unsigned* w = threadIdx.x == 0 ? ctl + (parity ^ 1)
-                                   : ctl + 8 + SY_BAR_GRP * (parity ^ 1) + threadIdx.x - 1;
-    __hip_atomic_store(w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  const GView D = gview(descs[blockIdx.y]);
-  pin_desc(D);
-  unsigned epoch = 0;
-  for (int k = p; k < q; ++k) {
-    // col step k: one block per 256 entries of row k (P >= that count)
-    col_body<true, TILE>(D, bx, k, p, 0, P);
-    if (!grid_barrier(ctl, parity, ++epoch, tree, err, descs)) return;
-    if (k < maxn - 1) {
-      if constexpr (TILE) symv_tile_body<true>(D, bx, P, k, p);
-      else symv_body<SY_SU, true>(D, bx, P, k, p);
-      if (!grid_barrier(ctl, parity, ++epoch, tree, err, descs)) return;
-    }
-  }
-  if (q < maxn) col_body<true, TILE>(D, bx, q, p, 1, P);
+  symv_body<SY_SU>(D, blockIdx.x, gridDim.x, k, p);
 }
 
 // trailing update A[q:,q:] -= V W^T + W V^T for the panel [p, q).
@@ -871,86 +536,12 @@ int sytrd_symv_blocks(int rows, int batch, int waves) {
   return g < 1 ? 1 : g;
 }
 
-// Persistent panels (sytrd_panel_kernel): KFAC_SYTRD_PERSIST = 0 (off), 1
-// (every panel) or R > 1 (panels with at most R rows left in the largest
-// member: the early columns stream so many bytes per column that the launch
-// latency hides behind them, the late ones are pure latency).  The grid is
-// KFAC_SYTRD_PERSIST_FRAC (default 0.25: three chains run concurrently) of
-// the chip's resident block count, never more than the whole of it.
-static int persist_rows() {
-  static const int v = [] {
-    const char* e = getenv("KFAC_SYTRD_PERSIST");
-    if (!e) return 0;
-    const int x = atoi(e);
-    return x == 1 ? (1 << 30) : (x < 0 ? 0 : x);
-  }();
-  return v;
-}
-
-static int tile_mode() {
-  static const int v = [] {
-    const char* e = getenv("KFAC_SYTRD_TILE");
-    return e && atoi(e) == 1 ? 1 : 0;
-  }();
-  return v;
-}
-
-static int panel_resident_blocks(int su) {
-  static int cap[4] = {-1, -1, -1, -1};
-  const int tile = tile_mode();
-  int& c = cap[(su == 8) + 2 * tile];
-  if (c < 0) {
-    int dev = 0, cus = 0, per = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (tile)
-      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, sytrd_panel_kernel<4, true>,
-                                                         SY_T, 0);
-    else if (su == 8)
-      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, sytrd_panel_kernel<8, false>,
-                                                         SY_T, 0);
-    else
-      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, sytrd_panel_kernel<4, false>,
-                                                         SY_T, 0);
-    c = cus * per;
-  }
-  return c;
-}
-
-// tile symv blocks per member at column k (two-launch form): the largest
-// member's lower-triangle tile count, capped by the wave budget and part2
-static int tile_blocks(int maxn, int k, int batch, int waves) {
-  if (waves <= 0) waves = 6 * 256 * 4;
-  const int T0 = ((k + 1) & ~63) >> 6, nt = (maxn + 63) >> 6, m = nt - T0;
-  int g = m * (m + 1) / 2;
-  const int budget = waves / 4 / (batch > 0 ? batch : 1);
-  if (g > budget) g = budget;
-  if (g > SY_MAXROWBLK) g = SY_MAXROWBLK;
-  return g < 1 ? 1 : g;
-}
-
-// blocks per member of a panel launch, or 0 when the panel cannot run
-// persistently (the grid would not be co-resident)
-static int panel_blocks(int maxn, int batch, int su) {
-  static const float frac = [] {
-    const char* e = getenv("KFAC_SYTRD_PERSIST_FRAC");
-    const float f = e ? (float)atof(e) : 0.25f;
-    return f > 0.f && f <= 1.f ? f : 0.25f;
-  }();
-  const int cap = panel_resident_blocks(su);
-  const int need = (int)ceil_div(maxn, SY_T);  // col-step chunks of row 0
-  int P = (int)((float)cap * frac) / (batch > 0 ? batch : 1);
-  if (P > SY_MAXROWBLK) P = SY_MAXROWBLK;
-  if (P < need) P = need;
-  if ((int64_t)P * batch > cap || P > SY_MAXROWBLK) return 0;
-  return P;
-}
-
-// Host driver: descs is a device table of `batch` descriptors (followed by
-// the chain's 3 control words), ns the host copy of their sizes.  Issues 2
-// launches per column of the largest matrix plus 2 per panel -- or one
-// persistent launch per panel plus the trailing update -- all on `stream`,
-// no host sync.
+// Host driver: descs is a device table of `batch` descriptors, ns the host
+// copy of their sizes.  Issues 2 launches per column of the largest matrix
+// plus 2 per panel, all on `stream`, no host sync.  (A persistent one-launch-
+// per-panel form with device-wide barriers and a lower-triangle tile symv
+// were measured slower -- 4608: 194 / 142 ms vs 103 ms, profiles/r5/
+// eigh_variants/ -- and removed in round 6.)
 void sytrd_batched_range(const SytrdDesc* descs_dev, const int* ns, int batch,
                          int k_begin, int k_end, hipStream_t stream, int waves) {
   int maxn = 0;
@@ -961,61 +552,9 @@ void sytrd_batched_range(const SytrdDesc* descs_dev, const int* ns, int batch,
     const char* e = getenv("KFAC_SYTRD_SU");
     return e && atoi(e) == 8 ? 8 : 4;
   }();
-  unsigned* ctl = reinterpret_cast<unsigned*>(
-      const_cast<char*>(reinterpret_cast<const char*>(descs_dev + batch)));
-  const int prow = persist_rows();
-  static const int tree = [] {
-    const char* e = getenv("KFAC_SYTRD_BARRIER");
-    return e && std::string(e) == "flat" ? 0 : 1;
-  }();
-  if (prow > 0 && k_begin == 0)
-    (void)hipMemsetAsync(ctl, 0, SY_CTL_WORDS * sizeof(unsigned), stream);
   // segments start on panel boundaries: panel [p, p+NB) is issued whole
   for (int p = k_begin; p < k_end; p += SY_NB) {
     const int q = (p + SY_NB < maxn) ? p + SY_NB : maxn;
-    const int P = (prow > 0 && maxn - p <= prow) ? panel_blocks(maxn, batch, su) : 0;
-    const int tile = tile_mode();
-    if (P > 0) {
-      const dim3 grid((unsigned)P, batch);
-      if (tile)
-        hipLaunchKernelGGL((sytrd_panel_kernel<4, true>), grid, dim3(SY_T), 0, stream, descs_dev,
-                           p, q, maxn, ctl, tree);
-      else if (su == 8)
-        hipLaunchKernelGGL((sytrd_panel_kernel<8, false>), grid, dim3(SY_T), 0, stream,
-                           descs_dev, p, q, maxn, ctl, tree);
-      else
-        hipLaunchKernelGGL((sytrd_panel_kernel<4, false>), grid, dim3(SY_T), 0, stream,
-                           descs_dev, p, q, maxn, ctl, tree);
-      if (q < maxn) {
-        const unsigned tiles = (unsigned)ceil_div(maxn - q, 64);
-        hipLaunchKernelGGL(sytrd_syr2k_kernel, dim3(tiles, tiles, batch), dim3(SY_T), 0,
-                           stream, descs_dev, q, p);
-      }
-      continue;
-    }
-    if (tile) {
-      for (int k = p; k < q; ++k) {
-        const int rem = maxn - k;
-        // cnt: the previous column's symv block count
-        hipLaunchKernelGGL(sytrd_col_tile_kernel, dim3((unsigned)ceil_div(rem, SY_T), batch),
-                           dim3(SY_T), 0, stream, descs_dev, k, p, 0,
-                           tile_blocks(maxn, k - 1, batch, waves));
-        if (k < maxn - 1)
-          hipLaunchKernelGGL(sytrd_symv_tile_kernel,
-                             dim3((unsigned)tile_blocks(maxn, k, batch, waves), batch),
-                             dim3(SY_T), 0, stream, descs_dev, k, p);
-      }
-      if (q < maxn) {
-        const int rem = maxn - q;
-        hipLaunchKernelGGL(sytrd_col_tile_kernel, dim3((unsigned)ceil_div(rem, SY_T), batch),
-                           dim3(SY_T), 0, stream, descs_dev, q, p, 1,
-                           tile_blocks(maxn, q - 1, batch, waves));
-        const unsigned tiles = (unsigned)ceil_div(rem, 64);
-        hipLaunchKernelGGL(sytrd_syr2k_kernel, dim3(tiles, tiles, batch), dim3(SY_T), 0,
-                           stream, descs_dev, q, p);
-      }
-      continue;
-    }
     for (int k = p; k < q; ++k) {
       const int rem = maxn - k;
       // the previous column's symv had maxn - k rows in the largest member

@@ -407,6 +407,16 @@ class BaseKFACPreconditioner:
         self._factor_a_events: dict[Any, torch.cuda.Event] = {}
         self._factor_inputs: list[tuple[torch.Tensor, int]] = []
         self._factor_stream_off = False
+        # Hook work queued for the side stream and launched a segment at a
+        # time (_flush_factor_segment): one stream fork / event / context
+        # switch per KFAC_FACTOR_SEGMENT layers instead of per layer (the
+        # per-hook stream switching was ~40 % of the eager factor step's
+        # host issue: profiles/r5/host_env/host_profile_factor.txt).  A
+        # pass's last layer (forward: the last registered, backward: the
+        # first) and every reader of the factors flush what is queued.
+        self._factor_pending: list[tuple[torch.Tensor, Callable[[], None], str, int]] = []
+        self._factor_segment = max(1, int(getenv('KFAC_FACTOR_SEGMENT', '8')))
+        self._layer_index = {m: i for i, m in enumerate(self._layers)}
         self._hook_handles: list[Any] = []
         for module in self._layers:
             self._hook_handles.append(
@@ -646,6 +656,8 @@ class BaseKFACPreconditioner:
         """Partial join: the current stream waits for the A-factor work only
         (the G SYRKs keep running on the side stream); the inputs' in-place
         modification check runs as in ``_join_factor_streams``."""
+        if self._factor_pending:
+            self._flush_factor_segment()
         for dev in self._factor_forked:
             ev = self._factor_a_events.get(dev)
             if ev is not None:
@@ -1012,6 +1024,8 @@ class BaseKFACPreconditioner:
     def _join_factor_streams(self) -> None:
         """Make the current stream wait for the factor side streams (every
         reader of the factors calls this first)."""
+        if self._factor_pending:
+            self._flush_factor_segment()
         if not self._factor_forked:
             return
         for dev in self._factor_forked:
@@ -1036,25 +1050,49 @@ class BaseKFACPreconditioner:
             )
 
     def _on_factor_stream(self, t: torch.Tensor, fn: Callable[[], None],
-                          which: str = 'G') -> None:
+                          which: str = 'G', last: bool = False) -> None:
         """Run ``fn`` (SYRK + EMA + all-reduce issue of one factor) on the
-        side stream after the work that produced ``t``; ``t`` is kept alive
-        for the side stream by the caching allocator."""
-        s = self._factor_stream(t)
-        if s is None:
+        side stream after the work that produced ``t``.
+
+        The work is queued and launched with the rest of its segment
+        (``_flush_factor_segment``): ``t`` stays referenced by the queue
+        until then, and by the caching allocator's stream record after.
+        ``last``: the pass's final hook -- flush now."""
+        if self._factor_pending and self._factor_pending[-1][2] != which:
+            self._flush_factor_segment()  # forward -> backward: A work goes first
+        if self._factor_stream(t) is None:
             fn()
             return
-        s.wait_stream(torch.cuda.current_stream(t.device))
+        self._factor_pending.append((t, fn, which, t._version))
+        if last or len(self._factor_pending) >= self._factor_segment:
+            self._flush_factor_segment()
+
+    def _flush_factor_segment(self) -> None:
+        """Launch the queued hook work on the side stream: one fork after
+        everything the compute stream has issued so far (which produced
+        every queued tensor), the layers' SYRKs in hook order, one A event."""
+        pending, self._factor_pending = self._factor_pending, []
+        if not pending:
+            return
+        dev = pending[0][0].device
+        s = self._factor_stream(pending[0][0])
+        if s is None:  # the side stream was switched off meanwhile: inline
+            for _, fn, _, _ in pending:
+                fn()
+            return
+        s.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(s):
-            fn()
-        if which == 'A':
-            ev = self._factor_a_events.get(t.device)
+            for _, fn, _, _ in pending:
+                fn()
+        if any(w == 'A' for _, _, w, _ in pending):
+            ev = self._factor_a_events.get(dev)
             if ev is None:
-                ev = self._factor_a_events[t.device] = torch.cuda.Event()
+                ev = self._factor_a_events[dev] = torch.cuda.Event()
             ev.record(s)
-        t.record_stream(s)
-        self._factor_inputs.append((t, t._version))
-        self._factor_forked.add(t.device)
+        for t, _, _, v in pending:
+            t.record_stream(s)
+            self._factor_inputs.append((t, v))
+        self._factor_forked.add(dev)
 
     @torch.no_grad()
     def _save_input(self, module: torch.nn.Module, input: tuple[torch.Tensor, ...]) -> None:
@@ -1079,7 +1117,8 @@ class BaseKFACPreconditioner:
                 with tracing.phase('factor_a'):
                     layer.save_and_update_a(list(input), alpha=decay)
                 layer.reduce_a_factor(group)
-            self._on_factor_stream(input[0], work, 'A')
+            self._on_factor_stream(input[0], work, 'A',
+                                   last=self._layer_index[module] == len(self._layers) - 1)
             return
         self._join_factor_streams()
         with tracing.phase('factor_a'):
@@ -1121,7 +1160,8 @@ class BaseKFACPreconditioner:
                 with tracing.phase('factor_g'):
                     layer.save_and_update_g(go, alpha=decay)
                 layer.reduce_g_factor(group)
-            self._on_factor_stream(grad_output[0], work)
+            self._on_factor_stream(grad_output[0], work, 'G',
+                                   last=self._layer_index[module] == 0)
             return
         self._join_factor_streams()
         with tracing.phase('factor_g'):

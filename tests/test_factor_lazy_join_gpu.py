@@ -18,13 +18,15 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _run(stream: str, join: str) -> tuple:
+def _run(stream: str, join: str, segment: str = '8') -> tuple:
     import distributed_kfac_pytorch_amd as kfac
     from tests.test_packed_factors import _Net
 
-    old = {k: os.environ.get(k) for k in ('KFAC_FACTOR_STREAM', 'KFAC_FACTOR_JOIN')}
+    old = {k: os.environ.get(k) for k in ('KFAC_FACTOR_STREAM', 'KFAC_FACTOR_JOIN',
+                                         'KFAC_FACTOR_SEGMENT')}
     os.environ['KFAC_FACTOR_STREAM'] = stream
     os.environ['KFAC_FACTOR_JOIN'] = join
+    os.environ['KFAC_FACTOR_SEGMENT'] = segment
     try:
         dev = torch.device('cuda', 0)
         torch.manual_seed(0)
@@ -58,11 +60,14 @@ def _run(stream: str, join: str) -> tuple:
                 os.environ[k] = v
 
 
-def test_lazy_factor_join_matches_inline() -> None:
+@pytest.mark.parametrize('segment', ['1', '2', '8'])
+def test_lazy_factor_join_matches_inline(segment: str) -> None:
+    """... for every side-stream segment size (hook work launched one
+    layer at a time, in pairs, or a whole pass at once)."""
     torch.backends.cudnn.deterministic = True
     inline = _run('0', 'lazy')
-    full = _run('1', 'full')
-    lazy = _run('1', 'lazy')
+    full = _run('1', 'full', segment)
+    lazy = _run('1', 'lazy', segment)
     assert inline[2] == 0 and full[2] == 0
     assert lazy[2] > 0, 'no factor work was left pending by step()'
     for other in (full, lazy):
