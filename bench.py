@@ -102,6 +102,11 @@ def parse_args() -> argparse.Namespace:
                    help='model compute dtype of the headline run: fp32 (the reference '
                         'ImageNet default, examples/torch_imagenet_resnet.py:73-76 --fp16 '
                         'off) or bf16 autocast')
+    p.add_argument('--secondary-exact-fp32', type=int, default=1,
+                   help='with an fp32 headline, also time the same K-FAC config with '
+                        'exact-fp32 model convolutions (1x1 on hipBLASLt fp32, 3x3 on '
+                        "MIOpen fp32: KFAC_CONV1X1_MATH=fp32, --conv-kxk miopen) and report "
+                        'it as the exact_fp32 field')
     p.add_argument('--fp32', action='store_true', help='alias of --dtype fp32')
     p.add_argument('--bf16', action='store_true', help='alias of --dtype bf16')
     p.add_argument('--secondary-bf16', type=int, default=1,
@@ -471,6 +476,22 @@ def main() -> None:
     sec = None
     if args.secondary_bf16 and not amp and not args.no_kfac:
         sec = run(args, True, rank, world, dev, True)
+    exact = None
+    if (args.secondary_exact_fp32 and not amp and not args.no_kfac and args.impl == 'native'
+            and (args.conv1x1 == 'gemm' or args.conv_kxk == 'gemm')):
+        # like-for-like with the reference's fp32 model math: every
+        # convolution product exact fp32 (the K-FAC math stays as reported in
+        # kfac_math)
+        old_math = os.environ.get('KFAC_CONV1X1_MATH')
+        os.environ['KFAC_CONV1X1_MATH'] = 'fp32'
+        try:
+            exact = run(argparse.Namespace(**{**vars(args), 'conv_kxk': 'miopen'}),
+                        True, rank, world, dev, False)
+        finally:
+            if old_math is None:
+                os.environ.pop('KFAC_CONV1X1_MATH', None)
+            else:
+                os.environ['KFAC_CONV1X1_MATH'] = old_math
     gb = args.batch_size * world
     window_value = gb * args.steps / res['seconds']
     # headline: period-averaged throughput (the reference baseline was timed
@@ -554,6 +575,16 @@ def main() -> None:
             # replayed from graphs (not just requested)
             'graphs': bool((sec.get('step_graphs') or {}).get('replays')),
             'step_graphs': sec.get('step_graphs'),
+        }
+    if exact is not None:
+        ms3 = exact.get('period_ms_per_step', exact['ms_per_step'])
+        v3 = gb * 1e3 / ms3
+        line['exact_fp32'] = {
+            'value': round(v3, 2), 'ms_per_step': round(ms3, 3),
+            'vs_baseline': round(v3 / (REFERENCE_IMG_S_PER_GPU['fp32'] * world), 4),
+            'kind_ms': exact['kind_ms'], 'params_finite': exact['params_finite'],
+            'model_math': 'fp32 (conv1x1 hipBLASLt fp32, conv3x3 / stem MIOpen fp32)',
+            'graphs': bool((exact.get('step_graphs') or {}).get('replays')),
         }
     if not args.no_kfac and args.impl == 'native':
         from distributed_kfac_pytorch_amd.ops import factors as fops
