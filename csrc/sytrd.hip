@@ -810,11 +810,12 @@ static int tri_blocks(int maxn, int k, int batch, int waves) {
 
 // KFAC_SYTRD_TRI: the triangle-tile symv runs while at least this many
 // trailing rows remain in the largest member (the bandwidth-bound early
-// columns); 0 = off.  Default 1536.
+// columns); 0 = off (the default: slower than the row symv so far, see
+// profiles/r6/tri_symv/).
 static int tri_min_rows() {
   static const int v = [] {
     const char* e = getenv("KFAC_SYTRD_TRI");
-    const int x = e ? atoi(e) : 1536;
+    const int x = e ? atoi(e) : 0;
     return x < 0 ? 0 : x;
   }();
   return v;

@@ -287,6 +287,9 @@ class GraphedTrainStep:
             # its first 10 iterations: a capture must come after them
             warmup = max(warmup, 11)
         self.warmup = warmup
+        self._eager_set_to_none = (
+            not isinstance(model, torch.nn.parallel.DistributedDataParallel)
+            and os.environ.get('KFAC_EAGER_SET_TO_NONE', '1') != '0')
         if enabled is None:
             multi = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
             enabled = torch.cuda.is_available() and (
@@ -412,7 +415,14 @@ class GraphedTrainStep:
         return loss.detach()
 
     def _eager_step(self) -> torch.Tensor:
-        self.optimizer.zero_grad(set_to_none=False)
+        # Without DDP an eager step drops the gradients first: autograd then
+        # hands its buffers to .grad (AccumulateGrad steals them) instead of
+        # one accumulate kernel per parameter -- 161 launches, ~0.9 ms of a
+        # ResNet-50 step (profiles/r6/model_step_profile_sgd.txt: aten::add_).
+        # The replays re-point .grad at their own buffers (_call).  A DDP
+        # model keeps them: its reducer copies a fresh gradient into the
+        # bucket view anyway, so dropping would buy nothing.
+        self.optimizer.zero_grad(set_to_none=self._eager_set_to_none)
         loss = self.forward_backward()
         if self.preconditioner is not None:
             self.preconditioner.step()
