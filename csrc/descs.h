@@ -96,7 +96,7 @@ struct SytrdDesc {
   float* part2;  // [SY_MAXROWBLK] symv partial w.v
   float* sc;     // [4 + 2 NB]: tau, v scale, t1.t2 of the last reflector,
                  // then t1 = W^T v and t2 = V^T v (tile symv)
-  float* P;      // [ceil(n / 128)][n] triangle-tile symv row partials
+  float* P;      // unused (was the tile symv's row partials; layout kept)
   int32_t n, pad;
 };
 

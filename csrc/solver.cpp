@@ -130,7 +130,6 @@ int sytrd_max_n();
 int sytrd_p1();
 int sytrd_maxch();
 int sytrd_maxrowblk();
-int sytrd_tri_tile();
 void sytrd_batched(const SytrdDesc* descs_dev, const int* ns, int batch,
                    hipStream_t stream);
 void sytrd_batched_range(const SytrdDesc* descs_dev, const int* ns, int batch,
@@ -158,8 +157,7 @@ static std::vector<at::Tensor> sytrd_setup(std::vector<at::Tensor>& stacks,
     const int64_t cnt = A.size(0), n = A.size(1);
     for (int64_t b = 0; b < cnt; ++b) ns.push_back((int)n);
     scratch += cnt * ((int64_t)NB * n + (int64_t)kfac::sytrd_maxch() * P1 +
-                      kfac::sytrd_maxrowblk() + 4 + 2 * NB +
-                      ((n + kfac::sytrd_tri_tile() - 1) / kfac::sytrd_tri_tile()) * n);
+                      kfac::sytrd_maxrowblk() + 4 + 2 * NB);
   }
   const int batch = (int)ns.size();
   if (batch == 0) return outs;
@@ -187,8 +185,7 @@ static std::vector<at::Tensor> sytrd_setup(std::vector<at::Tensor>& stacks,
       wp += kfac::sytrd_maxrowblk();
       D.sc = wp;
       wp += 4 + 2 * NB;
-      D.P = wp;  // triangle-tile symv slots [ceil(n / TT)][n]
-      wp += ((n + kfac::sytrd_tri_tile() - 1) / kfac::sytrd_tri_tile()) * n;
+      D.P = nullptr;
       D.n = (int)n;
       D.pad = 0;
     }

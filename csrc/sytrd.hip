@@ -47,18 +47,12 @@ constexpr int SY_RPW = SY_ROWS / (SY_T / 64);  // symv rows per wave (4)
 constexpr int SY_MAXN = 8192;             // v staged in LDS (32 KiB)
 constexpr int SY_MAXCH = SY_MAXN / SY_T;  // col-step chunks
 constexpr int SY_MAXROWBLK = SY_MAXN / SY_ROWS;
-// triangle-tile symv (sytrd_symv_tri_kernel): 128 x 128 tiles of the lower
-// triangle, one partial of A22 v per (tile, row) slot, at most SY_MAXN / TT
-// slots per row
-constexpr int TT = 128;
-constexpr int TT_MAXSLOT = SY_MAXN / TT;
 
 int sytrd_nb() { return SY_NB; }
 int sytrd_max_n() { return SY_MAXN; }
 int sytrd_p1() { return SY_P1; }
 int sytrd_maxch() { return SY_MAXCH; }
 int sytrd_maxrowblk() { return SY_MAXROWBLK; }
-int sytrd_tri_tile() { return TT; }
 
 namespace {
 
@@ -122,14 +116,6 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 // of column k) are formed by EVERY wave on its own -- wave reductions and
 // lane broadcasts, no LDS round trip -- so the kernel has one block
 // barrier, before the final cross-wave sums.
-//
-// TILE (the previous symv was the triangle-tile form): that symv left, per
-// row r >= k, one partial of A22 v per 128-wide tile slot (P[T][r], T >=
-// k / TT) plus t1 = W^T v, t2 = V^T v and t1.t2 in sc; this step sums the
-// slots -- all TM loads of a thread issued together with its panel loads --
-// and forms w = tau (A22 v - V t1 - W t2) and w.v = tau (v^T A22 v -
-// 2 t1.t2) itself (v^T A22 v = the sum of the symv's block partials).
-template <bool TILE, int TM>
 __device__ __forceinline__ void col_body(const GView& D, int bx, int k, int p, int fin_only,
                                          int cnt) {
   const int n = D.n;
@@ -155,7 +141,7 @@ __device__ __forceinline__ void col_body(const GView& D, int bx, int k, int p, i
     vj[j] = 0.f;
     wj[j] = 0.f;
   }
-  if (act && (!fin_only || TILE)) {
+  if (act && !fin_only) {
     if (!fin_only) a = ldc(D.A + (int64_t)k * n + r);
 #pragma unroll
     for (int j = 0; j < SY_NB; ++j) {
@@ -187,48 +173,10 @@ __device__ __forceinline__ void col_body(const GView& D, int bx, int k, int p, i
   float vraw = 0.f, wraw = 0.f;
   if (act && fin) {
     vraw = r == k ? 1.f : ldc(D.A + (int64_t)(k - 1) * n + r);
-    if (!TILE) wraw = ldc(D.Wt + (int64_t)(i - 1) * n + r);
+    wraw = ldc(D.Wt + (int64_t)(i - 1) * n + r);
   }
 
-  float alpha2 = 0.f;
-  if constexpr (TILE) {
-    if (fin) {
-      const int T0 = k / TT, nt = (n + TT - 1) / TT;
-      // this thread's row: every slot load in flight at once (clamped
-      // addresses, masked after)
-      float ps[TM];
-#pragma unroll
-      for (int u = 0; u < TM; ++u) {
-        const int T = T0 + u < nt ? T0 + u : nt - 1;
-        ps[u] = act ? ldc(D.P + (int64_t)T * n + r) : 0.f;
-      }
-      const float t1l = l < SY_NB ? ldc(D.sc + 4 + l) : 0.f;
-      const float t2l = l < SY_NB ? ldc(D.sc + 4 + SY_NB + l) : 0.f;
-      const float t12 = ldc(D.sc + 2);
-      // row k of the new column (lane i-1's panel entry), formed per wave
-      const float ykl = T0 + l < nt ? ldc(D.P + (int64_t)(T0 + l) * n + k) : 0.f;
-      float y = 0.f;
-#pragma unroll
-      for (int u = 0; u < TM; ++u) y += T0 + u < nt ? ps[u] : 0.f;
-      const int t1i = __builtin_bit_cast(int, t1l), t2i = __builtin_bit_cast(int, t2l);
-      float corr = 0.f;
-#pragma unroll
-      for (int j = 0; j < SY_NB; ++j) {
-        if (j < i - 1) {
-          const float t1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(t1i, j));
-          const float t2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(t2i, j));
-          corr += vj[j] * t1 + wj[j] * t2;
-        }
-      }
-      wraw = tp * (y - corr);
-      const float ck = (!fin_only && l < i - 1) ? cv_raw * t1l + cw_raw * t2l : 0.f;
-      const float wk = tp * (wave_sum_uniform(ykl) - wave_sum_uniform(ck));
-      if (l == i - 1) cw_raw = wk;
-      alpha2 = -0.5f * tp * tp * (wave_sum_uniform(s2) - 2.f * t12);
-    }
-  } else {
-    alpha2 = fin ? -0.5f * tp * wave_sum_uniform(s2) : 0.f;
-  }
+  const float alpha2 = fin ? -0.5f * tp * wave_sum_uniform(s2) : 0.f;
   // finalised W[k, i-1] gets the -tau/2 (w.v) v correction
   const float cw = l < i ? cw_raw + (l == i - 1 ? alpha2 : 0.f) : 0.f;
   const float cv = l < i ? cv_raw : 0.f;
@@ -294,12 +242,11 @@ __device__ __forceinline__ void col_body(const GView& D, int bx, int k, int p, i
   }
 }
 
-template <bool TILE, int TM>
 __global__ void __launch_bounds__(SY_T) sytrd_col_kernel(
     const SytrdDesc* __restrict__ descs, int k, int p, int fin_only, int cnt) {
   const GView D = gview(descs[blockIdx.y]);
   pin_desc(D);
-  col_body<TILE, TM>(D, blockIdx.x, k, p, fin_only, cnt);
+  col_body(D, blockIdx.x, k, p, fin_only, cnt);
 }
 
 // symv step for column k (k <= n-2).  grid (G, batch), G = sytrd_symv_blocks().
@@ -493,213 +440,6 @@ __global__ void __launch_bounds__(SY_T) sytrd_symv_kernel(
   symv_body<SY_SU>(D, blockIdx.x, gridDim.x, k, p);
 }
 
-// ---- triangle-tile symv: A22 v from the LOWER triangle only (half the
-// matrix bytes of the row symv, which streams whole rows of the symmetric
-// trailing matrix; the chain's early columns are bandwidth-bound: three
-// 4608 factors stream ~390 GB through the row symv).
-//
-// The trailing matrix is cut into 128 x 128 tiles on a fixed 128-aligned
-// grid (base = (k+1) rounded down); tile (I, J), I >= J, adds A_IJ v_J to
-// the rows of I (slot J) and, off the diagonal, A_IJ^T v_I to the rows of J
-// (slot I).  Every (slot, row) of the trailing rows is written exactly once
-// (no atomics: the next col step sums a row's slots in a fixed order, so
-// the chain stays bitwise reproducible).  A tile is read in two halves of
-// 64 rows; wave w takes 16 rows of a half, lane l columns l and 64 + l: one
-// coalesced 256-B row segment per load.  The column sums stay in the thread
-// and are combined over the 4 waves through LDS, the row sums are reduced
-// across the wave by recursive halving (16 values, 17 lane exchanges).
-// Every block writes its partial v^T A22 v (doubled off the diagonal) to
-// part2[b]; the reflector scalars and t1 / t2 / t1.t2 go to sc for the col
-// step (col_body<TILE>).  grid (G, batch).
-__device__ __forceinline__ void tri_of(int t, int& ip, int& jp) {
-  int x = (int)((sqrtf(8.f * (float)t + 1.f) - 1.f) * 0.5f);
-  while ((x + 1) * (x + 2) / 2 <= t) ++x;
-  while (x * (x + 1) / 2 > t) --x;
-  ip = x;
-  jp = t - x * (x + 1) / 2;
-}
-
-// rows TT I + 64 hf + 16 wv + e (e < 16) of tile t, columns TT J + l and
-// TT J + 64 + l; clamped addresses (masked by the caller)
-__device__ __forceinline__ void tri_load(const GView& D, int n, int T0, int t, int hf, int wv,
-                                         int l, float (&av)[16][2]) {
-  int ip, jp;
-  tri_of(t, ip, jp);
-  const int rb = TT * (T0 + ip) + 64 * hf + 16 * wv, cb = TT * (T0 + jp) + l;
-#pragma unroll
-  for (int e = 0; e < 16; ++e) {
-    const int rr = rb + e < n ? rb + e : n - 1;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int cc = cb + 64 * h < n ? cb + 64 * h : n - 1;
-      av[e][h] = D.A[(int64_t)rr * n + cc];
-    }
-  }
-}
-
-__global__ void __launch_bounds__(SY_T) sytrd_symv_tri_kernel(
-    const SytrdDesc* __restrict__ descs, int k, int p) {
-  const GView D = gview(descs[blockIdx.y]);
-  pin_desc(D);
-  const int n = D.n;
-  if (k >= n - 1) return;
-  const int bx = blockIdx.x, G = gridDim.x;
-  const int i = k - p;
-  __shared__ __attribute__((aligned(16))) float sv[SY_MAXN];
-  __shared__ float ptmp[SY_MAXCH * SY_P1];
-  __shared__ float red[SY_T / 64];
-  __shared__ float colp[2][SY_T / 64][TT];
-  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
-  const int base = (k + 1) & ~(TT - 1);
-  const int span = n - base;
-  const int T0 = base / TT, nt = (n + TT - 1) / TT, m = nt - T0;
-  const int total = m * (m + 1) / 2;
-  // ---- the first tile's first half, before the prologue (its loads
-  // depend on nothing the prologue computes)
-  float av[16][2];
-  if (bx < total) tri_load(D, n, T0, bx, 0, wv, l, av);
-  // ---- prologue (as the row symv): the col step's partials of column k,
-  // the raw reflector row, this lane's panel entry of column k+1, the pivot
-  float wa = 0.f;
-  if (l < i) wa = ldc(D.Wt + (int64_t)l * n + k + 1);
-  else if (l >= 32 && l - 32 < i) wa = ldc(D.A + (int64_t)(p + l - 32) * n + k + 1);
-  const float alpha = ldc(D.A + (int64_t)k * n + k + 1);
-  const int nch = (int)ceil_div(n - k, SY_T);
-  const int np1 = nch * SY_P1;
-  constexpr int PT = (SY_MAXCH * SY_P1 + SY_T - 1) / SY_T;
-  float pst[PT];
-#pragma unroll
-  for (int u = 0; u < PT; ++u) {
-    const int t = threadIdx.x + SY_T * u;
-    pst[u] = ldc(D.part1 + (t < np1 ? t : np1 - 1));
-  }
-  const GLOBAL float* arow = D.A + (int64_t)k * n;
-  constexpr int VT = SY_MAXN / SY_T;
-  float vst[VT];
-#pragma unroll
-  for (int u = 0; u < VT; ++u) {
-    const int c = threadIdx.x + SY_T * u;
-    const float v = ldc(arow + (c < span ? base + c : n - 1));
-    vst[u] = base + c > k + 1 && c < span ? v : 0.f;
-  }
-#pragma unroll
-  for (int u = 0; u < PT; ++u) {
-    const int t = threadIdx.x + SY_T * u;
-    if (t < np1) ptmp[t] = pst[u];
-  }
-  __syncthreads();
-  float xn2 = 0.f, xl = 0.f;
-  for (int c = 0; c < nch; ++c) {
-    xn2 += ptmp[c * SY_P1];
-    xl += ptmp[c * SY_P1 + 1 + l];
-  }
-  float tau_k, beta, scale;
-  if (xn2 == 0.f) {
-    tau_k = 0.f;
-    beta = alpha;
-    scale = 0.f;
-  } else {
-    beta = -copysignf(sqrtf(alpha * alpha + xn2), alpha);
-    tau_k = (beta - alpha) / beta;
-    scale = 1.f / (alpha - beta);
-  }
-  // t1 = W^T v (lanes < i), t2 = V^T v (lanes 32 .. 32 + i)
-  const bool tlive = l < i || (l >= 32 && l - 32 < i);
-  const float tl = tlive ? wa + scale * xl : 0.f;
-  if (bx == 0 && wv == 0) {
-    const float t2 = __shfl(tl, l + 32 < 64 ? l + 32 : l);
-    const float t12 = wave_sum_uniform(l < i ? tl * t2 : 0.f);
-    if (l < i) stc(D.sc + 4 + l, tl);
-    else if (l >= 32 && l - 32 < i) stc(D.sc + 4 + SY_NB + (l - 32), tl);
-    if (l == 0) {
-      stc(D.e + k, beta);
-      stc(D.tau + k, tau_k);
-      stc(D.sc, tau_k);
-      stc(D.sc + 1, scale);
-      stc(D.sc + 2, t12);
-    }
-  }
-  // the scaled reflector v (v[k+1] = 1, zero at and above row k)
-#pragma unroll
-  for (int u = 0; u < VT; ++u) {
-    const int c = threadIdx.x + SY_T * u;
-    if (c < span) sv[c] = base + c == k + 1 ? 1.f : scale * vst[u];
-  }
-  __syncthreads();
-
-  // ---- lower-triangle tiles
-  float pd = 0.f;
-  int buf = 0;
-  for (int t = bx; t < total; t += G) {
-    int ip, jp;
-    tri_of(t, ip, jp);
-    const int I = T0 + ip, J = T0 + jp;
-    const int cb = TT * J + l;
-    float vJ[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int c = cb + 64 * h;
-      vJ[h] = c > k && c < n ? sv[c - base] : 0.f;
-    }
-    float cs0 = 0.f, cs1 = 0.f;
-    // two halves of 64 rows, 16 per wave (no register prefetch of the next
-    // half / tile: more blocks per CU hide the latency instead)
-#pragma unroll 1
-    for (int hf = 0; hf < 2; ++hf) {
-      if (t != bx || hf != 0) tri_load(D, n, T0, t, hf, wv, l, av);
-      const int rb = TT * I + 64 * hf + 16 * wv;
-      float x[16];
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int r = rb + e;
-        const bool ok = r > k && r < n;
-        const float vI = ok ? sv[r - base] : 0.f;
-        // masked columns have vJ = 0 but their A entries must not reach the
-        // column sums: mask by column too
-        const float a0 = ok && cb > k && cb < n ? av[e][0] : 0.f;
-        const float a1 = ok && cb + 64 > k && cb + 64 < n ? av[e][1] : 0.f;
-        cs0 += a0 * vI;
-        cs1 += a1 * vI;
-        x[e] = a0 * vJ[0] + a1 * vJ[1];
-      }
-      // row sums: recursive halving over the wave (lane bits 5 .. 2 select
-      // the row), then the 4 lanes that differ in bits 1 and 0
-#pragma unroll
-      for (int st = 0; st < 4; ++st) {
-        const int M = 32 >> st, half = 8 >> st;
-        const bool up = (l & M) != 0;
-#pragma unroll
-        for (int j = 0; j < half; ++j) {
-          const float keep = up ? x[j + half] : x[j];
-          const float send = up ? x[j] : x[j + half];
-          x[j] = keep + __shfl_xor(send, M);
-        }
-      }
-      float rowdot = x[0] + __shfl_xor(x[0], 2);
-      rowdot += __shfl_xor(rowdot, 1);
-      const int re = rb + ((l >> 2) & 15);
-      if ((l & 3) == 0 && re > k && re < n) {
-        stc(D.P + (int64_t)J * n + re, rowdot);
-        pd += (I == J ? 1.f : 2.f) * sv[re - base] * rowdot;
-      }
-    }
-    if (I != J) {
-      colp[buf][wv][l] = cs0;
-      colp[buf][wv][64 + l] = cs1;
-      __syncthreads();
-      if (threadIdx.x < TT) {
-        const int c = TT * J + threadIdx.x;
-        const float sum = (colp[buf][0][threadIdx.x] + colp[buf][1][threadIdx.x]) +
-                          (colp[buf][2][threadIdx.x] + colp[buf][3][threadIdx.x]);
-        if (c > k && c < n) stc(D.P + (int64_t)I * n + c, sum);
-      }
-      buf ^= 1;
-    }
-  }
-  pd = block_sum(pd, red);
-  if (threadIdx.x == 0) stc(D.part2 + bx, pd);
-}
-
 // trailing update A[q:,q:] -= V W^T + W V^T for the panel [p, q).
 // grid (col tiles, row tiles, batch), 64x64 tiles, 16x16 threads x 4x4.
 __global__ void __launch_bounds__(SY_T) sytrd_syr2k_kernel(
@@ -796,52 +536,11 @@ int sytrd_symv_blocks(int rows, int batch, int waves) {
   return g < 1 ? 1 : g;
 }
 
-// triangle-tile symv blocks per member at column k: the largest member's
-// lower-triangle tile count, capped by the wave budget and part2
-static int tri_blocks(int maxn, int k, int batch, int waves) {
-  if (waves <= 0) waves = 6 * 256 * 4;
-  const int T0 = ((k + 1) & ~(TT - 1)) / TT, nt = (maxn + TT - 1) / TT, m = nt - T0;
-  int g = m * (m + 1) / 2;
-  const int budget = waves / 4 / (batch > 0 ? batch : 1);
-  if (g > budget) g = budget;
-  if (g > SY_MAXROWBLK) g = SY_MAXROWBLK;
-  return g < 1 ? 1 : g;
-}
-
-// KFAC_SYTRD_TRI: the triangle-tile symv runs while at least this many
-// trailing rows remain in the largest member (the bandwidth-bound early
-// columns); 0 = off (the default: slower than the row symv so far, see
-// profiles/r6/tri_symv/).
-static int tri_min_rows() {
-  static const int v = [] {
-    const char* e = getenv("KFAC_SYTRD_TRI");
-    const int x = e ? atoi(e) : 0;
-    return x < 0 ? 0 : x;
-  }();
-  return v;
-}
-
-template <bool TILE>
-static void launch_col(int maxn, dim3 grid, hipStream_t stream, const SytrdDesc* descs, int k,
-                       int p, int fin_only, int cnt) {
-  if (TILE && (maxn + TT - 1) / TT <= 40)
-    hipLaunchKernelGGL((sytrd_col_kernel<true, 40>), grid, dim3(SY_T), 0, stream, descs, k, p,
-                       fin_only, cnt);
-  else if (TILE)
-    hipLaunchKernelGGL((sytrd_col_kernel<true, TT_MAXSLOT>), grid, dim3(SY_T), 0, stream,
-                       descs, k, p, fin_only, cnt);
-  else
-    hipLaunchKernelGGL((sytrd_col_kernel<false, 1>), grid, dim3(SY_T), 0, stream, descs, k, p,
-                       fin_only, cnt);
-}
-
 // Host driver: descs is a device table of `batch` descriptors, ns the host
 // copy of their sizes.  Issues 2 launches per column of the largest matrix
-// plus 2 per panel, all on `stream`, no host sync.  The symv of column k is
-// the triangle-tile form while maxn - k - 1 >= KFAC_SYTRD_TRI rows remain,
-// the row form after; the col step of column k + 1 follows the form of
-// symv k.  (A persistent one-launch-per-panel form with device-wide
-// barriers was measured slower -- 4608: 194 vs 103 ms, profiles/r5/
+// plus 2 per panel, all on `stream`, no host sync.  (A persistent one-launch-
+// per-panel form with device-wide barriers and a lower-triangle tile symv
+// were measured slower -- 4608: 194 / 142 ms vs 103 ms, profiles/r5/
 // eigh_variants/ -- and removed in round 6.)
 void sytrd_batched_range(const SytrdDesc* descs_dev, const int* ns, int batch,
                          int k_begin, int k_end, hipStream_t stream, int waves) {
@@ -853,30 +552,18 @@ void sytrd_batched_range(const SytrdDesc* descs_dev, const int* ns, int batch,
     const char* e = getenv("KFAC_SYTRD_SU");
     return e && atoi(e) == 8 ? 8 : 4;
   }();
-  const int tmin = tri_min_rows();
-  auto tri = [&](int k) { return tmin > 0 && k >= 0 && maxn - k - 1 >= tmin; };
-  // blocks of the symv of column k (the count the next col step sums)
-  auto symv_g = [&](int k) {
-    return tri(k) ? tri_blocks(maxn, k, batch, waves)
-                  : sytrd_symv_blocks(maxn - k - 1, batch, waves);
-  };
   // segments start on panel boundaries: panel [p, p+NB) is issued whole
   for (int p = k_begin; p < k_end; p += SY_NB) {
     const int q = (p + SY_NB < maxn) ? p + SY_NB : maxn;
     for (int k = p; k < q; ++k) {
       const int rem = maxn - k;
-      const dim3 cgrid((unsigned)ceil_div(rem, SY_T), batch);
       // the previous column's symv had maxn - k rows in the largest member
-      if (tri(k - 1))
-        launch_col<true>(maxn, cgrid, stream, descs_dev, k, p, 0, symv_g(k - 1));
-      else
-        launch_col<false>(maxn, cgrid, stream, descs_dev, k, p, 0, symv_g(k - 1));
+      hipLaunchKernelGGL(sytrd_col_kernel, dim3((unsigned)ceil_div(rem, SY_T), batch),
+                         dim3(SY_T), 0, stream, descs_dev, k, p, 0,
+                         sytrd_symv_blocks(maxn - k, batch, waves));
       if (k < maxn - 1) {
-        const dim3 grid((unsigned)symv_g(k), batch);
-        if (tri(k))
-          hipLaunchKernelGGL(sytrd_symv_tri_kernel, grid, dim3(SY_T), 0, stream, descs_dev, k,
-                             p);
-        else if (su == 8)
+        const dim3 grid((unsigned)sytrd_symv_blocks(rem - 1, batch, waves), batch);
+        if (su == 8)
           hipLaunchKernelGGL(sytrd_symv_kernel<8>, grid, dim3(SY_T), 0, stream, descs_dev, k, p);
         else
           hipLaunchKernelGGL(sytrd_symv_kernel<4>, grid, dim3(SY_T), 0, stream, descs_dev, k, p);
@@ -884,11 +571,9 @@ void sytrd_batched_range(const SytrdDesc* descs_dev, const int* ns, int batch,
     }
     if (q < maxn) {
       const int rem = maxn - q;
-      const dim3 cgrid((unsigned)ceil_div(rem, SY_T), batch);
-      if (tri(q - 1))
-        launch_col<true>(maxn, cgrid, stream, descs_dev, q, p, 1, symv_g(q - 1));
-      else
-        launch_col<false>(maxn, cgrid, stream, descs_dev, q, p, 1, symv_g(q - 1));
+      hipLaunchKernelGGL(sytrd_col_kernel, dim3((unsigned)ceil_div(rem, SY_T), batch),
+                         dim3(SY_T), 0, stream, descs_dev, q, p, 1,
+                         sytrd_symv_blocks(maxn - q, batch, waves));
       const unsigned tiles = (unsigned)ceil_div(rem, 64);
       hipLaunchKernelGGL(sytrd_syr2k_kernel, dim3(tiles, tiles, batch), dim3(SY_T), 0,
                          stream, descs_dev, q, p);

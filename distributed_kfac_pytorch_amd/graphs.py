@@ -287,9 +287,6 @@ class GraphedTrainStep:
             # its first 10 iterations: a capture must come after them
             warmup = max(warmup, 11)
         self.warmup = warmup
-        self._eager_set_to_none = (
-            not isinstance(model, torch.nn.parallel.DistributedDataParallel)
-            and os.environ.get('KFAC_EAGER_SET_TO_NONE', '1') != '0')
         if enabled is None:
             multi = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
             enabled = torch.cuda.is_available() and (
@@ -415,14 +412,13 @@ class GraphedTrainStep:
         return loss.detach()
 
     def _eager_step(self) -> torch.Tensor:
-        # Without DDP an eager step drops the gradients first: autograd then
-        # hands its buffers to .grad (AccumulateGrad steals them) instead of
-        # one accumulate kernel per parameter -- 161 launches, ~0.9 ms of a
-        # ResNet-50 step (profiles/r6/model_step_profile_sgd.txt: aten::add_).
-        # The replays re-point .grad at their own buffers (_call).  A DDP
-        # model keeps them: its reducer copies a fresh gradient into the
-        # bucket view anyway, so dropping would buy nothing.
-        self.optimizer.zero_grad(set_to_none=self._eager_set_to_none)
+        # (Dropping the gradients here instead -- autograd's buffers handed
+        # over, no accumulate kernels -- was measured in round 6: the factor
+        # step's GPU time did not move, 17.39 vs 17.43 ms, and its host issue
+        # rose 12.6 -> 16.5 ms (fp32) and 18.4 -> 26.7 ms (bf16) rebuilding
+        # the grouped kernels' descriptor tables for the new addresses:
+        # profiles/r6/eager_set_to_none/.)
+        self.optimizer.zero_grad(set_to_none=False)
         loss = self.forward_backward()
         if self.preconditioner is not None:
             self.preconditioner.step()

@@ -112,13 +112,11 @@ print('ok', sorted({{t[0] for t in linalg.last_stats['tiers']}}))
 @pytest.mark.parametrize('env', [
     {},                                                          # default chain
     {'KFAC_SYTRD_SU': '8'},                                      # 8 column blocks in flight
-    {'KFAC_SYTRD_TRI': '0'},                                     # row symv only
-    {'KFAC_SYTRD_TRI': '129'},                                   # triangle-tile symv almost throughout
 ])
 def test_chain_variants_match_float64(env) -> None:
-    """Every Householder-chain variant (csrc/sytrd.hip: symv column blocks,
-    triangle-tile symv for none / the early / almost every column) on a mix
-    of chain sizes -- including ResNet-50's 256 / 512 / 576 -- twice in a fresh
+    """Every Householder-chain variant (csrc/sytrd.hip: symv column blocks in
+    flight) on a mix of chain sizes -- including ResNet-50's 256 / 512 / 576
+    -- twice in a fresh
     process (the variant is chosen once per process).  (The round-5
     persistent-panel and tile-symv variants, which returned wrong eigenpairs
     at 256 / 512 / 576 with PERSIST_FRAC 0.9 and were slower everywhere, are
