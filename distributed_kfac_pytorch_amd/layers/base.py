@@ -256,8 +256,9 @@ class KFACBaseLayer:
             self.grad = self._grad_buffer(self.module.device)
         g = self.grad
         if bucketed and self.tdc.bucket_cap_bytes > 0 and g.is_contiguous():
-            # fused per-(group, src) broadcast; flushed by the preconditioner
-            self.grad = self.tdc.broadcast_bucketed(g, src=src, group=group)
+            # fused per-group exchange (one all-gather of every member's
+            # share); flushed by the preconditioner
+            self.grad = self.tdc.exchange_bucketed(g, src=src, group=group)
         else:
             self.grad = self.tdc.broadcast(g, src=src, group=group)
 

@@ -423,6 +423,7 @@ class TorchDistributedCommunicator:
         self._bucket_cap_bytes = int(bucket_cap_mb * 1000 * 1000)
         self._allreduce_buckets: dict[Any, AllreduceTensorBucket | None] = {}
         self._broadcast_buckets: dict[Any, BroadcastTensorBucket] = {}
+        self._exchange_buckets: dict[Any, ExchangeTensorBucket] = {}
         self._packed: dict[Any, PackedFactorBuffer] = {}
 
     def packed_buffer(self, group: dist.ProcessGroup | None, dtype: torch.dtype,
@@ -595,11 +596,51 @@ class TorchDistributedCommunicator:
             self._broadcast_buckets[key] = bucket
         return bucket.add_tensor(tensor)
 
+    def exchange_bucketed(
+        self,
+        tensor: torch.Tensor,
+        *,
+        src: int,
+        group: dist.ProcessGroup | None = None,
+    ) -> AsyncTensor | torch.Tensor:
+        """Broadcast ``tensor`` from ``src`` to ``group`` through a per-group
+        exchange bucket: at flush every member contributes the tensors it is
+        the source of and receives the others' in ONE all-gather.
+
+        Used for the per-step preconditioned-gradient broadcasts (SURVEY C5:
+        every member of a KAISA receiver group is the source of some layers).
+        Per-(group, src) broadcasts run one after another on the group's
+        communicator, each using the links in one direction; the all-gather
+        sends every member's share at once, both directions of every xGMI
+        link busy (2-rank groups: half the time).  Same values, bit for bit,
+        as the broadcasts (``kfac/layers/base.py:223-251`` in the reference).
+        Every rank of ``group`` must add the same tensors (shapes, sources) in
+        the same order; the result is written in place on receivers."""
+        if get_world_size(group) == 1:
+            return tensor
+        if not tensor.is_contiguous():
+            raise RuntimeError('bucketed exchange needs contiguous tensors')
+        key = group
+        nbytes = tensor.numel() * tensor.element_size()
+        bucket = self._exchange_buckets.get(key)
+        if bucket is None:
+            bucket = ExchangeTensorBucket(group)
+            self._exchange_buckets[key] = bucket
+        elif bucket.size + nbytes > self._bucket_cap_bytes * get_world_size(group) or (
+                bucket.dtype is not None and bucket.dtype != tensor.dtype):
+            bucket.exchange()
+            bucket = ExchangeTensorBucket(group)
+            self._exchange_buckets[key] = bucket
+        return bucket.add_tensor(tensor, src)
+
     def flush_broadcast_buckets(self) -> None:
-        """Launch every pending broadcast bucket, in creation order."""
+        """Launch every pending broadcast and exchange bucket, in creation
+        order."""
         for key in list(self._broadcast_buckets):
             bucket = self._broadcast_buckets.pop(key)
             bucket.broadcast()
+        for key in list(self._exchange_buckets):
+            self._exchange_buckets.pop(key).exchange()
 
     def flush_allreduce_buckets(self) -> None:
         """Launch every partially filled bucket and every packed-factor
@@ -674,3 +715,84 @@ class BroadcastTensorBucket:
                     off += t.numel()
         self.work = dist.broadcast(self.flat, src=self._src, group=self._group, async_op=True)
         return self.work
+
+
+class ExchangeTensorBucket:
+    """Tensors of one KAISA receiver group, each from one source member,
+    exchanged by a single all-gather (``exchange_bucketed``).
+
+    Every member packs the tensors it is the source of into a send buffer
+    padded to the largest member's share; ``all_gather_into_tensor`` lays
+    the shares out in group-rank order; receivers copy theirs out.  Sizes
+    and sources are identical on every member, so every member computes the
+    same layout without communicating it."""
+
+    def __init__(self, group: dist.ProcessGroup | None) -> None:
+        self._group = group
+        self._entries: list[tuple[torch.Tensor, int, int]] = []  # tensor, src slot, offset
+        self._fill: dict[int, int] = {}  # src slot -> numel so far
+        self._size = 0
+        self._sent = False
+        self.dtype: torch.dtype | None = None
+        self.work: Any | None = None
+        self.flat: torch.Tensor | None = None
+        self._pad = 0
+        self._me = _group_rank(group, get_rank())
+
+    @property
+    def size(self) -> int:
+        return self._size
+
+    def communicated(self) -> bool:
+        return self._sent
+
+    def add_tensor(self, tensor: torch.Tensor, src: int) -> AsyncTensor:
+        if self._sent:
+            raise RuntimeError('bucket was already communicated')
+        if self.dtype is not None and tensor.dtype != self.dtype:
+            raise RuntimeError('an exchange bucket holds a single dtype')
+        self.dtype = tensor.dtype
+        slot = _group_rank(self._group, src)
+        off = self._fill.get(slot, 0)
+        n = tensor.numel()
+        self._fill[slot] = off + n
+        self._entries.append((tensor, slot, off))
+        self._size += n * tensor.element_size()
+
+        def _finish() -> torch.Tensor:
+            if slot != self._me:
+                assert self.flat is not None
+                start = slot * self._pad + off
+                comm_pack.scale_copy_(tensor, self.flat[start: start + n], 1.0)
+            return tensor
+
+        return AsyncTensor(finalize=_finish, bucket=self)  # type: ignore[arg-type]
+
+    def allreduce(self) -> Any:  # AsyncTensor resolves through .work
+        return self.exchange()
+
+    def exchange(self) -> Any | None:
+        if self._sent:
+            raise RuntimeError('bucket was already communicated')
+        self._sent = True
+        if not self._entries:
+            return None
+        size = get_world_size(self._group)
+        self._pad = max(self._fill.values())
+        ref = self._entries[0][0]
+        send = torch.zeros(self._pad, dtype=ref.dtype, device=ref.device)
+        for t, slot, off in self._entries:
+            if slot == self._me:
+                send[off: off + t.numel()].copy_(t.view(-1))
+        self.flat = torch.empty(size * self._pad, dtype=ref.dtype, device=ref.device)
+        self.work = dist.all_gather_into_tensor(self.flat, send, group=self._group,
+                                                async_op=True)
+        return self.work
+
+
+def _group_rank(group: dist.ProcessGroup | None, global_rank: int) -> int:
+    """Rank of ``global_rank`` inside ``group`` (its position in an
+    all-gather's output)."""
+    if group is None or not (dist.is_available() and dist.is_initialized()):
+        return global_rank
+    return dist.get_group_rank(group, global_rank)

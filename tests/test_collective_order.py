@@ -76,7 +76,8 @@ def _record(frac: float, method: str, bucket_mb: float, steps: int, packed: str 
     g = torch.Generator().manual_seed(rank)
     x = torch.randn(8, 3, 8, 8, generator=g)
     y = torch.randint(0, 10, (8,), generator=g)
-    for name in ('all_reduce', 'broadcast', 'all_gather', 'reduce_scatter'):
+    for name in ('all_reduce', 'broadcast', 'all_gather', 'all_gather_into_tensor',
+                 'reduce_scatter'):
         wrap(name)
     try:
         for _ in range(steps):

@@ -198,3 +198,33 @@ def _bcast_bucket_body():
 
 def test_broadcast_bucketed():
     _bcast_bucket_body()
+
+
+@distributed_test(4)
+def _exchange_bucket_body():
+    """Per-group gradient exchange (one all-gather per receiver group):
+    every member is the source of some tensors, shares are uneven, the cap
+    splits the bucket, and receivers get exactly the source's values."""
+    rank = dist.get_rank()
+    # two receiver groups {0, 1} and {2, 3} (KAISA rows at world 4, gwf 0.5)
+    groups = [dist.new_group([0, 1]), dist.new_group([2, 3])]
+    group = groups[rank // 2]
+    base = 2 * (rank // 2)
+    tdc = TorchDistributedCommunicator(bucket_cap_mb=3e-4)  # 300 bytes per member
+    shapes = [(2, 3), (4, 4), (10, 10), (1, 5), (7,), (3, 3)]
+    srcs = [base + s for s in (0, 1, 0, 0, 1, 1)]
+    handles, expect = [], []
+    for i, (shape, src) in enumerate(zip(shapes, srcs)):
+        val = torch.full(shape, float(i + 10 * src)) + torch.arange(
+            torch.Size(shape).numel(), dtype=torch.float32).view(shape)
+        t = val.clone() if rank == src else torch.full(shape, -1.0)
+        handles.append(tdc.exchange_bucketed(t, src=src, group=group))
+        expect.append(val)
+    tdc.flush_broadcast_buckets()
+    for h, e in zip(handles, expect):
+        out = h.wait() if isinstance(h, AsyncTensor) else h
+        assert torch.equal(out, e)
+
+
+def test_exchange_bucketed():
+    _exchange_bucket_body()

@@ -70,3 +70,37 @@ def test_training_single_process():
 )
 def test_training_distributed(world, frac, method, sym):
     run_distributed(_train, world, frac, method, sym)
+
+
+def _params_after(frac: float, method: str) -> list:
+    torch.manual_seed(7)
+    model = torch.nn.parallel.DistributedDataParallel(TinyModel())
+    opt = torch.optim.SGD(model.parameters(), lr=0.1)
+    pre = kfac.KFACPreconditioner(model, factor_update_steps=1, inv_update_steps=2,
+                                  grad_worker_fraction=frac, compute_method=method,
+                                  allreduce_bucket_cap_mb=0.0005)
+    g = torch.Generator().manual_seed(dist.get_rank())
+    x = torch.randn(16, 10, generator=g)
+    y = torch.randint(0, 10, (16,), generator=g)
+    for _ in range(6):
+        opt.zero_grad()
+        torch.nn.functional.cross_entropy(model(x), y).backward()
+        pre.step()
+        opt.step()
+    return [p.detach().clone() for p in model.parameters()]
+
+
+def _exchange_matches_local(method: str) -> None:
+    # HYBRID / MEM-OPT: receivers take the grad worker's preconditioned
+    # gradient through the per-group exchange; COMM-OPT computes it on every
+    # rank.  Same eigenbases (one inverse worker each), same bits.
+    local = _params_after(1.0, method)
+    for frac in (0.5, 1.0 / dist.get_world_size()):
+        got = _params_after(frac, method)
+        for a, b in zip(got, local):
+            assert torch.equal(a, b), (frac, float((a - b).abs().max()))
+
+
+@pytest.mark.parametrize('world,method', [(2, 'eigen'), (4, 'eigen'), (4, 'inverse')])
+def test_gradient_exchange_matches_comm_opt(world, method):
+    run_distributed(_exchange_matches_local, world, method)
