@@ -266,7 +266,6 @@ def _splitk(m: int, rows: int | None = None) -> int:
 # blocks the split-K weight gradients aim for (KFAC_WGRAD_SPLIT_BLOCKS, also
 # read by csrc/gemm3.hip gemm3_wgrad_splits): more splits fill the chip,
 # fewer shrink the partial-sum pass
-_WGRAD_SPLIT_BLOCKS = int(os.environ.get('KFAC_WGRAD_SPLIT_BLOCKS', '512'))
 
 
 def _wgrad_native(lib, gy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:  # type: ignore[no-untyped-def]
@@ -276,7 +275,7 @@ def _wgrad_native(lib, gy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:  # ty
     m, co = gy.shape
     ci = x.shape[1]
     tiles = -(-co // 128) * -(-ci // 128)
-    want = max(1, min(-(-_WGRAD_SPLIT_BLOCKS // tiles), (m // 32) // 8))
+    want = max(1, min(-(-int(getenv('KFAC_WGRAD_SPLIT_BLOCKS', '512')) // tiles), (m // 32) // 8))
     sp = int(lib.gemm3_mm_splits(m, want))
     if sp == 1:
         gw = torch.empty(co, ci, device=gy.device, dtype=gy.dtype)

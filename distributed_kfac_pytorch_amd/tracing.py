@@ -28,6 +28,8 @@ from typing import TypeVar
 
 import torch
 
+from distributed_kfac_pytorch_amd.utils.env import getenv
+
 RT = TypeVar('RT')
 
 _func_traces: dict[str, list[float]] = {}
@@ -167,9 +169,6 @@ def enable_phase_timing(enable: bool = True) -> PhaseTimer | None:
     return _PHASE_TIMER
 
 
-_DEBUG_SYNC = os.environ.get('KFAC_DEBUG_SYNC') == '1'
-
-
 def phase_timer() -> PhaseTimer | None:
     """The global phase timer, or None when phase timing is off."""
     return _PHASE_TIMER
@@ -180,7 +179,7 @@ def phase(name: str) -> Iterator[None]:
     """Record a K-FAC phase on the global timer (no-op when disabled, and
     while a HIP graph is being captured: event timing is not capturable)."""
     timer = _PHASE_TIMER
-    if _DEBUG_SYNC and torch.cuda.is_available() and not torch.cuda.is_current_stream_capturing():
+    if getenv('KFAC_DEBUG_SYNC') == '1' and torch.cuda.is_available() and not torch.cuda.is_current_stream_capturing():
         # KFAC_DEBUG_SYNC=1: synchronise after every phase so an asynchronous
         # device fault is reported by the phase that caused it
         yield
