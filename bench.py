@@ -170,10 +170,14 @@ def setup(args: argparse.Namespace) -> tuple[int, int, torch.device]:
             # captured RCCL collectives: the watchdog must not poll (and
             # abort on) events recorded inside a capture
             os.environ.setdefault('TORCH_NCCL_ASYNC_ERROR_HANDLING', '0')
+        # a rank that fails leaves the others waiting in a collective: give
+        # up after 5 minutes instead of the 10-minute default
+        import datetime
+        timeout = datetime.timedelta(seconds=300)
         if args.backend == 'nccl':
-            dist.init_process_group('nccl', device_id=dev)
+            dist.init_process_group('nccl', device_id=dev, timeout=timeout)
         else:
-            dist.init_process_group(args.backend)
+            dist.init_process_group(args.backend, timeout=timeout)
     return rank, world, dev
 
 

@@ -108,6 +108,29 @@ def _add_embeddings(
     return merged
 
 
+_GROUPS: dict = {}
+
+
+def _cached_new_group(ranks: list[int]) -> dist.ProcessGroup:
+    """``dist.new_group(ranks)``, created once per process and default group.
+
+    Every ``KFACPreconditioner`` asks for the same KAISA groups (reference:
+    one ``new_group`` per unique rank set per preconditioner,
+    ``kfac/preconditioner.py:283-295``).  On RCCL each group is a
+    communicator (init time and buffers per group), so a process that builds
+    several preconditioners -- the bench times K-FAC three times, a job that
+    rebuilds its model -- reuses them.  Every rank builds the same sequence
+    of preconditioners, so every rank hits or misses the cache together
+    (``new_group`` stays a collective called in the same order)."""
+    default = dist.distributed_c10d._get_default_group()
+    key = (id(default), tuple(sorted(ranks)))
+    pg = _GROUPS.get(key)
+    if pg is None or pg not in dist.distributed_c10d._world.pg_map:
+        pg = dist.new_group(ranks)
+        _GROUPS[key] = pg
+    return pg
+
+
 class KFACPreconditioner(BaseKFACPreconditioner):
     """KFAC distributed gradient preconditioner with KAISA placement."""
 
@@ -278,7 +301,7 @@ class KFACPreconditioner(BaseKFACPreconditioner):
             local_rank=get_rank(),
             world_size=size,
             grad_worker_fraction=frac,
-            group_func=(lambda ranks: dist.new_group(ranks)) if distributed else (lambda ranks: None),
+            group_func=_cached_new_group if distributed else (lambda ranks: None),
             colocate_factors=colocate_factors,
         )
         logger.log(loglevel, f'KFAC layer assignments: {assignment}')
