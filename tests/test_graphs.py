@@ -210,3 +210,20 @@ def test_graph_safe_conv_modes_cpu() -> None:
     assert type(m[0]) is GemmConv1x1 and type(m[2]) is GemmConv1x1
     assert type(m[3]) is torch.nn.Conv2d
     torch.testing.assert_close(m(x), ref, rtol=1e-5, atol=1e-6)
+
+
+def test_close_releases_graphs_and_drain_is_safe_without_gpu() -> None:
+    """``GraphedTrainStep.close()`` drops every graph (call it before
+    ``destroy_process_group``); ``drain_collectives`` is a no-op without a
+    GPU or a process group."""
+    from distributed_kfac_pytorch_amd.graphs import drain_collectives
+
+    drain_collectives()
+    _, opt, pre, fb = _setup(torch.device('cpu'))
+    runner = GraphedTrainStep(fb, opt, pre, enabled=False)
+    runner()
+    runner.graphs['plain'] = object()  # stand-in for a captured graph
+    runner.close()
+    assert not runner.graphs and not runner.enabled
+    runner()  # still steps, eagerly
+    assert runner.eager_steps == 2
