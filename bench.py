@@ -129,6 +129,9 @@ def parse_args() -> argparse.Namespace:
     p.add_argument('--cudnn-benchmark', type=int, default=0,
                    help='1: MIOpen find in every process (noisy); 0: immediate mode '
                         'with the shipped tuning db (miopen_db/)')
+    p.add_argument('--dump-steps', default='',
+                   help='write every timed step (kind, GPU ms, host issue ms) of the '
+                        'K-FAC run to this JSON file (rank 0)')
     p.add_argument('--profile-mark', action='store_true',
                    help='bracket the timed steps with marker kernels (rocprof windows)')
     p.add_argument('--conv1x1', default='gemm', choices=['miopen', 'gemm'],
@@ -381,6 +384,12 @@ def run(args: argparse.Namespace, use_kfac: bool, rank: int, world: int,
            'kind_counts': {k: kinds.count(k) for k in ('plain', 'factor', 'inverse')},
            'inverse_ms_each': [round(t, 1) for t, kk in zip(per_step, kinds) if kk == 'inverse'],
            'align_steps': align}
+    if args.dump_steps and rank == 0:
+        # one JSON line per timed run (K-FAC, SGD baseline, secondaries)
+        with open(args.dump_steps, 'a') as f:
+            f.write(json.dumps({'kfac': use_kfac, 'amp': amp, 'conv_kxk': args.conv_kxk,
+                                'kinds': kinds, 'gpu_ms': [round(t, 3) for t in per_step],
+                                'host_ms': [round(t, 3) for t in host_ms]}) + '\n')
     if precond is not None:
         # period-averaged step time at the reference cadence: one refresh,
         # (inv/factor - 1) factor-update steps and the rest plain steps per
@@ -624,6 +633,15 @@ def main() -> None:
               'refresh_ms_per_rank', 'params_finite'):
         if k in res:
             line[k] = res[k]
+    # runtime settings that serialise launches or change queueing: a box
+    # with any of these set times a different program (a replayed graph
+    # then blocks the host for its whole duration)
+    rt = {k: v for k, v in os.environ.items()
+          if k in ('HIP_LAUNCH_BLOCKING', 'AMD_SERIALIZE_KERNEL', 'AMD_SERIALIZE_COPY',
+                   'GPU_MAX_HW_QUEUES', 'HIP_FORCE_DEV_KERNARG', 'DEBUG_HIP_GRAPH_PACKET_CAPTURE',
+                   'HSA_ENABLE_SDMA', 'AMD_LOG_LEVEL', 'CUDA_LAUNCH_BLOCKING')}
+    if rt:
+        line['runtime_env'] = rt
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist.is_initialized():

@@ -39,8 +39,6 @@ input and the module's stride) and checkpoints are unchanged.
 """
 from __future__ import annotations
 
-import os
-
 import torch
 import torch.nn.functional as F
 from torch import nn
