@@ -96,12 +96,8 @@ void gemm3_grouped(const GemmDesc* table, int nlayers, int total_tiles,
 int gemm3s_align();
 int gemm3s_tile_m();
 int gemm3s_tile_n();
-int gemm3s_k_tile();
 int gemm3s_grid(int total_tiles);
 int64_t split_blocks_for(int64_t rows, int64_t total_cols);
-int64_t gemm3s_combine_blocks(int64_t M, int64_t N);
-void gemm3s_combine(const Gemm3sDesc* table, int n, int64_t total_blocks, bool out_split,
-                    hipStream_t s);
 void gemm3s_grouped(const Gemm3sDesc* table, int nlayers, int total_tiles, bool a_mc,
                     bool b_mc, bool out_split, hipStream_t s);
 void split_pad_multi(const SplitDesc* table, int n, int64_t total_blocks, hipStream_t s);
@@ -751,29 +747,19 @@ void check_extent(const at::Tensor& img, bool mc, int64_t mn, int64_t K, int64_t
 // Descriptor table of one grouped gemm3s launch; meta = (M, N, K) per GEMM.
 // The K padding of every image (columns / rows K..ru(K, 32)) must be zero:
 // images are allocated zeroed and only their logical part is ever written.
-// Returns (device table, GEMM tiles, pinned staging, combine layers, combine
-// blocks).  ksplits / parts (optional): split-K count and fp32 partial
-// workspace [ksplit][tiles_m * TM][tiles_n * TN] per layer; the table holds
-// the n GEMM descriptors followed by one combine descriptor per split layer
-// (tile_start = its first combine block), launched by gemm3s_combine.
-std::tuple<at::Tensor, int64_t, at::Tensor, int64_t, int64_t> build_gemm3s_table(
+std::tuple<at::Tensor, int64_t, at::Tensor> build_gemm3s_table(
     const std::vector<at::Tensor>& As, const std::vector<at::Tensor>& Bs,
     const std::vector<at::Tensor>& Cs, const std::vector<c10::optional<at::Tensor>>& Ss,
     const std::vector<c10::optional<at::Tensor>>& dgs,
     const std::vector<c10::optional<at::Tensor>>& das, const std::vector<int64_t>& meta,
     const std::vector<double>& dampings, bool a_mc, bool b_mc, bool out_split,
-    const c10::optional<at::Tensor>& host_buf, const std::vector<int64_t>& ksplits,
-    const std::vector<c10::optional<at::Tensor>>& parts) {
+    const c10::optional<at::Tensor>& host_buf) {
   const size_t n = As.size();
   TORCH_CHECK(Bs.size() == n && Cs.size() == n && Ss.size() == n && dgs.size() == n &&
                   das.size() == n && dampings.size() == n && meta.size() == 3 * n,
               "build_gemm3s_table: list sizes");
-  TORCH_CHECK((ksplits.empty() && parts.empty()) || (ksplits.size() == n && parts.size() == n),
-              "build_gemm3s_table: ksplits / parts sizes");
   const int64_t tm = kfac::gemm3s_tile_m(), tn = kfac::gemm3s_tile_n();
   std::vector<kfac::Gemm3sDesc> host(n);
-  std::vector<kfac::Gemm3sDesc> comb;
-  int64_t comb_blocks = 0;
   int tiles = 0;
   for (size_t i = 0; i < n; ++i) {
     const int64_t M = meta[3 * i], N = meta[3 * i + 1], K = meta[3 * i + 2];
@@ -829,51 +815,14 @@ std::tuple<at::Tensor, int64_t, at::Tensor, int64_t, int64_t> build_gemm3s_table
     d.N = (int32_t)N;
     d.K = (int32_t)K;
     d.tiles_n = (int32_t)((N + tn - 1) / tn);
-    d.tiles_m = (int32_t)((M + tm - 1) / tm);
     d.tile_start = tiles;
-    d.ksplit = 1;
-    d.part = nullptr;
-    int64_t ks = ksplits.empty() ? 1 : ksplits[i];
-    if (ks > 1) {
-      // every part gets at least one k-tile (of gemm3s_k_tile() columns)
-      const int64_t kt = kfac::gemm3s_k_tile(), nk = (K + kt - 1) / kt;
-      const int64_t per = (nk + ks - 1) / ks;
-      ks = (nk + per - 1) / per;
-    }
-    if (ks > 1) {
-      TORCH_CHECK(parts[i].has_value() && parts[i]->defined(), "split layer needs a workspace");
-      const auto& P = *parts[i];
-      check_cuda(P, "part");
-      TORCH_CHECK(P.scalar_type() == at::kFloat && P.is_contiguous() &&
-                      P.numel() >= ks * d.tiles_m * tm * d.tiles_n * tn &&
-                      (reinterpret_cast<uintptr_t>(P.data_ptr()) & 15) == 0,
-                  "part: contiguous fp32 [ksplit][tiles_m * TM][tiles_n * TN]");
-      d.ksplit = (int32_t)ks;
-      d.part = P.data_ptr<float>();
-      kfac::Gemm3sDesc c = d;
-      c.tile_start = (int32_t)comb_blocks;
-      comb_blocks += kfac::gemm3s_combine_blocks(M, N);
-      comb.push_back(c);
-    }
-    tiles += (int)(d.tiles_m * d.tiles_n * d.ksplit);
+    tiles += (int)((M + tm - 1) / tm) * d.tiles_n;
     host[i] = d;
   }
-  host.insert(host.end(), comb.begin(), comb.end());
-  const int64_t nbytes = (int64_t)(host.size() * sizeof(kfac::Gemm3sDesc));
+  const int64_t nbytes = (int64_t)(n * sizeof(kfac::Gemm3sDesc));
   at::Tensor dev_t, cpu;
   if (n > 0) std::tie(dev_t, cpu) = upload_table(host.data(), nbytes, As[0].device(), host_buf);
-  return {dev_t, tiles, cpu, (int64_t)comb.size(), comb_blocks};
-}
-
-// the combine launch of a split-K grouped GEMM: the `ncomb` descriptors
-// after the first `n` of `table`
-void gemm3s_combine(const at::Tensor& table, int64_t n, int64_t ncomb, int64_t blocks,
-                    bool out_split) {
-  check_cuda(table, "table");
-  TORCH_CHECK(table.numel() >= (n + ncomb) * (int64_t)sizeof(kfac::Gemm3sDesc));
-  c10::hip::HIPGuardMasqueradingAsCUDA g(table.device());
-  kfac::gemm3s_combine((const kfac::Gemm3sDesc*)table.data_ptr() + n, (int)ncomb, blocks,
-                       out_split, cur_stream());
+  return {dev_t, tiles, cpu};
 }
 
 void gemm3s_grouped(const at::Tensor& table, int64_t n, int64_t tiles, bool a_mc, bool b_mc,
@@ -1563,11 +1512,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("b_kc"), py::arg("splits") = 1);
   m.def("gemm3_mm_splits", &gemm3_mm_splits_for, py::arg("k"), py::arg("want"));
   m.def("gemm3s_align", &kfac::gemm3s_align);
-  m.def("gemm3s_tile_m", &kfac::gemm3s_tile_m);
-  m.def("gemm3s_tile_n", &kfac::gemm3s_tile_n);
   m.def("build_gemm3s_table", &build_gemm3s_table);
   m.def("gemm3s_grouped", &gemm3s_grouped);
-  m.def("gemm3s_combine", &gemm3s_combine);
   m.def("build_split_table", &build_split_table);
   m.def("split_pad_multi", &split_pad_multi);
   m.def("build_cast_table", &build_cast_table);

@@ -60,12 +60,6 @@ struct Gemm3sDesc {
   int32_t M, N, K;
   int32_t tiles_n, tile_start;
   float damping;
-  // split-K (gemm3s_grouped): ksplit > 1 runs the K range as ksplit parts
-  // whose raw fp32 tiles go to part[ksplit][tiles_m * TM][tiles_n * TN]; a
-  // combine launch (gemm3s_combine) sums them in fixed order and applies the
-  // epilogue (scaling, split image or fp32 output)
-  int32_t ksplit, tiles_m;
-  float* part;
 };
 
 // gemm3s.hip: fp32 [rows][cols] (+ one extra column read from a vector)

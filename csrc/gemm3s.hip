@@ -198,12 +198,8 @@ gemm3s_kernel(const Gemm3sDesc* __restrict__ descs, int nlayers, int total_tiles
   const int t = ((rr / CH) * 8 + xcd) * CH + (rr % CH);
   if (t >= total_tiles) return;
   const Gemm3sDesc d = descs[find_tile_layer(descs, nlayers, t)];
+  const int tl = t - d.tile_start;
   const int tiles_m = (d.M + BM - 1) / BM;
-  // split-K: part kp (slowest, so the blocks scheduled together share the
-  // operand panels as before) of the layer's k-tiles
-  const int ks = d.ksplit > 1 ? d.ksplit : 1;
-  const int kp = (t - d.tile_start) / (tiles_m * d.tiles_n);
-  const int tl = t - d.tile_start - kp * tiles_m * d.tiles_n;
   const int per_group = GM * d.tiles_n;
   const int first_m = (tl / per_group) * GM;
   const int gm = min(tiles_m - first_m, GM);
@@ -215,13 +211,10 @@ gemm3s_kernel(const Gemm3sDesc* __restrict__ descs, int nlayers, int total_tiles
   const int l = threadIdx.x & 63;
   const int wr = w / WN, wc = w % WN;
 
-  const int nt_all = (d.K + SK - 1) / SK;
-  const int kt_per = (nt_all + ks - 1) / ks;
-  const int kt0 = kp * kt_per;
   auto stage = [&](int kt) {
     if constexpr (GEMM3S_DIAG == 1) return;
     uint16_t* base = lds + (kt % NSTAGE) * STAGE;
-    const int k0 = (kt0 + kt) * SK;
+    const int k0 = kt * SK;
 #pragma unroll
     for (int j = 0; j < IPW; ++j) {
       const int idx = w * IPW + j;  // wave-uniform
@@ -245,7 +238,7 @@ gemm3s_kernel(const Gemm3sDesc* __restrict__ descs, int nlayers, int total_tiles
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
-  const int nt = min(nt_all - kt0, kt_per);
+  const int nt = (d.K + SK - 1) / SK;
   // NSTAGE - 1 k-tiles in flight.  With NSTAGE == 2 the wait + barrier at
   // the end of each k-tile is the plain double buffer; with NSTAGE == 3 the
   // next-but-one tile's DMA stays in flight across the barrier (counted
@@ -345,8 +338,7 @@ gemm3s_kernel(const Gemm3sDesc* __restrict__ descs, int nlayers, int total_tiles
   // clamped addresses: 4 memory round trips per wave instead of one per
   // element (loads inside the per-element bounds branch were each waited
   // for alone: 64 dependent round trips per tile in the T2 launch).
-  // a split-K part stores its raw sums (the combine launch scales them)
-  const int kind = ks > 1 ? 0 : (d.S != nullptr ? 1 : (d.dg != nullptr ? 2 : 0));
+  const int kind = d.S != nullptr ? 1 : (d.dg != nullptr ? 2 : 0);
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
 #pragma unroll
@@ -399,15 +391,7 @@ gemm3s_kernel(const Gemm3sDesc* __restrict__ descs, int nlayers, int total_tiles
       const int m = mw0 + i * 32 + rl;
       const int n = nw0 + c8;
       const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-      if (ks > 1) {
-        // raw partial tile: the padded [tiles_m * BM][tiles_n * BN] part
-        // plane holds every (m, n) of the tile, zeros past M / N
-        const int64_t np = (int64_t)d.tiles_n * BN;
-        GLOBAL float* c = (GLOBAL float*)d.part + (int64_t)kp * tiles_m * BM * np +
-                          (int64_t)m * np + n;
-        *(GLOBAL f4*)c = x0;
-        *(GLOBAL f4*)(c + 4) = x1;
-      } else if constexpr (OUT_SPLIT) {
+      if constexpr (OUT_SPLIT) {
         // whole chunk, padding included (the image rows / columns are
         // padded to 256 and these values are 0 there)
         typedef unsigned short u8v __attribute__((ext_vector_type(8)));
@@ -525,70 +509,6 @@ constexpr int TBM = 256, TBN = 256, TWM = 2, TWN = 4;
 #endif
 constexpr int TNS = GEMM3S_NSTAGE;
 
-// ---- split-K combine: out = epilogue(sum_kp part[kp]) for every layer of
-// a grouped launch that ran split (descs[i].tile_start = the layer's first
-// combine block).  Each thread owns 4 consecutive columns of one row; the
-// parts are summed in ascending kp (fixed order: bitwise reproducible).
-constexpr int CBT = 256;
-
-__device__ __forceinline__ int find_combine(const Gemm3sDesc* d, int n, int blk) {
-  int lo = 0, hi = n - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (d[mid].tile_start <= blk) lo = mid;
-    else hi = mid - 1;
-  }
-  return lo;
-}
-
-template <bool OUT_SPLIT>
-__global__ void __launch_bounds__(CBT)
-gemm3s_combine_kernel(const Gemm3sDesc* __restrict__ descs, int n) {
-  const Gemm3sDesc d = descs[find_combine(descs, n, blockIdx.x)];
-  const int q = (blockIdx.x - d.tile_start) * CBT + threadIdx.x;
-  const int qpr = (d.N + 3) >> 2;
-  const int m = q / qpr, n0 = (q - m * qpr) * 4;
-  if (m >= d.M) return;
-  const int tiles_m = (d.M + TBM - 1) / TBM;
-  const int64_t np = (int64_t)d.tiles_n * TBN, plane = (int64_t)tiles_m * TBM * np;
-  typedef float f4 __attribute__((ext_vector_type(4)));
-  const GLOBAL float* p = (const GLOBAL float*)d.part + (int64_t)m * np + n0;
-  f4 acc = *(const GLOBAL f4*)p;
-  for (int kp = 1; kp < d.ksplit; ++kp) acc += *(const GLOBAL f4*)(p + kp * plane);
-  float v[4] = {acc.x, acc.y, acc.z, acc.w};
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const int nn = min(n0 + e, d.N - 1);
-    if (d.S != nullptr) v[e] *= ((const GLOBAL float*)d.S)[(int64_t)m * d.lds + nn];
-    else if (d.dg != nullptr)
-      v[e] = v[e] / (((const GLOBAL float*)d.dg)[m] *
-                         (d.da != nullptr ? ((const GLOBAL float*)d.da)[nn] : 0.f) +
-                     d.damping);
-    if (n0 + e >= d.N) v[e] = 0.f;
-  }
-  if constexpr (OUT_SPLIT) {
-    // whole 4-chunk (the image is padded past N; those values are 0)
-    typedef unsigned short u4v __attribute__((ext_vector_type(4)));
-    u4v hv, lv;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      uint16_t h, lo;
-      split1(v[e], h, lo);
-      hv[e] = h;
-      lv[e] = lo;
-    }
-    GLOBAL uint16_t* c = (GLOBAL uint16_t*)d.C + (int64_t)m * d.ldc + n0;
-    *(GLOBAL u4v*)c = hv;
-    *(GLOBAL u4v*)(c + d.c_plane) = lv;
-  } else {
-    GLOBAL float* c = (GLOBAL float*)d.C + (int64_t)m * d.ldc + n0;
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-      if (n0 + e < d.N) c[e] = v[e];
-  }
-}
-
-
 }  // namespace
 
 // split images are padded to this many rows / columns (every tile config's
@@ -596,7 +516,6 @@ gemm3s_combine_kernel(const Gemm3sDesc* __restrict__ descs, int n) {
 int gemm3s_align() { return 256; }
 int gemm3s_tile_m() { return TBM; }
 int gemm3s_tile_n() { return TBN; }
-int gemm3s_k_tile() { return SK; }
 
 int gemm3s_grid(int total_tiles) {
   const int per = 8 * CH;
@@ -621,19 +540,6 @@ void gemm3s_grouped(const Gemm3sDesc* table, int nlayers, int total_tiles, bool 
   G3S(false, true, true) G3S(true, false, false) G3S(true, false, true)
   G3S(true, true, false) G3S(true, true, true)
 #undef G3S
-}
-
-int64_t gemm3s_combine_blocks(int64_t M, int64_t N) {
-  return ceil_div(M * ceil_div(N, 4), (int64_t)CBT);
-}
-
-void gemm3s_combine(const Gemm3sDesc* table, int n, int64_t total_blocks, bool out_split,
-                    hipStream_t s) {
-  if (n <= 0 || total_blocks <= 0) return;
-  if (out_split)
-    gemm3s_combine_kernel<true><<<dim3((unsigned)total_blocks), dim3(CBT), 0, s>>>(table, n);
-  else
-    gemm3s_combine_kernel<false><<<dim3((unsigned)total_blocks), dim3(CBT), 0, s>>>(table, n);
 }
 
 void split_pad_multi(const SplitDesc* table, int n, int64_t total_blocks, hipStream_t s) {

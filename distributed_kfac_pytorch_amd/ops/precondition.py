@@ -628,33 +628,6 @@ def _ru(x: int, m: int) -> int:
     return (x + m - 1) // m * m
 
 
-def _ksplits(dims: list[tuple[int, int, int]], device: torch.device) -> list[int]:
-    """Split-K parts per GEMM of one grouped launch (``KFAC_G3S_SPLITK``, 1 =
-    on).  A launch lasts as long as its longest tile, and one 256 x 256 tile
-    with K = 4608 (ResNet-50 layer4 conv2, T1 / T4) is ~2x the average
-    per-CU share of the whole launch: ~108 CUs grind through those while the
-    rest idle (T1 / T4 0.38 ms, T2 / T3 0.17 ms per step:
-    profiles/r6/prof_r6j/window.txt).  A GEMM whose K exceeds the per-CU
-    share of the launch's tile-k work is cut into ceil(K / share) parts
-    (at most 8, at least 512 of K each); a combine launch sums the parts in
-    fixed order."""
-    if getenv('KFAC_G3S_SPLITK', '1') == '0' or not dims:
-        return [1] * len(dims)
-    lib = native()
-    tm, tn = int(lib.gemm3s_tile_m()), int(lib.gemm3s_tile_n())
-    tiles = [-(-m // tm) * -(-n // tn) for m, n, _ in dims]
-    work = sum(t * k for t, (_, _, k) in zip(tiles, dims))
-    cus = torch.cuda.get_device_properties(device).multi_processor_count
-    share = max(work / max(cus, 1), 512.0)
-    out = []
-    for _, _, k in dims:
-        ks = 1
-        if k > share:
-            ks = max(1, min(8, -(-k // int(share)), k // 512))
-        out.append(ks)
-    return out
-
-
 class SplitGroupedPrecondition(GroupedPrecondition):
     """The grouped preconditioning GEMMs on PRE-SPLIT operands
     (csrc/gemm3s.hip): every operand lives in a bf16 hi/lo "split image"
@@ -701,25 +674,6 @@ class SplitGroupedPrecondition(GroupedPrecondition):
     def _capturing() -> bool:
         return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
 
-    def _part(self, st: dict, name: str, ks: int, dims: tuple) -> torch.Tensor | None:
-        """The persistent fp32 split-K workspace of one layer's ``name``
-        GEMM ([ks][M rounded to the tile][N rounded to the tile]), or None
-        when it would have to be allocated inside a capture."""
-        lib = native()
-        tm, tn = int(lib.gemm3s_tile_m()), int(lib.gemm3s_tile_n())
-        m, n, _ = dims
-        numel = ks * _ru(m, tm) * _ru(n, tn)
-        buf = st.get('part_' + name)
-        if buf is None or buf.numel() < numel:
-            if self._capturing():
-                return None
-            if buf is not None:
-                # cached tables still address the old workspace: keep it
-                st.setdefault('part_retired', []).append(buf)
-            buf = torch.empty(numel, dtype=torch.float32, device=st['w'].device)
-            st['part_' + name] = buf
-        return buf
-
     def _resplit(self, todo: list) -> None:
         """Split static operands whose content changed (one launch)."""
         if not todo:
@@ -763,19 +717,19 @@ class SplitGroupedPrecondition(GroupedPrecondition):
                         out.data_ptr(), st['w'].data_ptr()))
             none3 = (None, None, None)
             if kind == 'eigen':
-                t['t1'].append((st['w'], st['fa'], st['t1'], none3, (g, a, a), st))
+                t['t1'].append((st['w'], st['fa'], st['t1'], none3, (g, a, a)))
                 if layer.prediv_eigenvalues:
                     scale = (layer.dgda, None, None)
                 else:
                     scale = (None, layer.dg, layer.da)
                 key.append((layer.prediv_eigenvalues,) + tuple(
                     None if s is None else s.data_ptr() for s in scale))
-                t['t2'].append((st['fg'], st['t1'], st['t2'], scale, (g, a, g), st))
-                t['t3e'].append((st['fg'], st['t2'], st['t3'], none3, (g, a, g), st))
-                t['t4'].append((st['t3'], st['fa'], out, none3, (g, a, a), st))
+                t['t2'].append((st['fg'], st['t1'], st['t2'], scale, (g, a, g)))
+                t['t3e'].append((st['fg'], st['t2'], st['t3'], none3, (g, a, g)))
+                t['t4'].append((st['t3'], st['fa'], out, none3, (g, a, a)))
             else:
-                t['t1'].append((st['w'], st['fa'], st['t1'], none3, (g, a, a), st))
-                t['t3i'].append((st['fg'], st['t1'], out, none3, (g, a, g), st))
+                t['t1'].append((st['w'], st['fa'], st['t1'], none3, (g, a, a)))
+                t['t3i'].append((st['fg'], st['t1'], out, none3, (g, a, g)))
         if todo and self._capturing():
             # a basis changed since the last eager step: its split images are
             # refreshed eagerly (never inside a capture); capture the
@@ -790,38 +744,28 @@ class SplitGroupedPrecondition(GroupedPrecondition):
                 flags = [('t1', False, True, True), ('t2', True, True, True),
                          ('t3e', False, True, True), ('t3i', False, True, False),
                          ('t4', False, False, False)]
-                # longest tiles first: a tile's time is its K loop, and
-                # blocks start in table order, so the K = 4608 / 2304
-                # layers' tiles no longer form the launch's tail
-                order = {}
-                for name, *_ in flags:
-                    rows = sorted(t[name], key=lambda r: (-r[4][2], -r[4][0] * r[4][1]))
-                    ks = _ksplits([r[4] for r in rows], fa.device)
-                    parts = [self._part(r[5], name, k, r[4]) if k > 1 else None
-                             for r, k in zip(rows, ks)]
-                    if any(k > 1 and p is None for k, p in zip(ks, parts)):
-                        return False  # a workspace cannot be allocated in a capture
-                    order[name] = (rows, ks, parts)
                 slots = self._cache.reserve()
                 tables = []
                 stab, sblocks, shost = lib.build_split_table(
                     [s[0] for s in split], [s[1] for s in split], [s[2] for s in split], slots[0])
                 tables.append(('split', stab, len(split), sblocks, shost))
                 for (name, amc, bmc, osplit), slot in zip(flags, slots[1:]):
-                    rows, ks, parts = order[name]
+                    # longest tiles first: a tile's time is its K loop, and
+                    # blocks start in table order, so the K = 4608 / 2304
+                    # layers' tiles no longer form the launch's tail
+                    rows = sorted(t[name], key=lambda r: (-r[4][2], -r[4][0] * r[4][1]))
                     if not rows:
                         continue
                     meta: list[int] = []
                     for r in rows:
                         meta.extend(r[4])
                     sc = [r[3] for r in rows]
-                    tab, tiles, host, ncomb, cblocks = lib.build_gemm3s_table(
+                    tab, tiles, host = lib.build_gemm3s_table(
                         [r[0] for r in rows], [r[1] for r in rows], [r[2] for r in rows],
                         [s[0] for s in sc], [s[1] for s in sc], [s[2] for s in sc], meta,
                         [float(damping) if s[1] is not None else 0.0 for s in sc],
-                        amc, bmc, osplit, slot, ks, parts)
-                    tables.append((name, tab, len(rows), tiles, (amc, bmc, osplit), host,
-                                   (ncomb, cblocks)))
+                        amc, bmc, osplit, slot)
+                    tables.append((name, tab, len(rows), tiles, (amc, bmc, osplit), host))
                 self._cache.put(key_t, tables, slots)
             self._tables = tables
             self._key = key_t
@@ -836,11 +780,8 @@ class SplitGroupedPrecondition(GroupedPrecondition):
                 _, tab, n, blocks, _ = entry
                 lib.split_pad_multi(_used_here(tab), n, blocks)
             else:
-                _, tab, n, tiles, (amc, bmc, osplit), _, (ncomb, cblocks) = entry
+                _, tab, n, tiles, (amc, bmc, osplit), _ = entry
                 lib.gemm3s_grouped(_used_here(tab), n, tiles, amc, bmc, osplit)
-                if ncomb:
-                    # split-K layers: fixed-order sum of the parts + epilogue
-                    lib.gemm3s_combine(tab, n, ncomb, cblocks, osplit)
 
 
 def grouped_gemm_mode() -> str:
