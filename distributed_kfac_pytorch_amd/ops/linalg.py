@@ -240,6 +240,17 @@ def _launch_jobs(
                   and k[0] > JACOBI_MAX_N}
     ready = torch.cuda.Event()
     ready.record(main)
+    if os.environ.get('KFAC_REFRESH_SYNC', '1') == '1':
+        # The host is usually many steps ahead of the GPU (graph replays and
+        # eager steps enqueue faster than they run; ~28 ResNet-50 steps, bounded
+        # by the hardware queue's ring).  Lane work enqueued now would sit on
+        # the other hardware queues behind a barrier on `ready` for all those
+        # steps, and while it waits the queued steps ran 2.5x slower (13.3 ->
+        # 33 ms per plain step for the 28 steps before every refresh: 1605
+        # img/s over 300 steps vs 1979 with this wait, 1997 vs 1990 over 20;
+        # profiles/r6/refresh_sync/).  So the lanes are issued once the
+        # factors are ready on the GPU; the host has nothing better to do.
+        ready.synchronize()
     streams = _side_streams(dev)
     big = [(k, v) for k, v in gpu if k in chain_keys]
     rest = [(k, v) for k, v in gpu if k not in chain_keys]
