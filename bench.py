@@ -626,6 +626,18 @@ def main() -> None:
             'conv3x3_fwd_dgrad_stride1_wgrad_ge128ch': kxk if args.dtype == 'fp32' else args.dtype,
             'conv3x3_strided_dgrad_64ch_wgrad_stem': 'fp32 (MIOpen)'}
     line['host_issue_ms'] = res['host_issue_ms']
+    hi = res['host_issue_ms']
+    if not args.no_kfac and all(k in hi for k in ('plain', 'inverse')):
+        # host time to issue one inv_update_steps period at the same cadence
+        # as ms_per_step: below the GPU's period the run is not host-bound,
+        # whatever a single eager step's issue time (it hides behind the
+        # replays queued before it)
+        inv_p, f_p = args.kfac_inv_update_steps, args.kfac_factor_update_steps
+        n_factor = len([s_ for s_ in range(1, inv_p) if s_ % f_p == 0])
+        line['period_issue_ms'] = {
+            'host': round(hi['inverse'] + n_factor * hi.get('factor', hi['plain'])
+                          + (inv_p - 1 - n_factor) * hi['plain'], 1),
+            'gpu': round(ms * inv_p, 1)}
     if base is not None:
         line['sgd_host_issue_ms'] = base['host_issue_ms']
     for k in ('phase_ms_per_step', 'phase_counts', 'kfac_layers', 'step_graphs',
