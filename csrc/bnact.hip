@@ -116,10 +116,19 @@ __global__ void __launch_bounds__(BN_T) bn_partial_kernel(
   int64_t r1 = r0 + rows_per_block;
   if (r1 > M) r1 = M;
   float s0[8] = {}, s1[8] = {};
-  float mu[8] = {};
+  float mu[8] = {}, msc[8] = {}, msf[8] = {};
+  // y == nullptr: the ReLU mask from x (scale / shift follow the mean in
+  // the statistics, the forward's fma recomputed bit for bit)
+  const bool rec = MODE == 1 && relu && y == nullptr;
   if (MODE == 1 && rs < rpi) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) mu[i] = mean[c0 + i];
+    for (int i = 0; i < 8; ++i) {
+      mu[i] = mean[c0 + i];
+      if (rec) {
+        msc[i] = mean[2 * C + c0 + i];
+        msf[i] = mean[3 * C + c0 + i];
+      }
+    }
   }
   if (rs < rpi) {
     // U rows per iteration with independent loads: keeps enough 16-B loads
@@ -143,7 +152,7 @@ __global__ void __launch_bounds__(BN_T) bn_partial_kernel(
         ldraw8(x + offs[u], ra[u]);
         if (MODE == 1) ldraw8(dy + offs[u], rg[u]);
       }
-      if (MODE == 1 && relu) {
+      if (MODE == 1 && relu && !rec) {
 #pragma unroll
         for (int u = 0; u < U; ++u) ldraw8(y + offs[u], ro[u]);
       }
@@ -153,7 +162,7 @@ __global__ void __launch_bounds__(BN_T) bn_partial_kernel(
         cvt8(ra[u], a[u]);
         if (MODE == 1) {
           cvt8(rg[u], g[u]);
-          if (relu) cvt8(ro[u], o[u]);
+          if (relu && !rec) cvt8(ro[u], o[u]);
         }
       }
 #pragma unroll
@@ -168,7 +177,9 @@ __global__ void __launch_bounds__(BN_T) bn_partial_kernel(
         } else {
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
-            const float gi = (!relu || o[u][i] > 0.f) ? g[u][i] : 0.f;
+            const bool on = !relu || (rec ? __builtin_fmaf(a[u][i], msc[i], msf[i]) > 0.f
+                                                : o[u][i] > 0.f);
+            const float gi = on ? g[u][i] : 0.f;
             s0[i] += gi;
             s1[i] += gi * (a[u][i] - mu[i]);
           }
@@ -316,7 +327,7 @@ __global__ void __launch_bounds__(BN_T) bn_fwd_apply_kernel(
       if (row >= M) continue;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        float o = a[u][i] * sc[i] + sf[i];
+        float o = __builtin_fmaf(a[u][i], sc[i], sf[i]);
         if (res) o += r[u][i];
         a[u][i] = relu ? fmaxf(o, 0.f) : o;
       }
@@ -355,10 +366,13 @@ __global__ void __launch_bounds__(BN_T) bn_bwd_apply_kernel(
   const int cg = threadIdx.x % tpr, rs = threadIdx.x / tpr;
   if (rs >= rpi) return;
   const int c0 = cg * 8;
-  float mu[8], k1[8], k2[8], k3[8];
+  float mu[8], k1[8], k2[8], k3[8], msc[8], msf[8];
+  const bool rec = relu && y == nullptr;  // ReLU mask from x (bn_partial_kernel)
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     mu[i] = stats[c0 + i];
+    msc[i] = stats[2 * C + c0 + i];
+    msf[i] = stats[3 * C + c0 + i];
     k1[i] = coef[c0 + i];
     k2[i] = coef[C + c0 + i];
     k3[i] = coef[2 * C + c0 + i];
@@ -379,7 +393,7 @@ __global__ void __launch_bounds__(BN_T) bn_bwd_apply_kernel(
       ldraw8(x + offs[u], ra[u]);
       ldraw8(dy + offs[u], rg[u]);
     }
-    if (relu) {
+    if (relu && !rec) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) ldraw8(y + offs[u], ro[u]);
     }
@@ -388,14 +402,18 @@ __global__ void __launch_bounds__(BN_T) bn_bwd_apply_kernel(
       if (rb + (int64_t)u * rpi >= M) continue;
       cvt8(ra[u], a[u]);
       cvt8(rg[u], g[u]);
-      if (relu) cvt8(ro[u], o[u]);
+      if (relu && !rec) cvt8(ro[u], o[u]);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int64_t row = rb + (int64_t)u * rpi;
       if (row >= M) continue;
       const int64_t off = row * C + c0;
-      if (relu) {
+      if (rec) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          g[u][i] = __builtin_fmaf(a[u][i], msc[i], msf[i]) > 0.f ? g[u][i] : 0.f;
+      } else if (relu) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) g[u][i] = o[u][i] > 0.f ? g[u][i] : 0.f;
       }
@@ -431,10 +449,18 @@ __global__ void __launch_bounds__(BN_T) bn_partial_sliced_kernel(
   const int c0 = blockIdx.x * cw + tc * 8;
   const int64_t r0 = (int64_t)blockIdx.y * rows_per_chunk;
   const int64_t r1 = r0 + rows_per_chunk < M ? r0 + rows_per_chunk : M;
-  float s0[8] = {}, s1[8] = {}, mu[8] = {};
+  float s0[8] = {}, s1[8] = {}, mu[8] = {}, msc[8] = {}, msf[8] = {};
+  // y == nullptr: the ReLU mask from x (as bn_partial_kernel)
+  const bool rec = MODE == 1 && relu && y == nullptr;
   if (MODE == 1) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) mu[i] = mean[c0 + i];
+    for (int i = 0; i < 8; ++i) {
+      mu[i] = mean[c0 + i];
+      if (rec) {
+        msc[i] = mean[2 * C + c0 + i];
+        msf[i] = mean[3 * C + c0 + i];
+      }
+    }
   }
   constexpr int U = 4;
   for (int64_t rb = r0 + rt; rb < r1; rb += U * (int64_t)RT) {
@@ -455,7 +481,7 @@ __global__ void __launch_bounds__(BN_T) bn_partial_sliced_kernel(
       ldraw8(x + offs[u], ra[u]);
       if (MODE == 1) ldraw8(dy + offs[u], rg[u]);
     }
-    if (MODE == 1 && relu) {
+    if (MODE == 1 && relu && !rec) {
 #pragma unroll
       for (int u = 0; u < U; ++u) ldraw8(y + offs[u], ro[u]);
     }
@@ -465,7 +491,7 @@ __global__ void __launch_bounds__(BN_T) bn_partial_sliced_kernel(
       cvt8(ra[u], a[u]);
       if (MODE == 1) {
         cvt8(rg[u], g[u]);
-        if (relu) cvt8(ro[u], o[u]);
+        if (relu && !rec) cvt8(ro[u], o[u]);
       }
     }
 #pragma unroll
@@ -477,7 +503,9 @@ __global__ void __launch_bounds__(BN_T) bn_partial_sliced_kernel(
           s0[i] += a[u][i];
           s1[i] += a[u][i] * a[u][i];
         } else {
-          const float gi = (!relu || o[u][i] > 0.f) ? g[u][i] : 0.f;
+          const bool on = !relu || (rec ? __builtin_fmaf(a[u][i], msc[i], msf[i]) > 0.f
+                                                : o[u][i] > 0.f);
+            const float gi = on ? g[u][i] : 0.f;
           s0[i] += gi;
           s1[i] += gi * (a[u][i] - mu[i]);
         }
@@ -609,7 +637,7 @@ __global__ void __launch_bounds__(BN_T) bn_fwd_apply_sliced_kernel(
       if (row >= r1) continue;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        float o = a[u][i] * sc[i] + sf[i];
+        float o = __builtin_fmaf(a[u][i], sc[i], sf[i]);
         if (res) o += r[u][i];
         a[u][i] = relu ? fmaxf(o, 0.f) : o;
       }
@@ -651,10 +679,13 @@ __global__ void __launch_bounds__(BN_T) bn_bwd_apply_sliced_kernel(
   const int tpc = cw / 8, RT = BN_T / tpc;
   const int tc = threadIdx.x % tpc, rt = threadIdx.x / tpc;
   const int c0 = blockIdx.x * cw + tc * 8;
-  float mu[8], k1[8], k2[8], k3[8];
+  float mu[8], k1[8], k2[8], k3[8], msc[8], msf[8];
+  const bool rec = relu && y == nullptr;  // ReLU mask from x (bn_partial_kernel)
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     mu[i] = smu[tc * 8 + i];
+    msc[i] = stats[2 * C + c0 + i];
+    msf[i] = stats[3 * C + c0 + i];
     k1[i] = sk1[tc * 8 + i];
     k2[i] = sk2[tc * 8 + i];
     k3[i] = sk3[tc * 8 + i];
@@ -676,7 +707,7 @@ __global__ void __launch_bounds__(BN_T) bn_bwd_apply_sliced_kernel(
       ldraw8(x + offs[u], ra[u]);
       ldraw8(dy + offs[u], rg[u]);
     }
-    if (relu) {
+    if (relu && !rec) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) ldraw8(y + offs[u], ro[u]);
     }
@@ -685,14 +716,18 @@ __global__ void __launch_bounds__(BN_T) bn_bwd_apply_sliced_kernel(
       if (rb + (int64_t)u * RT >= r1) continue;
       cvt8(ra[u], a[u]);
       cvt8(rg[u], g[u]);
-      if (relu) cvt8(ro[u], o[u]);
+      if (relu && !rec) cvt8(ro[u], o[u]);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int64_t row = rb + (int64_t)u * RT;
       if (row >= r1) continue;
       const int64_t off = row * C + c0;
-      if (relu) {
+      if (rec) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          g[u][i] = __builtin_fmaf(a[u][i], msc[i], msf[i]) > 0.f ? g[u][i] : 0.f;
+      } else if (relu) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) g[u][i] = o[u][i] > 0.f ? g[u][i] : 0.f;
       }
@@ -805,6 +840,14 @@ template <typename E>
 void bn_backward_t(const E* x, const E* dy, const E* y, const float* weight, const float* stats,
                    int relu, int64_t M, int C, float* part, float* coef, float* dweight,
                    float* dbias, E* dx, E* dres, hipStream_t s) {
+  // Without a residual the ReLU mask y > 0 is x * scale + shift > 0, which
+  // the kernels recompute from the x they read anyway: two passes over y
+  // fewer per layer (KFAC_BN_MASK_FROM_Y=1 reads y as before)
+  static const bool from_y = [] {
+    const char* e = std::getenv("KFAC_BN_MASK_FROM_Y");
+    return e != nullptr && std::strcmp(e, "1") == 0;
+  }();
+  if (dres == nullptr && !from_y) y = nullptr;
   {
     int P, Q;
     int64_t rp, rq;
