@@ -89,7 +89,8 @@ int gemm3_wgrad_splits(int pixels, int Cout, int kcols);
 void gemm3_conv_wgrad(const float* x, const float* dy, float* dw, int N, int H, int W, int C,
                       int Cout, int kh, int kw, int stride, int pad, int splits, hipStream_t s);
 void gemm3_conv(const float* x, const float* w, float* y, int N, int H, int W, int C, int Cout,
-                int kh, int kw, int stride, int pad, int splits, bool flipw, hipStream_t s);
+                int kh, int kw, int stride, int pad, int splits, bool flipw, hipStream_t s,
+                float* bnpart = nullptr);
 void gemm3_grouped(const GemmDesc* table, int nlayers, int total_tiles,
                    bool a_kc, bool b_kc, hipStream_t s);
 // gemm3s.hip
@@ -110,7 +111,8 @@ int bn_max_c();
 void bn_forward(int dtype, const void* x, const void* res, const float* weight,
                 const float* bias, float* running_mean, float* running_var,
                 int64_t* num_batches, float momentum, float eps, int relu, int64_t M,
-                int C, float* part, float* stats, void* y, hipStream_t s);
+                int C, float* part, float* stats, void* y, hipStream_t s,
+                const float* ext_part = nullptr, int ext_p = 0);
 void bn_backward(int dtype, const void* x, const void* dy, const void* y, const float* weight,
                  const float* stats, int relu, int64_t M, int C, float* part, float* coef,
                  float* dweight, float* dbias, void* dx, void* dres, hipStream_t s);
@@ -1065,6 +1067,18 @@ int64_t gemm3_mm_splits_for(int64_t K, int64_t want) {
   return (kts + per - 1) / per;
 }
 
+// the BN statistics partials a single-pass gemm3 GEMM writes for an
+// [M, N] output (GemmDesc::bnpart): fp32 [2 * ceil(M / 128)][2][N]
+static float* bn_part_ptr(const c10::optional<at::Tensor>& p, int64_t M, int64_t N,
+                          const at::Device& dev) {
+  if (!p.has_value() || !p->defined()) return nullptr;
+  check_cuda(*p, "bnpart");
+  TORCH_CHECK(p->device() == dev && p->scalar_type() == at::kFloat && p->is_contiguous() &&
+                  p->numel() == 2 * ((M + 127) / 128) * 2 * N,
+              "bnpart: contiguous fp32 [2 * ceil(M / 128)][2][N]");
+  return p->data_ptr<float>();
+}
+
 // One fp32 GEMM C[M,N] = A . B on bf16x3 MFMA (csrc/gemm3.hip), the
 // descriptor passed by value (no table upload: capturable as a single
 // kernel node).  a_kc: A is [M, K], else the stored [K, M]; b_kc: B is the
@@ -1072,7 +1086,7 @@ int64_t gemm3_mm_splits_for(int64_t K, int64_t want) {
 // [splits, M, N] and receives one partial product per split (the caller
 // sums them; k-tiles are shared out equally, see gemm3_mm_splits).
 void gemm3_mm(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, bool a_kc,
-              bool b_kc, int64_t splits) {
+              bool b_kc, int64_t splits, const c10::optional<at::Tensor>& bnpart) {
   TORCH_CHECK(splits >= 1, "gemm3_mm: splits >= 1");
   if (splits > 1) {
     check_cuda(C, "gemm3_mm partials");
@@ -1109,6 +1123,8 @@ void gemm3_mm(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, boo
   d.Kmain = (int32_t)K;
   d.tiles_n = (int32_t)((N + 127) / 128);
   d.vec = (vec_ok(A) ? 1 : 0) | (vec_ok(B) ? 2 : 0);
+  d.bnpart = bn_part_ptr(bnpart, M, N, C.device());
+  TORCH_CHECK(d.bnpart == nullptr || splits == 1, "gemm3_mm: bnpart needs splits == 1");
   c10::hip::HIPGuardMasqueradingAsCUDA g(C.device());
   if (K == 0) {
     C.zero_();
@@ -1116,6 +1132,7 @@ void gemm3_mm(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, boo
   }
   kfac::gemm3_single(d, a_kc, b_kc, (int)splits, M * N, cur_stream());
 }
+
 
 // Implicit-GEMM convolution on bf16x3 MFMA (csrc/gemm3.hip): x [N, C, H, W]
 // and w [Cout, C, kh, kw] both channels_last fp32, C % 4 == 0 (% 32 with
@@ -1126,7 +1143,7 @@ void gemm3_mm(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, boo
 at::Tensor sum_splits(const at::Tensor& part, const c10::optional<at::Tensor>& out_opt);
 
 at::Tensor gemm3_conv(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad,
-                      bool flipw) {
+                      bool flipw, const c10::optional<at::Tensor>& bnpart) {
   check_cuda(x, "gemm3_conv x");
   check_cuda(w, "gemm3_conv w");
   TORCH_CHECK(x.scalar_type() == at::kFloat && w.scalar_type() == at::kFloat && x.dim() == 4 &&
@@ -1153,9 +1170,13 @@ at::Tensor gemm3_conv(const at::Tensor& x, const at::Tensor& w, int64_t stride, 
                                          (int)kw, (int)stride, (int)pad);
   // split-K partials summed in fixed order by one reduction (deterministic)
   at::Tensor part = sp > 1 ? at::empty({sp, N * Ho * Wo, Co}, x.options()) : y;
+  // BN statistics only from a single pass (the caller checks
+  // gemm3_conv_splits first); a split launch leaves bnpart unwritten
+  float* bnp = bn_part_ptr(bnpart, N * Ho * Wo, Co, x.device());
+  TORCH_CHECK(bnp == nullptr || (sp == 1 && !flipw), "gemm3_conv: bnpart needs a single pass");
   kfac::gemm3_conv(x.data_ptr<float>(), w.data_ptr<float>(), part.data_ptr<float>(), (int)N,
                    (int)H, (int)W, (int)C, (int)Co, (int)kh, (int)kw, (int)stride, (int)pad, sp,
-                   flipw, cur_stream());
+                   flipw, cur_stream(), bnp);
   if (sp > 1) sum_splits(part, y.permute({0, 2, 3, 1}).view({N * Ho * Wo, Co}));
   return y;
 }
@@ -1286,7 +1307,8 @@ std::vector<at::Tensor> bn_act_forward(const at::Tensor& x,
                                        const c10::optional<at::Tensor>& running_mean,
                                        const c10::optional<at::Tensor>& running_var,
                                        const c10::optional<at::Tensor>& num_batches,
-                                       double momentum, double eps, bool relu) {
+                                       double momentum, double eps, bool relu,
+                                       const c10::optional<at::Tensor>& ext_part) {
   TORCH_CHECK(bn_act_supported(x), "bn_act_forward: unsupported input");
   const int64_t C = x.size(1), M = x.numel() / C;
   const bool has_res = residual.has_value() && residual->defined();
@@ -1312,10 +1334,23 @@ std::vector<at::Tensor> bn_act_forward(const at::Tensor& x,
                   ? running_mean->data_ptr<float>() : nullptr;
   float* rv = running_var.has_value() && running_var->defined()
                   ? running_var->data_ptr<float>() : nullptr;
+  // ext_part: the statistics partials of the convolution that produced x
+  // ([P][2][C], GemmDesc::bnpart): no statistics pass over x
+  const float* ep = nullptr;
+  int ext_p = 0;
+  if (ext_part.has_value() && ext_part->defined()) {
+    check_cuda(*ext_part, "ext_part");
+    TORCH_CHECK(x.scalar_type() == at::kFloat && ext_part->scalar_type() == at::kFloat &&
+                    ext_part->is_contiguous() && ext_part->numel() % (2 * C) == 0 &&
+                    ext_part->numel() / (2 * C) == 2 * ((M + 127) / 128),
+                "bn_act_forward: ext_part must be the producer's fp32 [2 * ceil(M / 128)][2][C]");
+    ep = ext_part->data_ptr<float>();
+    ext_p = (int)(ext_part->numel() / (2 * C));
+  }
   kfac::bn_forward(dtype_tag(x), x.data_ptr(), has_res ? residual->data_ptr() : nullptr,
                    opt_f(weight), opt_f(bias), rm, rv, nb, (float)momentum, (float)eps,
                    relu ? 1 : 0, M, (int)C, part.data_ptr<float>(), stats.data_ptr<float>(),
-                   y.data_ptr(), cur_stream());
+                   y.data_ptr(), cur_stream(), ep, ext_p);
   return {y, stats};
 }
 
@@ -1361,10 +1396,11 @@ struct BNActFn : public torch::autograd::Function<BNActFn> {
                             const at::Tensor& weight, const at::Tensor& bias,
                             const at::Tensor& residual, at::Tensor running_mean,
                             at::Tensor running_var, at::Tensor num_batches,
-                            double momentum, double eps, bool relu, bool has_res) {
+                            double momentum, double eps, bool relu, bool has_res,
+                            const c10::optional<at::Tensor>& ext_part) {
     auto out = bn_act_forward(x, has_res ? c10::optional<at::Tensor>(residual) : c10::nullopt,
                               weight, bias, running_mean, running_var, num_batches,
-                              momentum, eps, relu);
+                              momentum, eps, relu, ext_part);
     ctx->save_for_backward({x, out[0], weight, out[1]});
     ctx->saved_data["relu"] = relu;
     ctx->saved_data["has_res"] = has_res;
@@ -1378,7 +1414,7 @@ struct BNActFn : public torch::autograd::Function<BNActFn> {
     auto r = bn_act_backward(saved[0], grads[0], saved[1], saved[2], saved[3], relu, has_res);
     at::Tensor undef;
     return {r[0], r[1], r[2], has_res ? r[3] : undef,
-            undef, undef, undef, undef, undef, undef, undef};
+            undef, undef, undef, undef, undef, undef, undef, undef};
   }
 };
 
@@ -1386,10 +1422,11 @@ struct BNActFn : public torch::autograd::Function<BNActFn> {
 at::Tensor bn_act(const at::Tensor& x, const at::Tensor& weight, const at::Tensor& bias,
                   const c10::optional<at::Tensor>& residual,
                   const at::Tensor& running_mean, const at::Tensor& running_var,
-                  const at::Tensor& num_batches, double momentum, double eps, bool relu) {
+                  const at::Tensor& num_batches, double momentum, double eps, bool relu,
+                  const c10::optional<at::Tensor>& ext_part) {
   const bool has_res = residual.has_value() && residual->defined();
   return BNActFn::apply(x, weight, bias, has_res ? *residual : x, running_mean, running_var,
-                        num_batches, momentum, eps, relu, has_res);
+                        num_batches, momentum, eps, relu, has_res, ext_part);
 }
 
 // tridiag_host.cpp
@@ -1482,9 +1519,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sytrd_nb", &sytrd_panel);
   m.def("sytrd_max_n", &sytrd_max_n);
   m.def("bn_act_supported", &bn_act_supported);
-  m.def("bn_act_forward", &bn_act_forward);
+  m.def("bn_act_forward", &bn_act_forward, py::arg("x"), py::arg("residual"), py::arg("weight"),
+        py::arg("bias"), py::arg("running_mean"), py::arg("running_var"),
+        py::arg("num_batches"), py::arg("momentum"), py::arg("eps"), py::arg("relu"),
+        py::arg("ext_part") = py::none());
   m.def("bn_act_backward", &bn_act_backward);
-  m.def("bn_act", &bn_act);
+  m.def("bn_act", &bn_act, py::arg("x"), py::arg("weight"), py::arg("bias"), py::arg("residual"),
+        py::arg("running_mean"), py::arg("running_var"), py::arg("num_batches"),
+        py::arg("momentum"), py::arg("eps"), py::arg("relu"), py::arg("ext_part") = py::none());
   m.def("spd_inverse_blocked", &spd_inverse_blocked, py::call_guard<py::gil_scoped_release>());
   m.def("sytrd_reduce", &sytrd_reduce, py::call_guard<py::gil_scoped_release>());
   m.def("sytrd_begin", &sytrd_begin, py::call_guard<py::gil_scoped_release>());
@@ -1507,9 +1549,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm3_conv_wgrad", &gemm3_conv_wgrad, py::arg("x"), py::arg("dy"), py::arg("kh"),
         py::arg("kw"), py::arg("stride"), py::arg("pad"));
   m.def("gemm3_conv", &gemm3_conv, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"),
-        py::arg("flipw") = false);
+        py::arg("flipw") = false, py::arg("bnpart") = py::none());
+  m.def("gemm3_conv_splits",
+        [](int64_t n, int64_t h, int64_t w, int64_t c, int64_t co, int64_t kh, int64_t kw,
+           int64_t stride, int64_t pad) {
+          return kfac::gemm3_conv_splits((int)n, (int)h, (int)w, (int)c, (int)co, (int)kh,
+                                         (int)kw, (int)stride, (int)pad);
+        });
   m.def("gemm3_mm", &gemm3_mm, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("a_kc"),
-        py::arg("b_kc"), py::arg("splits") = 1);
+        py::arg("b_kc"), py::arg("splits") = 1, py::arg("bnpart") = py::none());
   m.def("gemm3_mm_splits", &gemm3_mm_splits_for, py::arg("k"), py::arg("want"));
   m.def("gemm3s_align", &kfac::gemm3s_align);
   m.def("build_gemm3s_table", &build_gemm3s_table);

@@ -808,7 +808,27 @@ template <typename E>
 void bn_forward_t(const E* x, const E* res, const float* weight, const float* bias,
                   float* running_mean, float* running_var, int64_t* num_batches, float momentum,
                   float eps, int relu, int64_t M, int C, float* part, float* stats, E* y,
-                  hipStream_t s) {
+                  hipStream_t s, const float* ext_part, int ext_p) {
+  if (ext_part != nullptr) {
+    // statistics partials from the producing convolution's epilogue
+    // ([ext_p][2][C]): no pass over x before the apply
+    int P, Q;
+    int64_t rp, rq;
+    if (sliced_plan(M, C, &P, &Q, &rp, &rq) && ext_p <= 2 * SB_PMAX) {
+      // small activation: each apply block reduces its slice's partials
+      const unsigned nsl = (unsigned)(C / sliced_cw(C));
+      hipLaunchKernelGGL(bn_fwd_apply_sliced_kernel<E>, dim3(nsl, (unsigned)Q), dim3(BN_T), 0, s,
+                         x, res, ext_part, ext_p, M, C, rq, weight, bias, running_mean,
+                         running_var, num_batches, momentum, eps, relu, stats, y);
+      return;
+    }
+    hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((unsigned)ceil_div(C, BN_FIN_CH)),
+                       dim3(BN_FIN_T), 0, s, ext_part, ext_p, M, C, weight, bias, running_mean,
+                       running_var, num_batches, momentum, eps, stats);
+    hipLaunchKernelGGL(bn_fwd_apply_kernel<E>, dim3(apply_grid(M, C)), dim3(BN_T), 0, s, x, res,
+                       stats, relu, M, C, y);
+    return;
+  }
   {
     int P, Q;
     int64_t rp, rq;
@@ -881,14 +901,16 @@ void bn_backward_t(const E* x, const E* dy, const E* y, const float* weight, con
 void bn_forward(int dtype, const void* x, const void* res, const float* weight,
                 const float* bias, float* running_mean, float* running_var,
                 int64_t* num_batches, float momentum, float eps, int relu, int64_t M,
-                int C, float* part, float* stats, void* y, hipStream_t s) {
+                int C, float* part, float* stats, void* y, hipStream_t s,
+                const float* ext_part, int ext_p) {
   if (dtype == kF32)
     bn_forward_t((const float*)x, (const float*)res, weight, bias, running_mean, running_var,
-                 num_batches, momentum, eps, relu, M, C, part, stats, (float*)y, s);
+                 num_batches, momentum, eps, relu, M, C, part, stats, (float*)y, s, ext_part,
+                 ext_p);
   else
     bn_forward_t((const uint16_t*)x, (const uint16_t*)res, weight, bias, running_mean,
                  running_var, num_batches, momentum, eps, relu, M, C, part, stats,
-                 (uint16_t*)y, s);
+                 (uint16_t*)y, s, ext_part, ext_p);
 }
 
 void bn_backward(int dtype, const void* x, const void* dy, const void* y, const float* weight,

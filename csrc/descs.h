@@ -40,6 +40,12 @@ struct GemmDesc {
   // stores them to LDS without the per-tile split
   const uint16_t* Ah;
   const uint16_t* Bh;
+  // optional BatchNorm statistics of the output (single-pass GEMMs without
+  // an epilogue scaling): per 64-row half tile and column, the sum and the
+  // sum of squares of the stored values, [2 * tiles_m][2][N] fp32 -- the
+  // partials the fused BN's finalize reads (csrc/bnact.hip), so the BN that
+  // follows a native convolution skips its statistics pass
+  float* bnpart;
 };
 
 // gemm3s.hip: one GEMM of a grouped launch on split images.  A split image

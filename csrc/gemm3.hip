@@ -692,6 +692,32 @@ __device__ __forceinline__ void gemm3_tile(const GemmDesc& d, int t, const Patch
       }
     }
   }
+  if (d.bnpart != nullptr) {
+    // BN statistics of this wave's 64 rows: lanes l and l + 32 hold the
+    // two interleaved row sets of a column; rows past M are zero
+    typedef float __attribute__((address_space(1)))* gout_t;
+    const int prow = (m0 / GT) * 2 + wr;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + wc * 64 + j * 32 + (l & 31);
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int m = m0 + wr * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (l >> 5);
+          const float v = m < d.M ? acc[i][j][e] : 0.f;
+          s += v;
+          q += v * v;
+        }
+      s += __shfl_xor(s, 32);
+      q += __shfl_xor(q, 32);
+      if (l < 32 && n < d.N) {
+        ((gout_t)d.bnpart)[(int64_t)(prow * 2) * d.N + n] = s;
+        ((gout_t)d.bnpart)[(int64_t)(prow * 2 + 1) * d.N + n] = q;
+      }
+    }
+  }
 }
 
 template <bool A_KC, bool B_KC>
@@ -819,7 +845,8 @@ int gemm3_conv_splits(int N, int H, int W, int C, int Cout, int kh, int kw, int 
 // the kernel applied is its flipped transpose (the input gradient of x is
 // gemm3_conv(dy, w, flipw) with pad kh - 1 - pad)
 void gemm3_conv(const float* x, const float* w, float* y, int N, int H, int W, int C, int Cout,
-                int kh, int kw, int stride, int pad, int splits, bool flipw, hipStream_t s) {
+                int kh, int kw, int stride, int pad, int splits, bool flipw, hipStream_t s,
+                float* bnpart) {
   const int Ho = (H + 2 * pad - kh) / stride + 1;
   const int Wo = (W + 2 * pad - kw) / stride + 1;
   GemmDesc d{};
@@ -835,6 +862,7 @@ void gemm3_conv(const float* x, const float* w, float* y, int N, int H, int W, i
   d.Kmain = d.K;
   d.tiles_n = (Cout + GT - 1) / GT;
   d.vec = 3;
+  d.bnpart = splits == 1 ? bnpart : nullptr;  // partial sums are not outputs
   const PatchGeom g{H, W, C, Ho, Wo, kw, stride, pad, kh};
   const int tiles = ((d.M + GT - 1) / GT) * d.tiles_n;
   if (tiles <= 0) return;
@@ -889,7 +917,7 @@ void gemm3_conv_wgrad(const float* x, const float* dy, float* dw, int N, int H, 
   d.Kmain = d.K;
   d.tiles_n = (d.N + GT - 1) / GT;
   d.vec = 3;
-  const PatchGeom g{H, W, C, Ho, Wo, kw, stride, pad, kh};
+    const PatchGeom g{H, W, C, Ho, Wo, kw, stride, pad, kh};
   const int tiles = ((d.M + GT - 1) / GT) * d.tiles_n;
   const int kts = (d.K + GK - 1) / GK;
   const int per = (kts + splits - 1) / splits;

@@ -152,6 +152,20 @@ class ResNet(nn.Module):
                     nn.init.zeros_(m.bn3.weight)
                 elif isinstance(m, BasicBlock):
                     nn.init.zeros_(m.bn2.weight)
+        # every convolution whose output goes straight into a BN: a native
+        # convolution then also writes the BN's statistics partials
+        # (ops/conv.py take_bn_part), sparing the BN its pass over the output
+        pairs = [(self.conv1, self.bn1)]
+        for m in self.modules():
+            if isinstance(m, (Bottleneck, BasicBlock)):
+                pairs += [(m.conv1, m.bn1), (m.conv2, m.bn2)]
+                if isinstance(m, Bottleneck):
+                    pairs.append((m.conv3, m.bn3))
+                if isinstance(m.downsample, nn.Sequential) and len(m.downsample) == 2:
+                    pairs.append((m.downsample[0], m.downsample[1]))
+        for conv, bn in pairs:
+            if isinstance(bn, BatchNormAct2d):
+                conv._feeds_bn = True
 
     def _make_layer(
         self,

@@ -21,6 +21,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from distributed_kfac_pytorch_amd.ops._native import native
+from distributed_kfac_pytorch_amd.ops.conv import take_bn_part
 from distributed_kfac_pytorch_amd.utils.env import getenv
 
 __all__ = ['BatchNormAct2d', 'bn_act']
@@ -106,12 +107,16 @@ def bn_act(
     relu: bool = True,
 ) -> torch.Tensor:
     """``relu(bn(x) + residual)`` (ReLU / residual optional)."""
+    # statistics partials from the native convolution that produced x
+    # (ops/conv.py take_bn_part): the fused BN then skips its pass over x
+    part = take_bn_part(x)
     if _fusable(bn, x, residual):
         # C++ autograd node (csrc/bindings.cpp BNActFn): no Python in the
         # forward or backward of the layer
         return native().bn_act(
             x, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var,
             bn.num_batches_tracked, float(bn.momentum), float(bn.eps), relu,
+            part if x.dtype == torch.float32 else None,
         )
     y = bn(x)
     if residual is not None:

@@ -178,6 +178,37 @@ def _splitk_few_tiles() -> bool:
     return getenv('KFAC_CONV1X1_SPLITK', '0') == '1'
 
 
+def _bn_stats_on() -> bool:
+    return getenv('KFAC_BN_CONV_STATS', '1') == '1'
+
+
+# The BatchNorm statistics of a native convolution's output, written by the
+# GEMM epilogue (csrc/gemm3.hip GemmDesc::bnpart), handed to the fused BN
+# that consumes that output (ops/bnact.py bn_act): the convolution offers
+# (its output tensor, the partials), the BN takes them if it was given that
+# very tensor.  Only convolutions marked ``_feeds_bn`` (models/resnet.py)
+# compute them.
+_BN_SLOT: list = [None, None]
+
+
+def _bn_part_for(m: int, n: int, device: torch.device) -> torch.Tensor:
+    return torch.empty(2 * (-(-m // 128)) * 2 * n, device=device, dtype=torch.float32)
+
+
+def _offer_bn_part(y: torch.Tensor, part: torch.Tensor | None) -> None:
+    _BN_SLOT[0], _BN_SLOT[1] = (y, part) if part is not None else (None, None)
+
+
+def take_bn_part(x: torch.Tensor) -> torch.Tensor | None:
+    """The statistics partials of ``x`` if the native convolution that
+    produced it offered them (cleared either way)."""
+    y, part = _BN_SLOT
+    if y is None:
+        return None
+    _BN_SLOT[0] = _BN_SLOT[1] = None
+    return part if y is x else None
+
+
 def conv1x1_math() -> str:
     """``KFAC_CONV1X1_MATH``: bf16x3 (default) or fp32 -- how an fp32
     ``GemmConv1x1`` computes its forward and input-gradient GEMMs.
@@ -215,9 +246,12 @@ def _gemm3_pays(m: int, n: int, k: int) -> bool:
     return k < 1024 or tiles >= 128
 
 
-def _mm3(lib, a: torch.Tensor, b: torch.Tensor, n: int, b_kc: bool) -> torch.Tensor:  # type: ignore[no-untyped-def]
+def _mm3(lib, a: torch.Tensor, b: torch.Tensor, n: int, b_kc: bool,  # type: ignore[no-untyped-def]
+         bn: list | None = None) -> torch.Tensor:
     """C[m, n] = a . B on gemm3_mm; split-K (fixed-order partial sum) when a
-    long reduction leaves fewer than 128 tiles (``KFAC_CONV1X1_SPLITK=1``)."""
+    long reduction leaves fewer than 128 tiles (``KFAC_CONV1X1_SPLITK=1``).
+    ``bn``: a single pass also writes the output's BN statistics partials
+    into ``bn[0]``."""
     m, k = a.shape
     tiles = -(-m // 128) * -(-n // 128)
     sp = 1
@@ -225,20 +259,23 @@ def _mm3(lib, a: torch.Tensor, b: torch.Tensor, n: int, b_kc: bool) -> torch.Ten
         sp = int(lib.gemm3_mm_splits(k, max(1, min(-(-256 // tiles), (k // 32) // 8))))
     if sp == 1:
         y = torch.empty(m, n, device=a.device, dtype=a.dtype)
-        lib.gemm3_mm(a, b, y, True, b_kc)
+        part = _bn_part_for(m, n, a.device) if bn is not None else None
+        lib.gemm3_mm(a, b, y, True, b_kc, 1, part)
+        if bn is not None:
+            bn[0] = part
         return y
     part = torch.empty(sp, m, n, device=a.device, dtype=a.dtype)
     lib.gemm3_mm(a, b, part, True, b_kc, sp)
     return lib.sum_splits(part)
 
 
-def _mm_nt(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    """``x @ w.T`` for fp32 [m, k] x [n, k]."""
+def _mm_nt(x: torch.Tensor, w: torch.Tensor, bn: list | None = None) -> torch.Tensor:
+    """``x @ w.T`` for fp32 [m, k] x [n, k] (``bn``: as ``_mm3``)."""
     lib = _gemm3_lib(x, w)
     if lib is None or (not _splitk_few_tiles()
                        and not _gemm3_pays(x.shape[0], w.shape[0], x.shape[1])):
         return x @ w.t()
-    return _mm3(lib, x, w, w.shape[0], True)
+    return _mm3(lib, x, w, w.shape[0], True, bn)
 
 
 def _mm_nn(g: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
@@ -293,12 +330,12 @@ class _Conv1x1Gemm(torch.autograd.Function):
 
     @staticmethod
     def forward(  # type: ignore[override]
-        ctx, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None,
+        ctx, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None, bn: list | None = None,
     ) -> torch.Tensor:
         ctx.save_for_backward(x, w)
         ctx.has_bias = b is not None
         if _gemm3_lib(x, w) is not None and x.stride(1) == 1 and w.is_contiguous():
-            y = _mm_nt(x, w)
+            y = _mm_nt(x, w, bn if b is None else None)
             return y if b is None else y.add_(b)
         return F.linear(x, w, b)
 
@@ -330,7 +367,7 @@ class _Conv1x1Gemm(torch.autograd.Function):
             else:
                 gw = gy.t() @ x
         gb = gy.sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
-        return gx, gw, gb
+        return gx, gw, gb, None
 
 
 class GemmConv1x1(StridedConv1x1):
@@ -364,9 +401,13 @@ class GemmConv1x1(StridedConv1x1):
             dt = torch.get_autocast_dtype(dev)
             x2, w2 = x2.to(dt), w2.to(dt)
             bias = bias.to(dt) if bias is not None else None
+        bn = [None] if getattr(self, '_feeds_bn', False) and _bn_stats_on() else None
         with torch.autocast(dev, enabled=False):
-            y = _Conv1x1Gemm.apply(x2, w2, bias)
-        return y.view(n, h, w, -1).permute(0, 3, 1, 2)
+            y = _Conv1x1Gemm.apply(x2, w2, bias, bn)
+        out = y.view(n, h, w, -1).permute(0, 3, 1, 2)
+        if bn is not None:
+            _offer_bn_part(out, bn[0])
+        return out
 
 
 def use_gemm_conv1x1(model: nn.Module) -> int:
@@ -403,11 +444,23 @@ class _ConvImplicit(torch.autograd.Function):
     def forward(  # type: ignore[override]
         ctx, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None, stride: int, pad: int,
         lib,  # type: ignore[no-untyped-def]
+        bn: list | None = None,
     ) -> torch.Tensor:
         ctx.save_for_backward(x, w)
         ctx.conf = (stride, pad, b is not None, lib)
-        y = lib.gemm3_conv(_pad4(x), _pad4(w).contiguous(memory_format=torch.channels_last),
-                           stride, pad)
+        xp = _pad4(x)
+        part = None
+        if bn is not None and b is None:
+            n, c, h, wd = xp.shape
+            k = w.shape[2]
+            if int(lib.gemm3_conv_splits(n, h, wd, c, w.shape[0], k, w.shape[3], stride, pad)) == 1:
+                ho = (h + 2 * pad - k) // stride + 1
+                wo = (wd + 2 * pad - w.shape[3]) // stride + 1
+                part = _bn_part_for(n * ho * wo, w.shape[0], x.device)
+        y = lib.gemm3_conv(xp, _pad4(w).contiguous(memory_format=torch.channels_last),
+                           stride, pad, False, part)
+        if bn is not None:
+            bn[0] = part
         if b is not None:
             y.add_(b.view(1, -1, 1, 1))
         return y
@@ -449,7 +502,7 @@ class _ConvImplicit(torch.autograd.Function):
                 gw = r[1]
         if has_bias and ctx.needs_input_grad[2]:
             gb = gy.sum((0, 2, 3))
-        return gx, gw, gb, None, None, None
+        return gx, gw, gb, None, None, None, None
 
 
 def _pad4(t: torch.Tensor) -> torch.Tensor:
@@ -497,7 +550,11 @@ class ImplicitGemmConv2d(nn.Conv2d):
         if (lib is None or torch.is_autocast_enabled(input.device.type)
                 or not input.is_contiguous(memory_format=torch.channels_last)):
             return super()._conv_forward(input, weight, bias)
-        return _ConvImplicit.apply(input, weight, bias, self.stride[0], self.padding[0], lib)
+        bn = [None] if getattr(self, '_feeds_bn', False) and _bn_stats_on() else None
+        out = _ConvImplicit.apply(input, weight, bias, self.stride[0], self.padding[0], lib, bn)
+        if bn is not None:
+            _offer_bn_part(out, bn[0])
+        return out
 
 
 def use_implicit_gemm_conv(model: nn.Module) -> int:

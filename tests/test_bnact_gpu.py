@@ -122,3 +122,69 @@ def test_cpp_node_matches_python_function(cuda):
         outs.append((y, xa.grad, ra.grad, bn.weight.grad, bn.bias.grad, bn.running_var))
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize('kind', ['1x1', '3x3', '3x3s2'])
+@pytest.mark.parametrize('shape', [(4, 64, 14, 14), (8, 128, 28, 28), (2, 256, 7, 9),
+                                   (16, 64, 56, 56)])
+def test_conv_epilogue_bn_statistics(cuda, monkeypatch, kind, shape):
+    """A native fp32 convolution marked ``_feeds_bn`` writes the following
+    BN's statistics partials from its GEMM epilogue (csrc/gemm3.hip
+    bnpart); the fused BN then skips its statistics pass.  Output, running
+    statistics and every gradient match the BN's own statistics pass
+    (``KFAC_BN_CONV_STATS=0``) to fp32 summation-order noise, and the
+    partials were actually taken."""
+    from distributed_kfac_pytorch_amd.ops import conv as cops
+
+    n, c, h, w = shape
+    torch.manual_seed(7)
+    if kind == '1x1':
+        base = torch.nn.Conv2d(c, 96, 1, bias=False)
+    else:
+        base = torch.nn.Conv2d(c, 96, 3, stride=2 if kind == '3x3s2' else 1, padding=1,
+                               bias=False)
+    x = _cl(torch.randn(shape, device=cuda))
+    runs = {}
+    gys: list = []
+    for stats in ('1', '0'):
+        monkeypatch.setenv('KFAC_BN_CONV_STATS', stats)
+        conv = _cl_module(base, cuda)
+        if kind == '1x1':
+            cops.use_gemm_conv1x1(conv)
+        else:
+            cops.use_implicit_gemm_conv(conv)
+        conv[0]._feeds_bn = True
+        bn = bnact.BatchNormAct2d(96).to(cuda)
+        taken = []
+        orig = cops.take_bn_part
+
+        def spy(t):  # type: ignore[no-untyped-def]
+            p = orig(t)
+            taken.append(p is not None)
+            return p
+        monkeypatch.setattr(bnact, 'take_bn_part', spy)
+        xa = x.clone().requires_grad_(True)
+        y = bn.act(conv(xa))
+        if not gys:
+            gys.append(_cl(torch.randn_like(y)))
+        y.backward(gys[0])
+        runs[stats] = (y.detach(), xa.grad, conv[0].weight.grad, bn.weight.grad, bn.bias.grad,
+                       bn.running_mean, bn.running_var, taken)
+    # a split-K convolution (small images) sums partial outputs afterwards:
+    # no epilogue statistics there, the BN takes its own pass
+    from distributed_kfac_pytorch_amd.ops._native import native
+
+    single = kind == '1x1' or int(native().gemm3_conv_splits(
+        n, h, w, c, 96, 3, 3, 2 if kind == '3x3s2' else 1, 1)) == 1
+    assert runs['1'][-1] == [single] and runs['0'][-1] == [False]
+    names = ('y', 'dx', 'dw', 'dgamma', 'dbeta', 'running_mean', 'running_var')
+    for name, a, b in zip(names, runs['1'][:-1], runs['0'][:-1]):
+        scale = b.abs().max().item() + 1e-12
+        assert (a - b).abs().max().item() <= 1e-4 * scale, (name, (a - b).abs().max().item(), scale)
+
+
+def _cl_module(base: torch.nn.Conv2d, cuda: torch.device) -> torch.nn.Sequential:
+    import copy
+
+    return torch.nn.Sequential(copy.deepcopy(base)).to(cuda).to(
+        memory_format=torch.channels_last)
