@@ -1086,7 +1086,8 @@ static float* bn_part_ptr(const c10::optional<at::Tensor>& p, int64_t M, int64_t
 // [splits, M, N] and receives one partial product per split (the caller
 // sums them; k-tiles are shared out equally, see gemm3_mm_splits).
 void gemm3_mm(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, bool a_kc,
-              bool b_kc, int64_t splits, const c10::optional<at::Tensor>& bnpart) {
+              bool b_kc, int64_t splits, const c10::optional<at::Tensor>& bnpart,
+              const c10::optional<at::Tensor>& addend) {
   TORCH_CHECK(splits >= 1, "gemm3_mm: splits >= 1");
   if (splits > 1) {
     check_cuda(C, "gemm3_mm partials");
@@ -1125,9 +1126,22 @@ void gemm3_mm(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, boo
   d.vec = (vec_ok(A) ? 1 : 0) | (vec_ok(B) ? 2 : 0);
   d.bnpart = bn_part_ptr(bnpart, M, N, C.device());
   TORCH_CHECK(d.bnpart == nullptr || splits == 1, "gemm3_mm: bnpart needs splits == 1");
+  if (addend.has_value() && addend->defined()) {
+    // C = A . B + addend (addend may be C itself)
+    check_cuda(*addend, "gemm3_mm addend");
+    TORCH_CHECK(splits == 1 && addend->scalar_type() == at::kFloat && addend->dim() == 2 &&
+                    addend->size(0) == M && addend->size(1) == N && addend->stride(1) == 1 &&
+                    addend->stride(0) == C2.stride(0) && addend->device() == C.device(),
+                "gemm3_mm: addend must be an fp32 [M, N] with C's strides (splits == 1)");
+    d.D = addend->data_ptr<float>();
+  }
   c10::hip::HIPGuardMasqueradingAsCUDA g(C.device());
   if (K == 0) {
-    C.zero_();
+    if (d.D != nullptr) {
+      if (addend->data_ptr() != C.data_ptr()) C.copy_(*addend);
+    } else {
+      C.zero_();
+    }
     return;
   }
   kfac::gemm3_single(d, a_kc, b_kc, (int)splits, M * N, cur_stream());
@@ -1557,7 +1571,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                                          (int)kw, (int)stride, (int)pad);
         });
   m.def("gemm3_mm", &gemm3_mm, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("a_kc"),
-        py::arg("b_kc"), py::arg("splits") = 1, py::arg("bnpart") = py::none());
+        py::arg("b_kc"), py::arg("splits") = 1, py::arg("bnpart") = py::none(),
+        py::arg("addend") = py::none());
   m.def("gemm3_mm_splits", &gemm3_mm_splits_for, py::arg("k"), py::arg("want"));
   m.def("gemm3s_align", &kfac::gemm3s_align);
   m.def("build_gemm3s_table", &build_gemm3s_table);

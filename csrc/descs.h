@@ -46,6 +46,9 @@ struct GemmDesc {
   // partials the fused BN's finalize reads (csrc/bnact.hip), so the BN that
   // follows a native convolution skips its statistics pass
   float* bnpart;
+  // optional addend [M][ldc] added to the stored values (may alias C: an
+  // accumulation of the GEMM into an existing gradient)
+  const float* D;
 };
 
 // gemm3s.hip: one GEMM of a grouped launch on split images.  A split image

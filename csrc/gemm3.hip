@@ -681,11 +681,22 @@ __device__ __forceinline__ void gemm3_tile(const GemmDesc& d, int t, const Patch
       const int n = n0 + wc * 64 + j * 32 + (l & 31);
       if (n >= d.N) continue;
       const float dan = d.da != nullptr ? gload(d.da + n) : 0.f;
+      // the addend's 16 values loaded together at clamped rows (one memory
+      // round trip, not one per element)
+      float dv[16];
+      if (d.D != nullptr) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int m = m0 + wr * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (l >> 5);
+          dv[e] = gload(d.D + (int64_t)(m < d.M ? m : d.M - 1) * d.ldc + n);
+        }
+      }
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int m = m0 + wr * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (l >> 5);
         if (m >= d.M) continue;
         float v = acc[i][j][e];
+        if (d.D != nullptr) v += dv[e];
         if (d.S != nullptr) v *= gload(d.S + (int64_t)m * d.lds + n);
         else if (d.dg != nullptr) v = v / (gload(d.dg + m) * dan + d.damping);
         *(float __attribute__((address_space(1)))*)(d.C + (int64_t)m * d.ldc + n) = v;

@@ -20,7 +20,10 @@ import torch
 import torch.nn as nn
 
 from distributed_kfac_pytorch_amd.ops.bnact import BatchNormAct2d
+from distributed_kfac_pytorch_amd.ops.conv import ResidualGradSlot
 from distributed_kfac_pytorch_amd.ops.conv import StridedConv1x1
+from distributed_kfac_pytorch_amd.ops.conv import _fuse_residual_grad
+from distributed_kfac_pytorch_amd.ops.conv import residual_tap
 
 __all__ = [
     'Bottleneck',
@@ -107,6 +110,18 @@ class Bottleneck(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         # BN (+ residual) + ReLU are one fused native op in bf16 training
         # (ops/bnact.py); elsewhere the same math through PyTorch
+        if self.downsample is None and x.requires_grad and _fuse_residual_grad():
+            # identity shortcut: its gradient is added by conv1's input-
+            # gradient GEMM (ops/conv.py ResidualGradSlot) when conv1 takes
+            # the slot; the tap is made after conv3 so its backward runs first
+            slot = ResidualGradSlot()
+            self.conv1._dgrad_slot = slot
+            try:
+                y = self.bn1.act(self.conv1(x))
+            finally:
+                self.conv1.__dict__.pop('_dgrad_slot', None)
+            y = self.conv3(self.bn2.act(self.conv2(y)))
+            return self.bn3.act(y, residual=residual_tap(x, slot) if slot.armed else x)
         idt = _shortcut(self.downsample, x)
         y = self.bn1.act(self.conv1(x))
         y = self.bn2.act(self.conv2(y))

@@ -209,6 +209,51 @@ def take_bn_part(x: torch.Tensor) -> torch.Tensor | None:
     return part if y is x else None
 
 
+def _fuse_residual_grad() -> bool:
+    return getenv('KFAC_RESIDUAL_GRAD_FUSE', '1') == '1'
+
+
+class ResidualGradSlot:
+    """Hand-off of an identity shortcut's gradient to the block's first
+    1x1 convolution, whose input-gradient GEMM then adds it in its epilogue
+    (csrc/gemm3.hip ``GemmDesc::D``) instead of autograd summing the two
+    gradients of the block input with a separate add.
+
+    ``_ResidualTap`` (the shortcut) runs its backward before the
+    convolution's in the normal order (it is created after the block's last
+    convolution, so the engine reaches it first) and parks its gradient
+    here; if the convolution's backward ran first anyway, it marks ``done``
+    and the tap returns its gradient to autograd as usual -- correct in
+    either order."""
+
+    __slots__ = ('g', 'done', 'armed')
+
+    def __init__(self) -> None:
+        self.g: torch.Tensor | None = None
+        self.done = False
+        self.armed = False
+
+
+class _ResidualTap(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x: torch.Tensor, slot: ResidualGradSlot) -> torch.Tensor:  # type: ignore[override]
+        ctx.slot = slot
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g: torch.Tensor) -> tuple:  # type: ignore[override]
+        slot = ctx.slot
+        if slot.done or g is None:
+            return g, None
+        slot.g = g
+        return None, None
+
+
+def residual_tap(x: torch.Tensor, slot: ResidualGradSlot) -> torch.Tensor:
+    """The identity shortcut ``x`` whose gradient goes to ``slot``."""
+    return _ResidualTap.apply(x, slot)
+
+
 def conv1x1_math() -> str:
     """``KFAC_CONV1X1_MATH``: bf16x3 (default) or fp32 -- how an fp32
     ``GemmConv1x1`` computes its forward and input-gradient GEMMs.
@@ -247,17 +292,20 @@ def _gemm3_pays(m: int, n: int, k: int) -> bool:
 
 
 def _mm3(lib, a: torch.Tensor, b: torch.Tensor, n: int, b_kc: bool,  # type: ignore[no-untyped-def]
-         bn: list | None = None) -> torch.Tensor:
+         bn: list | None = None, addend: torch.Tensor | None = None) -> torch.Tensor:
     """C[m, n] = a . B on gemm3_mm; split-K (fixed-order partial sum) when a
     long reduction leaves fewer than 128 tiles (``KFAC_CONV1X1_SPLITK=1``).
     ``bn``: a single pass also writes the output's BN statistics partials
-    into ``bn[0]``."""
+    into ``bn[0]``.  ``addend``: C = a . B + addend, written into ``addend``."""
     m, k = a.shape
     tiles = -(-m // 128) * -(-n // 128)
     sp = 1
     if _splitk_few_tiles() and tiles < 128 and k >= 1024:
         sp = int(lib.gemm3_mm_splits(k, max(1, min(-(-256 // tiles), (k // 32) // 8))))
     if sp == 1:
+        if addend is not None:
+            lib.gemm3_mm(a, b, addend, True, b_kc, 1, None, addend)
+            return addend
         y = torch.empty(m, n, device=a.device, dtype=a.dtype)
         part = _bn_part_for(m, n, a.device) if bn is not None else None
         lib.gemm3_mm(a, b, y, True, b_kc, 1, part)
@@ -266,7 +314,8 @@ def _mm3(lib, a: torch.Tensor, b: torch.Tensor, n: int, b_kc: bool,  # type: ign
         return y
     part = torch.empty(sp, m, n, device=a.device, dtype=a.dtype)
     lib.gemm3_mm(a, b, part, True, b_kc, sp)
-    return lib.sum_splits(part)
+    y = lib.sum_splits(part)
+    return y if addend is None else y.add_(addend)
 
 
 def _mm_nt(x: torch.Tensor, w: torch.Tensor, bn: list | None = None) -> torch.Tensor:
@@ -278,13 +327,13 @@ def _mm_nt(x: torch.Tensor, w: torch.Tensor, bn: list | None = None) -> torch.Te
     return _mm3(lib, x, w, w.shape[0], True, bn)
 
 
-def _mm_nn(g: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    """``g @ w`` for fp32 [m, k] x [k, n]."""
+def _mm_nn(g: torch.Tensor, w: torch.Tensor, addend: torch.Tensor | None = None) -> torch.Tensor:
+    """``g @ w (+ addend)`` for fp32 [m, k] x [k, n]."""
     lib = _gemm3_lib(g, w)
     if lib is None or (not _splitk_few_tiles()
                        and not _gemm3_pays(g.shape[0], w.shape[1], g.shape[1])):
-        return g @ w
-    return _mm3(lib, g, w, w.shape[1], False)
+        return g @ w if addend is None else torch.addmm(addend, g, w)
+    return _mm3(lib, g, w, w.shape[1], False, addend=addend)
 
 
 def _splitk(m: int, rows: int | None = None) -> int:
@@ -331,9 +380,11 @@ class _Conv1x1Gemm(torch.autograd.Function):
     @staticmethod
     def forward(  # type: ignore[override]
         ctx, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None, bn: list | None = None,
+        slot: ResidualGradSlot | None = None,
     ) -> torch.Tensor:
         ctx.save_for_backward(x, w)
         ctx.has_bias = b is not None
+        ctx.slot = slot
         if _gemm3_lib(x, w) is not None and x.stride(1) == 1 and w.is_contiguous():
             y = _mm_nt(x, w, bn if b is None else None)
             return y if b is None else y.add_(b)
@@ -343,7 +394,19 @@ class _Conv1x1Gemm(torch.autograd.Function):
     def backward(ctx, gy: torch.Tensor) -> tuple:  # type: ignore[override]
         x, w = ctx.saved_tensors
         gy = gy.contiguous()
-        gx = _mm_nn(gy, w.contiguous()) if ctx.needs_input_grad[0] else None
+        gx = None
+        if ctx.needs_input_grad[0]:
+            add = None
+            slot = ctx.slot
+            if slot is not None:
+                # the identity shortcut's gradient (ResidualGradSlot), parked
+                # by its tap: added in the GEMM epilogue, in place
+                add, slot.g, slot.done = slot.g, None, True
+                if add is not None:
+                    add = add.permute(0, 2, 3, 1).reshape(x.shape)
+                    if add.stride(1) != 1 or add.stride(0) != add.shape[1] or add.dtype != x.dtype:
+                        add = add.contiguous().to(x.dtype)
+            gx = _mm_nn(gy, w.contiguous(), add)
         gw = None
         lib = _gemm3_lib(gy, x) if ctx.needs_input_grad[1] else None
         # native split-K from 256 x 128 weights up (51 vs 61 us there, 44 vs
@@ -367,7 +430,7 @@ class _Conv1x1Gemm(torch.autograd.Function):
             else:
                 gw = gy.t() @ x
         gb = gy.sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
-        return gx, gw, gb, None
+        return gx, gw, gb, None, None
 
 
 class GemmConv1x1(StridedConv1x1):
@@ -402,8 +465,13 @@ class GemmConv1x1(StridedConv1x1):
             x2, w2 = x2.to(dt), w2.to(dt)
             bias = bias.to(dt) if bias is not None else None
         bn = [None] if getattr(self, '_feeds_bn', False) and _bn_stats_on() else None
+        slot = self.__dict__.pop('_dgrad_slot', None)
+        if slot is not None and ((sh, sw) != (1, 1) or torch.is_autocast_enabled(dev)):
+            slot = None  # the shortcut's gradient is summed by autograd
+        if slot is not None:
+            slot.armed = True
         with torch.autocast(dev, enabled=False):
-            y = _Conv1x1Gemm.apply(x2, w2, bias, bn)
+            y = _Conv1x1Gemm.apply(x2, w2, bias, bn, slot)
         out = y.view(n, h, w, -1).permute(0, 3, 1, 2)
         if bn is not None:
             _offer_bn_part(out, bn[0])
