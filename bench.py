@@ -631,7 +631,9 @@ def main() -> None:
         # host time to issue one inv_update_steps period at the same cadence
         # as ms_per_step: below the GPU's period the run is not host-bound,
         # whatever a single eager step's issue time (it hides behind the
-        # replays queued before it)
+        # replays queued before it).  Meaningful for short windows: in a
+        # long one the host fills the hardware queue and every issue time
+        # includes the wait for a free slot
         inv_p, f_p = args.kfac_inv_update_steps, args.kfac_factor_update_steps
         n_factor = len([s_ for s_ in range(1, inv_p) if s_ % f_p == 0])
         line['period_issue_ms'] = {
