@@ -84,6 +84,8 @@ void subsample_fwd(const float* x, float* y, int N, int H, int W, int C, int sh,
 void sum_splits(const float* part, float* out, int S, int64_t T, hipStream_t s);
 void subsample_bwd(const float* g, float* gx, int N, int H, int W, int C, int sh, int sw,
                    hipStream_t s);
+void subsample_bwd_acc(const float* g, float* gx, int N, int H, int W, int C, int sh, int sw,
+                   hipStream_t s);
 int gemm3_conv_splits(int N, int H, int W, int C, int Cout, int kh, int kw, int stride, int pad);
 int gemm3_wgrad_splits(int pixels, int Cout, int kcols);
 void gemm3_conv_wgrad(const float* x, const float* dy, float* dw, int N, int H, int W, int C,
@@ -1281,6 +1283,19 @@ at::Tensor subsample_bwd(const at::Tensor& gy, int64_t H, int64_t W, int64_t sh,
   return gx;
 }
 
+// gx += adjoint(gy), in place: gx is the other branch's full-size gradient
+void subsample_bwd_acc(const at::Tensor& gy, const at::Tensor& gx, int64_t sh, int64_t sw) {
+  check_nhwc4(gy, "subsample gradient");
+  check_nhwc4(gx, "subsample accumulation target");
+  const int64_t N = gy.size(0), C = gy.size(1), H = gx.size(2), W = gx.size(3);
+  TORCH_CHECK(gx.size(0) == N && gx.size(1) == C && gy.size(2) == (H + sh - 1) / sh &&
+                  gy.size(3) == (W + sw - 1) / sw && gx.device() == gy.device(),
+              "subsample_bwd_acc: shapes");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(gy.device());
+  kfac::subsample_bwd_acc(gy.data_ptr<float>(), gx.data_ptr<float>(), (int)N, (int)H, (int)W,
+                          (int)C, (int)sh, (int)sw, cur_stream());
+}
+
 void gemm3_grouped(const at::Tensor& table, int64_t nlayers, int64_t total_tiles,
                    bool a_kc, bool b_kc) {
   check_cuda(table, "table");
@@ -1558,6 +1573,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm3_grouped", &gemm3_grouped);
   m.def("subsample_fwd", &subsample_fwd, py::arg("x"), py::arg("sh"), py::arg("sw"));
   m.def("sum_splits", &sum_splits, py::arg("part"), py::arg("out") = py::none());
+  m.def("subsample_bwd_acc", &subsample_bwd_acc, py::arg("gy"), py::arg("gx"), py::arg("sh"),
+        py::arg("sw"));
   m.def("subsample_bwd", &subsample_bwd, py::arg("gy"), py::arg("h"), py::arg("w"),
         py::arg("sh"), py::arg("sw"));
   m.def("gemm3_conv_wgrad", &gemm3_conv_wgrad, py::arg("x"), py::arg("dy"), py::arg("kh"),

@@ -50,6 +50,26 @@ __global__ void __launch_bounds__(256) subsample_bwd_kernel(
   }
 }
 
+// gx[n][ho * sh][wo * sw][c] += g[n][ho][wo][c]: the adjoint accumulated
+// into an existing full-size gradient (the other branch's), touching only
+// the kept pixels
+__global__ void __launch_bounds__(256) subsample_bwd_acc_kernel(
+    const float4* __restrict__ g, float4* __restrict__ gx, int64_t total4, int C4, int H, int W,
+    int Ho, int Wo, int sh, int sw) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total4;
+       i += (int64_t)gridDim.x * 256) {
+    const int64_t pix = i / C4;
+    const int c = (int)(i - pix * C4);
+    const int wo = (int)(pix % Wo);
+    const int64_t q = pix / Wo;
+    const int ho = (int)(q % Ho);
+    const int64_t n = q / Ho;
+    const int64_t dst = ((n * H + (int64_t)ho * sh) * W + (int64_t)wo * sw) * C4 + c;
+    const float4 a = g[i], b = gx[dst];
+    gx[dst] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+  }
+}
+
 int grid_for(int64_t total4) {
   const int64_t b = ceil_div(total4, 256);
   return (int)(b < 8192 ? (b > 0 ? b : 1) : 8192);
@@ -72,6 +92,15 @@ void subsample_bwd(const float* g, float* gx, int N, int H, int W, int C, int sh
   const int64_t total4 = (int64_t)N * H * W * (C / 4);
   if (total4 == 0) return;
   subsample_bwd_kernel<<<grid_for(total4), 256, 0, s>>>(
+      (const float4*)g, (float4*)gx, total4, C / 4, H, W, Ho, Wo, sh, sw);
+}
+
+void subsample_bwd_acc(const float* g, float* gx, int N, int H, int W, int C, int sh, int sw,
+                       hipStream_t s) {
+  const int Ho = (H + sh - 1) / sh, Wo = (W + sw - 1) / sw;
+  const int64_t total4 = (int64_t)N * Ho * Wo * (C / 4);
+  if (total4 == 0) return;
+  subsample_bwd_acc_kernel<<<grid_for(total4), 256, 0, s>>>(
       (const float4*)g, (float4*)gx, total4, C / 4, H, W, Ho, Wo, sh, sw);
 }
 

@@ -122,8 +122,28 @@ class Bottleneck(nn.Module):
                 self.conv1.__dict__.pop('_dgrad_slot', None)
             y = self.conv3(self.bn2.act(self.conv2(y)))
             return self.bn3.act(y, residual=residual_tap(x, slot) if slot.armed else x)
-        idt = _shortcut(self.downsample, x)
-        y = self.bn1.act(self.conv1(x))
+        if (self.downsample is not None and x.requires_grad and _fuse_residual_grad()
+                and isinstance(self.downsample, nn.Sequential) and len(self.downsample) == 2):
+            # projection shortcut: conv1's input gradient is parked and the
+            # shortcut's backward (which runs after conv1's) accumulates into
+            # it -- at the kept pixels for a strided projection, in the GEMM
+            # epilogue for a stride-1 one -- instead of autograd's add
+            slot = ResidualGradSlot()
+            ds = self.downsample[0]
+            ds._dgrad_slot = slot
+            try:
+                idt = _shortcut(self.downsample, x)
+            finally:
+                ds.__dict__.pop('_dgrad_slot', None)
+            if slot.armed:
+                self.conv1._dgrad_park = slot
+            try:
+                y = self.bn1.act(self.conv1(x))
+            finally:
+                self.conv1.__dict__.pop('_dgrad_park', None)
+        else:
+            idt = _shortcut(self.downsample, x)
+            y = self.bn1.act(self.conv1(x))
         y = self.bn2.act(self.conv2(y))
         return self.bn3.act(self.conv3(y), residual=idt)
 

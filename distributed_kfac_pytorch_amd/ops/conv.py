@@ -72,9 +72,11 @@ class _Subsample(torch.autograd.Function):
     shortcuts (profiles/r5/prof_fp32_r6o/)."""
 
     @staticmethod
-    def forward(ctx, x: torch.Tensor, sh: int, sw: int) -> torch.Tensor:  # type: ignore[override]
+    def forward(ctx, x: torch.Tensor, sh: int, sw: int,  # type: ignore[override]
+                slot: ResidualGradSlot | None = None) -> torch.Tensor:
         lib = _subsample_lib(x)
         ctx.conf = (x.shape, sh, sw, lib)
+        ctx.slot = slot
         if lib is not None:  # csrc/subsample.hip: one 16-byte gather pass
             return lib.subsample_fwd(x, sh, sw)
         return x[:, :, ::sh, ::sw].contiguous(memory_format=torch.channels_last)
@@ -83,13 +85,26 @@ class _Subsample(torch.autograd.Function):
     def backward(ctx, g: torch.Tensor) -> tuple:  # type: ignore[override]
         shape, sh, sw, lib = ctx.conf
         g = g.contiguous(memory_format=torch.channels_last)
+        slot = ctx.slot
+        if slot is not None:
+            base, slot.g, slot.done = slot.g, None, True
+            if base is not None:
+                # the block's other branch (conv1's input gradient, parked by
+                # its backward): accumulate into it at the kept pixels only
+                n, c, h, w = shape
+                base = base.reshape(n, h, w, c).permute(0, 3, 1, 2)
+                if lib is not None and base.is_contiguous(memory_format=torch.channels_last):
+                    lib.subsample_bwd_acc(g, base, sh, sw)
+                else:
+                    base[:, :, ::sh, ::sw] += g
+                return base, None, None, None
         if lib is not None:
             # one pass writing every element (a zero fill + strided copy ran
             # at 0.4 TB/s: 118 us at ResNet-50's layer2 input)
-            return lib.subsample_bwd(g, shape[2], shape[3], sh, sw), None, None
+            return lib.subsample_bwd(g, shape[2], shape[3], sh, sw), None, None, None
         gx = g.new_zeros(shape).contiguous(memory_format=torch.channels_last)
         gx[:, :, ::sh, ::sw] = g
-        return gx, None, None
+        return gx, None, None, None
 
 
 def _subsample_lib(x: torch.Tensor):  # type: ignore[no-untyped-def]
@@ -100,9 +115,12 @@ def _subsample_lib(x: torch.Tensor):  # type: ignore[no-untyped-def]
     return _nat.native()
 
 
-def _subsample(x: torch.Tensor, sh: int, sw: int) -> torch.Tensor:
+def _subsample(x: torch.Tensor, sh: int, sw: int,
+               slot: ResidualGradSlot | None = None) -> torch.Tensor:
     if x.is_contiguous(memory_format=torch.channels_last):
-        return _Subsample.apply(x, sh, sw)
+        if slot is not None:
+            slot.armed = True
+        return _Subsample.apply(x, sh, sw, slot)
     return x[:, :, ::sh, ::sw]
 
 
@@ -380,11 +398,12 @@ class _Conv1x1Gemm(torch.autograd.Function):
     @staticmethod
     def forward(  # type: ignore[override]
         ctx, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None, bn: list | None = None,
-        slot: ResidualGradSlot | None = None,
+        slot: ResidualGradSlot | None = None, park: ResidualGradSlot | None = None,
     ) -> torch.Tensor:
         ctx.save_for_backward(x, w)
         ctx.has_bias = b is not None
         ctx.slot = slot
+        ctx.park = park
         if _gemm3_lib(x, w) is not None and x.stride(1) == 1 and w.is_contiguous():
             y = _mm_nt(x, w, bn if b is None else None)
             return y if b is None else y.add_(b)
@@ -403,10 +422,17 @@ class _Conv1x1Gemm(torch.autograd.Function):
                 # by its tap: added in the GEMM epilogue, in place
                 add, slot.g, slot.done = slot.g, None, True
                 if add is not None:
-                    add = add.permute(0, 2, 3, 1).reshape(x.shape)
+                    if add.dim() == 4:  # an identity tap's [N, C, H, W] gradient
+                        add = add.permute(0, 2, 3, 1)
+                    add = add.reshape(x.shape)
                     if add.stride(1) != 1 or add.stride(0) != add.shape[1] or add.dtype != x.dtype:
                         add = add.contiguous().to(x.dtype)
             gx = _mm_nn(gy, w.contiguous(), add)
+            park = ctx.park
+            if park is not None and not park.done:
+                # a projection block's conv1: the shortcut's backward (which
+                # runs after this one) accumulates into this gradient
+                park.g, gx = gx, None
         gw = None
         lib = _gemm3_lib(gy, x) if ctx.needs_input_grad[1] else None
         # native split-K from 256 x 128 weights up (51 vs 61 us there, 44 vs
@@ -430,7 +456,7 @@ class _Conv1x1Gemm(torch.autograd.Function):
             else:
                 gw = gy.t() @ x
         gb = gy.sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
-        return gx, gw, gb, None, None
+        return gx, gw, gb, None, None, None
 
 
 class GemmConv1x1(StridedConv1x1):
@@ -454,24 +480,30 @@ class GemmConv1x1(StridedConv1x1):
             return super()._conv_forward(input, weight, bias)
         sh, sw = self.stride
         x = input
+        dev = x.device.type
+        # the block's gradient hand-offs (models/resnet.py Bottleneck):
+        # _dgrad_slot = add the slot's gradient to this input gradient,
+        # _dgrad_park = park this input gradient for the shortcut
+        slot = self.__dict__.pop('_dgrad_slot', None)
+        park = self.__dict__.pop('_dgrad_park', None)
+        if torch.is_autocast_enabled(dev):
+            slot = park = None  # the gradients are summed by autograd
         if (sh, sw) != (1, 1):
-            x = _subsample(input, sh, sw)
+            x = _subsample(input, sh, sw, slot)
+            slot = park = None
         n, c, h, w = x.shape
         x2 = x.permute(0, 2, 3, 1).reshape(n * h * w, c)
         w2 = weight.view(weight.shape[0], c)
-        dev = x.device.type
         if torch.is_autocast_enabled(dev):
             dt = torch.get_autocast_dtype(dev)
             x2, w2 = x2.to(dt), w2.to(dt)
             bias = bias.to(dt) if bias is not None else None
         bn = [None] if getattr(self, '_feeds_bn', False) and _bn_stats_on() else None
-        slot = self.__dict__.pop('_dgrad_slot', None)
-        if slot is not None and ((sh, sw) != (1, 1) or torch.is_autocast_enabled(dev)):
-            slot = None  # the shortcut's gradient is summed by autograd
-        if slot is not None:
-            slot.armed = True
+        for sl in (slot, park):
+            if sl is not None:
+                sl.armed = True
         with torch.autocast(dev, enabled=False):
-            y = _Conv1x1Gemm.apply(x2, w2, bias, bn, slot)
+            y = _Conv1x1Gemm.apply(x2, w2, bias, bn, slot, park)
         out = y.view(n, h, w, -1).permute(0, 3, 1, 2)
         if bn is not None:
             _offer_bn_part(out, bn[0])
