@@ -227,3 +227,26 @@ def test_close_releases_graphs_and_drain_is_safe_without_gpu() -> None:
     assert not runner.graphs and not runner.enabled
     runner()  # still steps, eagerly
     assert runner.eager_steps == 2
+
+
+@pytest.mark.gpu
+def test_verify_leaves_factors_bit_identical(cuda, deterministic) -> None:
+    """The capture-time check runs eager steps (one of them a factor step,
+    whose G-factor SYRKs may still be running on the factor side stream when
+    ``step()`` returns) and restores the saved state after each: the factors
+    after the check and the following factor / plain steps must be bit for
+    bit those of the same run with the check off (restore()
+    ordered after the side stream's work)."""
+    runs = []
+    for verify in (True, False):
+        model, opt, pre, fb = _setup(cuda, method='eigen')
+        runner = GraphedTrainStep(fb, opt, pre, kinds=('plain', 'factor'), verify=verify)
+        for _ in range(14):
+            runner()
+        pre.sync_factors()
+        torch.cuda.synchronize()
+        assert runner.captures == 2, runner.captures
+        runs.append([t.clone() for _, l in pre._layers.values() for t in (l.a_factor, l.g_factor)]
+                    + [p.detach().clone() for p in model.parameters()])
+    for a, b in zip(*runs):
+        assert torch.equal(a, b)
