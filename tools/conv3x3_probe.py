@@ -96,6 +96,17 @@ def main() -> None:
                     [0, 0], 1, [True, False, False])[0]
                 nat['dgrad_err'] = f'{float((dx.double() - refx).norm() / refx.norm()):.1e}'
                 nat['dgrad_us'] = round(timed(nat_dgrad), 1)
+        if lib is not None and ci < 4:
+            # the 3-channel stem: native weight gradient on the 4-channel
+            # zero-padded input (ops/conv.py _pad4) vs MIOpen's
+            from distributed_kfac_pytorch_amd.ops.conv import _pad4
+            xp = _pad4(x)
+            dw = lib.gemm3_conv_wgrad(xp, gy, k, k, s, p)[:, :ci]
+            refw = torch.ops.aten.convolution_backward(
+                gy.double(), x.double(), wt.double(), None, [s, s], [p, p], [1, 1], False,
+                [0, 0], 1, [False, True, False])[1]
+            nat['wgrad_err'] = f'{float((dw.double() - refw).norm() / refw.norm()):.1e}'
+            nat['wgrad_us'] = round(timed(lambda: lib.gemm3_conv_wgrad(xp, gy, k, k, s, p)), 1)
         gf = 2.0 * args.batch * ho * wo * co * ci * k * k / 1e9
         for key, v in zip(('fwd', 'dgrad', 'wgrad'), t):
             tot[key] += cnt * v
