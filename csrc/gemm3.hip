@@ -842,8 +842,14 @@ int gemm3_conv_splits(int N, int H, int W, int C, int Cout, int kh, int kw, int 
   const int Wo = (W + 2 * pad - kw) / stride + 1;
   const int tiles = ((N * Ho * Wo + GT - 1) / GT) * ((Cout + GT - 1) / GT);
   const int kts = (kh * kw * C + GK - 1) / GK;
-  // fill 256 CUs, keeping >= 8 k-tiles per split
-  int sp = (256 + tiles - 1) / tiles;
+  // fill the chip (KFAC_CONV_SPLIT_TARGET blocks, default 256: one per CU),
+  // keeping >= 8 k-tiles per split
+  static const int target = [] {
+    const char* e = std::getenv("KFAC_CONV_SPLIT_TARGET");
+    const int v = e != nullptr ? std::atoi(e) : 256;
+    return v > 0 ? v : 256;
+  }();
+  int sp = (target + tiles - 1) / tiles;
   if (sp > kts / 8) sp = kts / 8;
   if (sp < 1) sp = 1;
   // equal k-tile counts: every split non-empty
