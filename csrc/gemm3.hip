@@ -42,6 +42,7 @@
 #include "common.h"
 
 #include <cstdlib>
+#include <cstring>
 #include "descs.h"
 
 namespace kfac {
@@ -535,6 +536,14 @@ __device__ __forceinline__ void gemm3_tile(const GemmDesc& d, int t, const Patch
   const int w = threadIdx.x >> 6;
   const int l = threadIdx.x & 63;
   const int wr = w >> 1, wc = w & 1;
+  // narrow tile (at most 64 valid columns: a 64-channel convolution
+  // output): the four waves split the 128 rows 32 each over all 64 columns
+  // instead of two of them multiplying zero columns.  Wave w owns rows
+  // rb + 32 i (i < ni) and columns cb + 32 j.
+  const bool narrow = d.N - n0 <= 64 && !(d.vec & 4);
+  const int rb = narrow ? w * 32 : wr * 64;
+  const int cb = narrow ? 0 : wc * 64;
+  const int ni = narrow ? 1 : 2;
 
   v16f acc[2][2];
 #pragma unroll
@@ -619,14 +628,16 @@ __device__ __forceinline__ void gemm3_tile(const GemmDesc& d, int t, const Patch
       v8bf16 ah[2], al[2], bh[2], bl[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const int am = wr * 64 + i * 32;
-        const int bn = wc * 64 + i * 32;
-        if constexpr (A_KC) {
-          ah[i] = frag_kc(Ah, am, kk);
-          al[i] = frag_kc(Al, am, kk);
-        } else {
-          ah[i] = frag_mc(Ah, am, kk);
-          al[i] = frag_mc(Al, am, kk);
+        const int am = rb + (i < ni ? i : 0) * 32;
+        const int bn = cb + i * 32;
+        if (i < ni) {
+          if constexpr (A_KC) {
+            ah[i] = frag_kc(Ah, am, kk);
+            al[i] = frag_kc(Al, am, kk);
+          } else {
+            ah[i] = frag_mc(Ah, am, kk);
+            al[i] = frag_mc(Al, am, kk);
+          }
         }
         if constexpr (B_KC) {
           bh[i] = frag_kc(Bh, bn, kk);
@@ -643,13 +654,15 @@ __device__ __forceinline__ void gemm3_tile(const GemmDesc& d, int t, const Patch
         continue;
       }
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < 2; ++i) {
+        if (i >= ni) continue;  // uniform: narrow tiles have one row block
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
         }
+      }
     }
   };
   // iteration kt: LDS buf[kt&1] holds tile kt, stage (kt+1)&1 holds tile
@@ -676,9 +689,10 @@ __device__ __forceinline__ void gemm3_tile(const GemmDesc& d, int t, const Patch
   // epilogue: C/D layout col = lane & 31, row = (reg&3) + 8 (reg>>2) + 4 (lane>>5)
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
+    if (i >= ni) continue;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int n = n0 + wc * 64 + j * 32 + (l & 31);
+      const int n = n0 + cb + j * 32 + (l & 31);
       if (n >= d.N) continue;
       const float dan = d.da != nullptr ? gload(d.da + n) : 0.f;
       // the addend's 16 values loaded together at clamped rows (one memory
@@ -687,13 +701,13 @@ __device__ __forceinline__ void gemm3_tile(const GemmDesc& d, int t, const Patch
       if (d.D != nullptr) {
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-          const int m = m0 + wr * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (l >> 5);
+          const int m = m0 + rb + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (l >> 5);
           dv[e] = gload(d.D + (int64_t)(m < d.M ? m : d.M - 1) * d.ldc + n);
         }
       }
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        const int m = m0 + wr * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (l >> 5);
+        const int m = m0 + rb + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (l >> 5);
         if (m >= d.M) continue;
         float v = acc[i][j][e];
         if (d.D != nullptr) v += dv[e];
@@ -704,28 +718,58 @@ __device__ __forceinline__ void gemm3_tile(const GemmDesc& d, int t, const Patch
     }
   }
   if (d.bnpart != nullptr) {
-    // BN statistics of this wave's 64 rows: lanes l and l + 32 hold the
-    // two interleaved row sets of a column; rows past M are zero
+    // BN statistics per 64-row half tile: lanes l and l + 32 hold the two
+    // interleaved row sets of a column; rows past M are zero.  A narrow
+    // tile's waves own 32 rows each: waves 2h and 2h + 1 are summed in LDS
+    // (free after the main loop's last barrier) into half h.
     typedef float __attribute__((address_space(1)))* gout_t;
-    const int prow = (m0 / GT) * 2 + wr;
+    float sj[2], qj[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int n = n0 + wc * 64 + j * 32 + (l & 31);
       float s = 0.f, q = 0.f;
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < 2; ++i) {
+        if (i >= ni) continue;
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-          const int m = m0 + wr * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (l >> 5);
+          const int m = m0 + rb + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (l >> 5);
           const float v = m < d.M ? acc[i][j][e] : 0.f;
           s += v;
           q += v * v;
         }
-      s += __shfl_xor(s, 32);
-      q += __shfl_xor(q, 32);
-      if (l < 32 && n < d.N) {
-        ((gout_t)d.bnpart)[(int64_t)(prow * 2) * d.N + n] = s;
-        ((gout_t)d.bnpart)[(int64_t)(prow * 2 + 1) * d.N + n] = q;
+      }
+      sj[j] = s + __shfl_xor(s, 32);
+      qj[j] = q + __shfl_xor(q, 32);
+    }
+    int half = wr;
+    bool writer = true;
+    if (narrow) {
+      float* red = reinterpret_cast<float*>(lds);  // [4 waves][2 j][2][32]
+      if (l < 32) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          red[((w * 2 + j) * 2 + 0) * 32 + l] = sj[j];
+          red[((w * 2 + j) * 2 + 1) * 32 + l] = qj[j];
+        }
+      }
+      __syncthreads();
+      half = w >> 1;
+      writer = (w & 1) == 0;
+      if (writer && l < 32) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          sj[j] += red[(((w + 1) * 2 + j) * 2 + 0) * 32 + l];
+          qj[j] += red[(((w + 1) * 2 + j) * 2 + 1) * 32 + l];
+        }
+      }
+    }
+    const int prow = (m0 / GT) * 2 + half;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + cb + j * 32 + (l & 31);
+      if (writer && l < 32 && n < d.N) {
+        ((gout_t)d.bnpart)[(int64_t)(prow * 2) * d.N + n] = sj[j];
+        ((gout_t)d.bnpart)[(int64_t)(prow * 2 + 1) * d.N + n] = qj[j];
       }
     }
   }
@@ -811,8 +855,21 @@ void gemm3_grouped(const GemmDesc* table, int nlayers, int total_tiles,
 // splits > 1: d.C holds `splits` partial [M][ldc] outputs, split_stride
 // elements apart, each over an equal share of whole k-tiles (every split
 // non-empty: the host passes splits <= the k-tile count)
-void gemm3_single(const GemmDesc& d, bool a_kc, bool b_kc, int splits, int64_t split_stride,
+// KFAC_GEMM3_NARROW (default 0 until measured): 1 = the narrow-tile wave
+// mapping for tiles with at most 64 valid columns (GemmDesc::vec bit 2 set
+// = off)
+static int narrow_off_bit() {
+  static const int bit = [] {
+    const char* e = std::getenv("KFAC_GEMM3_NARROW");
+    return e != nullptr && std::strcmp(e, "1") == 0 ? 0 : 4;
+  }();
+  return bit;
+}
+
+void gemm3_single(const GemmDesc& d0, bool a_kc, bool b_kc, int splits, int64_t split_stride,
                   hipStream_t s) {
+  GemmDesc d = d0;
+  d.vec |= narrow_off_bit();
   const int tiles = ((d.M + GT - 1) / GT) * d.tiles_n;
   if (tiles <= 0 || d.K <= 0) return;
   const int kts = (d.K + GK - 1) / GK;
@@ -823,7 +880,7 @@ void gemm3_single(const GemmDesc& d, bool a_kc, bool b_kc, int splits, int64_t s
   const dim3 grid((unsigned)gemm3_grid(tiles * splits));
   // whole float4-able k-tiles and 4-aligned m-contiguous extents: the
   // tail-free loaders
-  const bool fast = d.K % GK == 0 && d.vec == 3 && d.A_extra == nullptr &&
+  const bool fast = d.K % GK == 0 && (d.vec & 3) == 3 && d.A_extra == nullptr &&
                     (a_kc || d.M % 4 == 0) && (b_kc || d.N % 4 == 0);
 #define G3S(A, B)                                                                    \
   (fast ? gemm3_single_kernel<A, B, true><<<grid, dim3(GNT), 0, s>>>(d, tiles, splits, per,  \
@@ -878,7 +935,7 @@ void gemm3_conv(const float* x, const float* w, float* y, int N, int H, int W, i
   d.K = kh * kw * C;
   d.Kmain = d.K;
   d.tiles_n = (Cout + GT - 1) / GT;
-  d.vec = 3;
+  d.vec = 3 | narrow_off_bit();
   d.bnpart = splits == 1 ? bnpart : nullptr;  // partial sums are not outputs
   const PatchGeom g{H, W, C, Ho, Wo, kw, stride, pad, kh};
   const int tiles = ((d.M + GT - 1) / GT) * d.tiles_n;

@@ -127,7 +127,8 @@ def test_cpp_node_matches_python_function(cuda):
 @pytest.mark.parametrize('kind', ['1x1', '3x3', '3x3s2'])
 @pytest.mark.parametrize('shape', [(4, 64, 14, 14), (8, 128, 28, 28), (2, 256, 7, 9),
                                    (16, 64, 56, 56)])
-def test_conv_epilogue_bn_statistics(cuda, monkeypatch, kind, shape):
+@pytest.mark.parametrize('cout', [96, 64])
+def test_conv_epilogue_bn_statistics(cuda, monkeypatch, kind, shape, cout):
     """A native fp32 convolution marked ``_feeds_bn`` writes the following
     BN's statistics partials from its GEMM epilogue (csrc/gemm3.hip
     bnpart); the fused BN then skips its statistics pass.  Output, running
@@ -139,9 +140,9 @@ def test_conv_epilogue_bn_statistics(cuda, monkeypatch, kind, shape):
     n, c, h, w = shape
     torch.manual_seed(7)
     if kind == '1x1':
-        base = torch.nn.Conv2d(c, 96, 1, bias=False)
+        base = torch.nn.Conv2d(c, cout, 1, bias=False)
     else:
-        base = torch.nn.Conv2d(c, 96, 3, stride=2 if kind == '3x3s2' else 1, padding=1,
+        base = torch.nn.Conv2d(c, cout, 3, stride=2 if kind == '3x3s2' else 1, padding=1,
                                bias=False)
     x = _cl(torch.randn(shape, device=cuda))
     runs = {}
@@ -154,7 +155,7 @@ def test_conv_epilogue_bn_statistics(cuda, monkeypatch, kind, shape):
         else:
             cops.use_implicit_gemm_conv(conv)
         conv[0]._feeds_bn = True
-        bn = bnact.BatchNormAct2d(96).to(cuda)
+        bn = bnact.BatchNormAct2d(cout).to(cuda)
         taken = []
         orig = cops.take_bn_part
 
@@ -175,7 +176,7 @@ def test_conv_epilogue_bn_statistics(cuda, monkeypatch, kind, shape):
     from distributed_kfac_pytorch_amd.ops._native import native
 
     single = kind == '1x1' or int(native().gemm3_conv_splits(
-        n, h, w, c, 96, 3, 3, 2 if kind == '3x3s2' else 1, 1)) == 1
+        n, h, w, c, cout, 3, 3, 2 if kind == '3x3s2' else 1, 1)) == 1
     assert runs['1'][-1] == [single] and runs['0'][-1] == [False]
     names = ('y', 'dx', 'dw', 'dgamma', 'dbeta', 'running_mean', 'running_var')
     for name, a, b in zip(names, runs['1'][:-1], runs['0'][:-1]):
