@@ -509,7 +509,7 @@ __device__ __forceinline__ int gemm3_tile_of_block() {
 // k-tiles [kt_begin, kt_begin + kt_count) of the reduction (split-K
 // callers; kt_count < 0: to the end)
 template <bool A_KC, bool B_KC, bool CONV = false, bool FLIPW = false, bool FASTLD = false,
-          bool PATCHB = false>
+          bool PATCHB = false, bool NARROW = false>
 __device__ __forceinline__ void gemm3_tile(const GemmDesc& d, int t, const PatchGeom& g = {},
                                            int kt_begin = 0, int kt_count = -1) {
   constexpr int A_SZ = A_KC ? GT * LDK : GK * LDM;
@@ -536,14 +536,15 @@ __device__ __forceinline__ void gemm3_tile(const GemmDesc& d, int t, const Patch
   const int w = threadIdx.x >> 6;
   const int l = threadIdx.x & 63;
   const int wr = w >> 1, wc = w & 1;
-  // narrow tile (at most 64 valid columns: a 64-channel convolution
-  // output): the four waves split the 128 rows 32 each over all 64 columns
-  // instead of two of them multiplying zero columns.  Wave w owns rows
-  // rb + 32 i (i < ni) and columns cb + 32 j.
-  const bool narrow = d.N - n0 <= 64 && !(d.vec & 4);
+  // NARROW (a launch whose N <= 64: a 64-channel convolution output): the
+  // four waves split the 128 rows 32 each over all 64 columns instead of
+  // two of them multiplying zero columns.  Wave w owns rows rb + 32 i
+  // (i < ni) and columns cb + 32 j.  A template parameter, so the wide
+  // tiles' index arithmetic stays compile-time.
+  constexpr bool narrow = NARROW;
   const int rb = narrow ? w * 32 : wr * 64;
   const int cb = narrow ? 0 : wc * 64;
-  const int ni = narrow ? 1 : 2;
+  constexpr int ni = narrow ? 1 : 2;
 
   v16f acc[2][2];
 #pragma unroll
@@ -743,7 +744,7 @@ __device__ __forceinline__ void gemm3_tile(const GemmDesc& d, int t, const Patch
     }
     int half = wr;
     bool writer = true;
-    if (narrow) {
+    if constexpr (narrow) {
       float* red = reinterpret_cast<float*>(lds);  // [4 waves][2 j][2][32]
       if (l < 32) {
 #pragma unroll
@@ -789,26 +790,27 @@ gemm3_kernel(const GemmDesc* __restrict__ descs, int nlayers, int total_tiles) {
 // fp32 1x1 convolutions, ops/conv.py)
 // split-K as gemm3_conv_kernel: block b covers tile b % tiles of split
 // b / tiles, whose partial goes to C + split * split_stride
-template <bool A_KC, bool B_KC, bool FASTLD>
+template <bool A_KC, bool B_KC, bool FASTLD, bool NARROW>
 __global__ void __launch_bounds__(GNT, 2)
 gemm3_single_kernel(const GemmDesc d, int tiles, int splits, int kt_per, int64_t split_stride) {
   const int b = gemm3_tile_of_block();
   if (b >= tiles * splits) return;
   if (splits == 1) {
-    gemm3_tile<A_KC, B_KC, false, false, FASTLD>(d, b);
+    gemm3_tile<A_KC, B_KC, false, false, FASTLD, false, NARROW>(d, b);
     return;
   }
   const int z = b / tiles;
   GemmDesc dz = d;
   dz.C = d.C + (int64_t)z * split_stride;
-  gemm3_tile<A_KC, B_KC, false, false, FASTLD>(dz, b - z * tiles, {}, z * kt_per, kt_per);
+  gemm3_tile<A_KC, B_KC, false, false, FASTLD, false, NARROW>(dz, b - z * tiles, {},
+                                                             z * kt_per, kt_per);
 }
 
 // implicit-GEMM convolution: C[N*Ho*Wo][Cout] = patches(x) . w^T, the
 // descriptor and the geometry by value
 // split-K: block b covers tile (b' % tiles) of split (b' / tiles) and
 // writes its partial sum to C + split * split_stride (the host sums them)
-template <bool FLIPW, bool FASTB>
+template <bool FLIPW, bool FASTB, bool NARROW>
 __global__ void __launch_bounds__(GNT, 2)
 gemm3_conv_kernel(const GemmDesc d, const PatchGeom g, int tiles, int splits, int kt_per,
                   int64_t split_stride) {
@@ -817,7 +819,8 @@ gemm3_conv_kernel(const GemmDesc d, const PatchGeom g, int tiles, int splits, in
   const int z = b / tiles;
   GemmDesc dz = d;
   dz.C = d.C + (int64_t)z * split_stride;
-  gemm3_tile<true, !FLIPW, true, FLIPW, FASTB>(dz, b - z * tiles, g, z * kt_per, kt_per);
+  gemm3_tile<true, !FLIPW, true, FLIPW, FASTB, false, NARROW>(dz, b - z * tiles, g, z * kt_per,
+                                                             kt_per);
 }
 
 // weight gradient of the implicit-GEMM convolution: dW[Co][(tap, c)] =
@@ -855,21 +858,18 @@ void gemm3_grouped(const GemmDesc* table, int nlayers, int total_tiles,
 // splits > 1: d.C holds `splits` partial [M][ldc] outputs, split_stride
 // elements apart, each over an equal share of whole k-tiles (every split
 // non-empty: the host passes splits <= the k-tile count)
-// KFAC_GEMM3_NARROW (default 0 until measured): 1 = the narrow-tile wave
-// mapping for tiles with at most 64 valid columns (GemmDesc::vec bit 2 set
-// = off)
-static int narrow_off_bit() {
-  static const int bit = [] {
+// the narrow-tile instantiation for launches with N <= 64
+// (KFAC_GEMM3_NARROW=0: the square wave layout, for A/B runs)
+static bool narrow_for(int N) {
+  static const bool on = [] {
     const char* e = std::getenv("KFAC_GEMM3_NARROW");
-    return e != nullptr && std::strcmp(e, "1") == 0 ? 0 : 4;
+    return e == nullptr || std::strcmp(e, "0") != 0;
   }();
-  return bit;
+  return on && N <= 64;
 }
 
-void gemm3_single(const GemmDesc& d0, bool a_kc, bool b_kc, int splits, int64_t split_stride,
+void gemm3_single(const GemmDesc& d, bool a_kc, bool b_kc, int splits, int64_t split_stride,
                   hipStream_t s) {
-  GemmDesc d = d0;
-  d.vec |= narrow_off_bit();
   const int tiles = ((d.M + GT - 1) / GT) * d.tiles_n;
   if (tiles <= 0 || d.K <= 0) return;
   const int kts = (d.K + GK - 1) / GK;
@@ -880,18 +880,21 @@ void gemm3_single(const GemmDesc& d0, bool a_kc, bool b_kc, int splits, int64_t 
   const dim3 grid((unsigned)gemm3_grid(tiles * splits));
   // whole float4-able k-tiles and 4-aligned m-contiguous extents: the
   // tail-free loaders
-  const bool fast = d.K % GK == 0 && (d.vec & 3) == 3 && d.A_extra == nullptr &&
+  const bool fast = d.K % GK == 0 && d.vec == 3 && d.A_extra == nullptr &&
                     (a_kc || d.M % 4 == 0) && (b_kc || d.N % 4 == 0);
-#define G3S(A, B)                                                                    \
-  (fast ? gemm3_single_kernel<A, B, true><<<grid, dim3(GNT), 0, s>>>(d, tiles, splits, per,  \
-                                                                       split_stride)        \
-        : gemm3_single_kernel<A, B, false><<<grid, dim3(GNT), 0, s>>>(d, tiles, splits, per, \
-                                                                        split_stride))
+  const bool nar = narrow_for(d.N);
+#define G3S_(A, B, NW)                                                                        \
+  (fast ? gemm3_single_kernel<A, B, true, NW><<<grid, dim3(GNT), 0, s>>>(d, tiles, splits, per, \
+                                                                           split_stride)      \
+        : gemm3_single_kernel<A, B, false, NW><<<grid, dim3(GNT), 0, s>>>(d, tiles, splits,    \
+                                                                            per, split_stride))
+#define G3S(A, B) (nar ? G3S_(A, B, true) : G3S_(A, B, false))
   if (a_kc && b_kc) G3S(true, true);
   else if (a_kc) G3S(true, false);
   else if (b_kc) G3S(false, true);
   else G3S(false, false);
 #undef G3S
+#undef G3S_
 }
 
 int gemm3_conv_splits(int N, int H, int W, int C, int Cout, int kh, int kw, int stride, int pad) {
@@ -935,7 +938,7 @@ void gemm3_conv(const float* x, const float* w, float* y, int N, int H, int W, i
   d.K = kh * kw * C;
   d.Kmain = d.K;
   d.tiles_n = (Cout + GT - 1) / GT;
-  d.vec = 3 | narrow_off_bit();
+  d.vec = 3;
   d.bnpart = splits == 1 ? bnpart : nullptr;  // partial sums are not outputs
   const PatchGeom g{H, W, C, Ho, Wo, kw, stride, pad, kh};
   const int tiles = ((d.M + GT - 1) / GT) * d.tiles_n;
@@ -943,17 +946,20 @@ void gemm3_conv(const float* x, const float* w, float* y, int N, int H, int W, i
   const int kts = (d.K + GK - 1) / GK;
   const int per = (kts + splits - 1) / splits;
   const dim3 grid((unsigned)gemm3_grid(tiles * splits));
+  const int64_t st = (int64_t)d.M * Cout;
+#define G3C(FW, FB)                                                                         \
+  (narrow_for(Cout)                                                                         \
+       ? gemm3_conv_kernel<FW, FB, true><<<grid, dim3(GNT), 0, s>>>(d, g, tiles, splits, per, st) \
+       : gemm3_conv_kernel<FW, FB, false><<<grid, dim3(GNT), 0, s>>>(d, g, tiles, splits, per, st))
   if (flipw) {  // host: C % 32 == 0 (whole taps per k-tile)
     d.ldb = Cout;
-    gemm3_conv_kernel<true, true><<<grid, dim3(GNT), 0, s>>>(d, g, tiles, splits, per,
-                                                             (int64_t)d.M * Cout);
+    G3C(true, true);
   } else if (d.K % GK == 0) {
-    gemm3_conv_kernel<false, true><<<grid, dim3(GNT), 0, s>>>(d, g, tiles, splits, per,
-                                                              (int64_t)d.M * Cout);
+    G3C(false, true);
   } else {
-    gemm3_conv_kernel<false, false><<<grid, dim3(GNT), 0, s>>>(d, g, tiles, splits, per,
-                                                               (int64_t)d.M * Cout);
+    G3C(false, false);
   }
+#undef G3C
 }
 
 int gemm3_wgrad_splits(int pixels, int Cout, int kcols) {
