@@ -411,6 +411,15 @@ def run(args: argparse.Namespace, use_kfac: bool, rank: int, world: int,
     if runner is not None:
         out['step_graphs'] = {'replays': runner.replays, 'captures': runner.captures,
                               'eager_steps': runner.eager_steps}
+        # the capture-time check per captured kind: the largest eager-vs-
+        # eager relative difference over parameters / gradients (noise_max:
+        # 0 for a bitwise-deterministic step) and the worst replay distance
+        rep = getattr(runner, 'verify_report', None) or {}
+        if rep:
+            out['step_graphs']['verify'] = {
+                k: {'noise_max': v.get('noise_max'), 'worst': v.get('worst'),
+                    'worst_pair': v.get('worst_pair'), 'ok': v.get('ok')}
+                for k, v in rep.items()}
     if precond is not None and args.impl == 'native':
         out['kfac_layers'] = len(precond._layers)
         out['kfac_steps_end'] = precond.steps
