@@ -129,6 +129,10 @@ def parse_args() -> argparse.Namespace:
     p.add_argument('--cudnn-benchmark', type=int, default=0,
                    help='1: MIOpen find in every process (noisy); 0: immediate mode '
                         'with the shipped tuning db (miopen_db/)')
+    p.add_argument('--cudnn-deterministic', type=int, default=0,
+                   help='1: MIOpen restricted to deterministic solvers (the fp32 step '
+                        'becomes bit-reproducible: its strided 3x3 input gradients are '
+                        'otherwise nondeterministic, tools/determinism_probe.py --fp32)')
     p.add_argument('--dump-steps', default='',
                    help='write every timed step (kind, GPU ms, host issue ms) of the '
                         'K-FAC run to this JSON file (rank 0)')
@@ -168,6 +172,7 @@ def setup(args: argparse.Namespace) -> tuple[int, int, torch.device]:
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
     torch.backends.cudnn.benchmark = bool(args.cudnn_benchmark)
+    torch.backends.cudnn.deterministic = bool(args.cudnn_deterministic)
     if world > 1 or args.ddp:
         if args.graphs and (world == 1 or os.environ.get('KFAC_STEP_GRAPHS_MULTI') == '1'):
             # captured RCCL collectives: the watchdog must not poll (and
@@ -665,6 +670,7 @@ def main() -> None:
                    'HSA_ENABLE_SDMA', 'AMD_LOG_LEVEL', 'CUDA_LAUNCH_BLOCKING')}
     if rt:
         line['runtime_env'] = rt
+    line['cudnn_deterministic'] = bool(args.cudnn_deterministic)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist.is_initialized():

@@ -1,7 +1,8 @@
-"""Are two EAGER bf16 twins of the bench step bit-identical?
+"""Are two EAGER twins of the bench step bit-identical?
 
     python tools/determinism_probe.py [--steps 24] [--conv1x1 gemm|miopen] [--graphed]
                                       [--db=tuned|--db=fresh] [--det-algos] [--go-on]
+                                      [--fp32 [--kxk gemm|miopen]] [--cudnn-det 0|1]
 
 Builds two copies of the bench's ResNet-50 step (batch 32, 224x224, bf16
 autocast, fused weight casts, fused SGD, K-FAC factor 2 / inverse 8) from the
@@ -11,7 +12,11 @@ step the parameters, preconditioned gradients and K-FAC factors: the first
 mismatch is reported with the layers involved, in backward order, so a
 nondeterministic op shows up as the deepest mismatching layer.  With
 ``--graphed`` the first copy runs under ``GraphedTrainStep`` (plain steps
-replayed) as in ``tests/test_graphs_refresh_gpu.py``.
+replayed) as in ``tests/test_graphs_refresh_gpu.py``.  ``--fp32`` steps the
+bench's fp32 headline configuration instead (no autocast; ``--kxk gemm``:
+3x3 convolutions on the native implicit GEMM as in the bench); with
+``--cudnn-det 0`` MIOpen picks its algorithms as the bench lets it
+(``torch.backends.cudnn.deterministic`` off).
 """
 from __future__ import annotations
 
@@ -40,13 +45,17 @@ from distributed_kfac_pytorch_amd.graphs import GraphedTrainStep  # noqa: E402
 from distributed_kfac_pytorch_amd.models.resnet import resnet50  # noqa: E402
 from distributed_kfac_pytorch_amd.ops.cast import enable_fused_weight_cast  # noqa: E402
 from distributed_kfac_pytorch_amd.ops.conv import use_gemm_conv1x1  # noqa: E402
+from distributed_kfac_pytorch_amd.ops.conv import use_implicit_gemm_conv  # noqa: E402
 
 
-def build(base, dev, conv1x1: str, graphed: bool):
+def build(base, dev, conv1x1: str, graphed: bool, fp32: bool = False, kxk: str = 'gemm'):
     model = copy.deepcopy(base).to(dev).to(memory_format=torch.channels_last)
     if conv1x1 == 'gemm':
         use_gemm_conv1x1(model)
-    enable_fused_weight_cast(model)
+    if fp32 and kxk == 'gemm':
+        use_implicit_gemm_conv(model)
+    if not fp32:
+        enable_fused_weight_cast(model)
     opt = torch.optim.SGD(model.parameters(), lr=0.0125, momentum=0.9, weight_decay=5e-5,
                           fused=True)
     pre = kfac.KFACPreconditioner(model, factor_update_steps=2, inv_update_steps=8,
@@ -58,7 +67,7 @@ def build(base, dev, conv1x1: str, graphed: bool):
     raw: dict = {}
 
     def fb() -> torch.Tensor:
-        with torch.autocast('cuda', dtype=torch.bfloat16, cache_enabled=False):
+        with torch.autocast('cuda', dtype=torch.bfloat16, enabled=not fp32, cache_enabled=False):
             loss = crit(model(x), y)
         loss.backward()
         if not torch.cuda.is_current_stream_capturing():
@@ -99,8 +108,11 @@ def main() -> None:
     ap.add_argument('--go-on', action='store_true', help='keep stepping after a mismatch')
     ap.add_argument('--det-algos', action='store_true',
                     help='torch.use_deterministic_algorithms(True, warn_only=True)')
+    ap.add_argument('--fp32', action='store_true', help="the bench's fp32 step (no autocast)")
+    ap.add_argument('--kxk', choices=('gemm', 'miopen'), default='gemm')
+    ap.add_argument('--cudnn-det', type=int, default=1)
     args = ap.parse_args()
-    torch.backends.cudnn.deterministic = True
+    torch.backends.cudnn.deterministic = bool(args.cudnn_det)
     if args.det_algos:
         torch.use_deterministic_algorithms(True, warn_only=True)
     dev = torch.device('cuda', 0)
@@ -110,9 +122,10 @@ def main() -> None:
     gen = torch.Generator(device='cpu').manual_seed(1)
     pool = [(torch.randn(32, 3, 224, 224, generator=gen),
              torch.randint(0, 1000, (32,), generator=gen)) for _ in range(4)]
-    A = build(base, dev, args.conv1x1, args.graphed)
-    B = build(base, dev, args.conv1x1, False)
+    A = build(base, dev, args.conv1x1, args.graphed, args.fp32, args.kxk)
+    B = build(base, dev, args.conv1x1, False, args.fp32, args.kxk)
     report = {'conv1x1': args.conv1x1, 'graphed': args.graphed, 'steps': args.steps,
+              'fp32': args.fp32, 'kxk': args.kxk, 'cudnn_det': args.cudnn_det,
               'db': args.db, 'det_algos': args.det_algos,
               'first_mismatch': None}
     for i in range(args.steps):
