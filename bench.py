@@ -423,7 +423,8 @@ def run(args: argparse.Namespace, use_kfac: bool, rank: int, world: int,
         if rep:
             out['step_graphs']['verify'] = {
                 k: {'noise_max': v.get('noise_max'), 'worst': v.get('worst'),
-                    'worst_pair': v.get('worst_pair'), 'ok': v.get('ok')}
+                    'worst_pair': v.get('worst_pair'), 'strict': v.get('strict'),
+                    'ok': v.get('ok')}
                 for k, v in rep.items()}
     if precond is not None and args.impl == 'native':
         out['kfac_layers'] = len(precond._layers)

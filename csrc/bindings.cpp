@@ -87,6 +87,8 @@ void subsample_bwd(const float* g, float* gx, int N, int H, int W, int C, int sh
 void subsample_bwd_acc(const float* g, float* gx, int N, int H, int W, int C, int sh, int sw,
                    hipStream_t s);
 int gemm3_conv_splits(int N, int H, int W, int C, int Cout, int kh, int kw, int stride, int pad);
+void col2im_nhwc(const float* cols, float* gx, int B, int H, int W, int C, int OH, int OW,
+                 int kh, int kw, int sh, int sw, int ph, int pw, hipStream_t s);
 int gemm3_wgrad_splits(int pixels, int Cout, int kcols);
 void gemm3_conv_wgrad(const float* x, const float* dy, float* dw, int N, int H, int W, int C,
                       int Cout, int kh, int kw, int stride, int pad, int splits, hipStream_t s);
@@ -1296,6 +1298,30 @@ void subsample_bwd_acc(const at::Tensor& gy, const at::Tensor& gx, int64_t sh, i
                           (int)C, (int)sh, (int)sw, cur_stream());
 }
 
+// gx[B, C, H, W] (channels_last) = col2im(cols): the adjoint of the NHWC
+// im2col, cols the contiguous fp32 [B * OH * OW, kh * kw * C] in (ky, kx, c)
+// column order (csrc/im2col.hip col2im_nhwc; fixed-order sums)
+at::Tensor col2im_nhwc(const at::Tensor& cols, int64_t B, int64_t C, int64_t H, int64_t W,
+                       int64_t kh, int64_t kw, int64_t stride, int64_t pad) {
+  check_cuda(cols, "col2im cols");
+  TORCH_CHECK(C % 4 == 0 && kh >= 1 && kw >= 1 && stride >= 1 && pad >= 0,
+              "col2im_nhwc: C % 4 == 0, positive geometry");
+  const int64_t OH = (H + 2 * pad - kh) / stride + 1, OW = (W + 2 * pad - kw) / stride + 1;
+  TORCH_CHECK(OH >= 1 && OW >= 1 && cols.scalar_type() == at::kFloat && cols.dim() == 2 &&
+                  cols.is_contiguous() && cols.size(0) == B * OH * OW &&
+                  cols.size(1) == kh * kw * C &&
+                  (reinterpret_cast<uintptr_t>(cols.data_ptr()) & 15) == 0,
+              "col2im_nhwc: cols must be a 16-byte aligned contiguous fp32 [B*OH*OW, kh*kw*C]");
+  TORCH_CHECK(B * H * W * C < ((int64_t)1 << 31) * 4 && B * H * W < ((int64_t)1 << 31),
+              "col2im_nhwc: too large");
+  auto gx = at::empty({B, C, H, W}, cols.options().memory_format(at::MemoryFormat::ChannelsLast));
+  c10::hip::HIPGuardMasqueradingAsCUDA g(cols.device());
+  kfac::col2im_nhwc(cols.data_ptr<float>(), gx.data_ptr<float>(), (int)B, (int)H, (int)W, (int)C,
+                    (int)OH, (int)OW, (int)kh, (int)kw, (int)stride, (int)stride, (int)pad,
+                    (int)pad, cur_stream());
+  return gx;
+}
+
 void gemm3_grouped(const at::Tensor& table, int64_t nlayers, int64_t total_tiles,
                    bool a_kc, bool b_kc) {
   check_cuda(table, "table");
@@ -1573,6 +1599,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm3_grouped", &gemm3_grouped);
   m.def("subsample_fwd", &subsample_fwd, py::arg("x"), py::arg("sh"), py::arg("sw"));
   m.def("sum_splits", &sum_splits, py::arg("part"), py::arg("out") = py::none());
+  m.def("col2im_nhwc", &col2im_nhwc, py::arg("cols"), py::arg("B"), py::arg("C"), py::arg("H"),
+        py::arg("W"), py::arg("kh"), py::arg("kw"), py::arg("stride"), py::arg("pad"));
   m.def("subsample_bwd_acc", &subsample_bwd_acc, py::arg("gy"), py::arg("gx"), py::arg("sh"),
         py::arg("sw"));
   m.def("subsample_bwd", &subsample_bwd, py::arg("gy"), py::arg("h"), py::arg("w"),

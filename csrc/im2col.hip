@@ -115,6 +115,40 @@ im2col_nchw_kernel(const TI* __restrict__ x, int64_t C, int64_t H, int64_t W,
   }
 }
 
+// col2im, the adjoint of im2col_nhwc_vec_kernel (fp32, float4 lanes): gx[b][y][x][c] =
+// sum over the taps (ky, kx) whose output pixel oy = (y + ph - ky) / sh, ox = (x + pw - kx) / sw
+// is integral and in range of cols[(b, oy, ox)][(ky, kx, c)].  A strided convolution's input
+// gradient as (dy . W) then col2im: every gx element is one thread's fixed-order sum, so the
+// result is bit-reproducible (MIOpen's strided backward-data solvers are not).
+__global__ void __launch_bounds__(256)
+col2im_nhwc_kernel(const float4* __restrict__ cols, float4* __restrict__ gx, int64_t total4,
+                   int C4, int H, int W, int OH, int OW, int kh, int kw, int sh, int sw, int ph,
+                   int pw) {
+  const int64_t KC4 = (int64_t)kh * kw * C4;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total4;
+       i += (int64_t)gridDim.x * 256) {
+    const int64_t pix = i / C4;
+    const int c = (int)(i - pix * C4);
+    const int x = (int)(pix % W);
+    const int64_t q = pix / W;
+    const int y = (int)(q % H);
+    const int64_t b = q / H;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int ky = 0; ky < kh; ++ky) {
+      const int t = y + ph - ky;
+      if (t < 0 || t % sh != 0 || t / sh >= OH) continue;
+      const int64_t rowy = (b * OH + t / sh) * OW;
+      for (int kx = 0; kx < kw; ++kx) {
+        const int u = x + pw - kx;
+        if (u < 0 || u % sw != 0 || u / sw >= OW) continue;
+        const float4 v = cols[(rowy + u / sw) * KC4 + (int64_t)(ky * kw + kx) * C4 + c];
+        a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+      }
+    }
+    gx[i] = a;
+  }
+}
+
 inline unsigned grid_for(int64_t n) {
   int64_t g = ceil_div(n, 256);
   if (g > 8192) g = 8192;
@@ -185,6 +219,14 @@ void im2col_nchw(int dtype, const void* x, int64_t B, int64_t C, int64_t H,
   else if (dtype == kF16 && out_dtype == kBF16) KFAC_NCHW(__half, bf16_t);
   else if (dtype == kF16 && out_dtype == kF32) KFAC_NCHW(__half, float);
 #undef KFAC_NCHW
+}
+
+void col2im_nhwc(const float* cols, float* gx, int B, int H, int W, int C, int OH, int OW,
+                 int kh, int kw, int sh, int sw, int ph, int pw, hipStream_t s) {
+  const int64_t total4 = (int64_t)B * H * W * (C / 4);
+  if (total4 == 0) return;
+  col2im_nhwc_kernel<<<grid_for(total4), 256, 0, s>>>(
+      (const float4*)cols, (float4*)gx, total4, C / 4, H, W, OH, OW, kh, kw, sh, sw, ph, pw);
 }
 
 }  // namespace kfac

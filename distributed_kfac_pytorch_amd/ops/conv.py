@@ -192,6 +192,15 @@ def _wgrad_kxk() -> str:
     return getenv('KFAC_CONV_KXK_WGRAD', 'native')
 
 
+def _conv_deterministic() -> bool:
+    """``KFAC_CONV_DETERMINISTIC`` (default 1): the fp32 ``ImplicitGemmConv2d``
+    backward keeps off MIOpen's nondeterministic solvers -- strided input
+    gradients as ``dy . W`` plus a fixed-order col2im, 64-channel and stem
+    weight gradients on the native split-K kernel -- so the fp32 step is bit
+    reproducible (``tools/determinism_probe.py --fp32``)."""
+    return getenv('KFAC_CONV_DETERMINISTIC', '1') == '1'
+
+
 def _splitk_few_tiles() -> bool:
     return getenv('KFAC_CONV1X1_SPLITK', '0') == '1'
 
@@ -537,17 +546,24 @@ class _ConvImplicit(torch.autograd.Function):
     gradient at stride 1 (the convolution of ``dy`` with the flipped,
     transposed kernel, read in place) and the weight gradient
     (``dy^T . patches(x)``, split-K) on the native implicit GEMM; strided
-    input gradients (and 64-channel weight gradients) through MIOpen's
-    ``convolution_backward``."""
+    input gradients as ``dy . W`` (gemm3) plus the native fixed-order col2im
+    under ``KFAC_CONV_DETERMINISTIC`` (MIOpen's ``convolution_backward``
+    otherwise, as for 64-channel weight gradients then).  ``miopen_fwd``:
+    the forward through MIOpen (``StemConv2d``)."""
 
     @staticmethod
     def forward(  # type: ignore[override]
         ctx, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None, stride: int, pad: int,
         lib,  # type: ignore[no-untyped-def]
         bn: list | None = None,
+        miopen_fwd: bool = False,
     ) -> torch.Tensor:
         ctx.save_for_backward(x, w)
         ctx.conf = (stride, pad, b is not None, lib)
+        if miopen_fwd:
+            # the stem: MIOpen's forward is the faster one there, the
+            # backward below is native
+            return F.conv2d(x, w, b, stride, pad)
         xp = _pad4(x)
         part = None
         if bn is not None and b is None:
@@ -578,12 +594,24 @@ class _ConvImplicit(torch.autograd.Function):
             # the flipped, transposed kernel is read in place (flipw)
             gx = lib.gemm3_conv(gy, w.contiguous(memory_format=torch.channels_last), 1,
                                 k - 1 - pad, True)
+        det = _conv_deterministic()
+        if (ctx.needs_input_grad[0] and not native_dx and det and stride > 1
+                and x.shape[1] % 4 == 0):
+            # strided: cols = dy . W ([pixels, Cout] x [Cout, kh*kw*C], the
+            # channels_last weight read in place), then each input-gradient
+            # element sums its taps in a fixed order (col2im)
+            n, c, h, wd = x.shape
+            cout = w.shape[0]
+            w2 = w.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1)
+            w2 = w2.reshape(cout, -1)
+            cols = _mm3(lib, gy.permute(0, 2, 3, 1).reshape(-1, cout), w2, w2.shape[1], False)
+            gx = lib.col2im_nhwc(cols, n, c, h, wd, k, w.shape[3], stride, pad)
         # native weight gradient (split-K over the pixels) from 128 input
         # channels up: 54-71 us vs MIOpen's 85-87; at 64 MIOpen's 85 beats
         # 96 (profiles/r5/conv3x3_probe.jsonl)
         # (the kernel indexes output pixels in 22 bits: larger inputs, e.g.
         # 128 channels at 512x512 from batch 16, go to MIOpen)
-        native_dw = (ctx.needs_input_grad[1] and (x.shape[1] >= 128 or x.shape[1] < 4)
+        native_dw = (ctx.needs_input_grad[1] and (x.shape[1] >= 128 or x.shape[1] < 4 or det)
                      and w.shape[0] % 4 == 0
                      and gy.shape[0] * gy.shape[2] * gy.shape[3] < (1 << 22)
                      and x.numel() + 4 * x.shape[0] * x.shape[2] * x.shape[3] < (1 << 31)
@@ -591,7 +619,7 @@ class _ConvImplicit(torch.autograd.Function):
         if native_dw:
             gw = lib.gemm3_conv_wgrad(_pad4(x), gy, k, w.shape[3], stride, pad)
             gw = gw[:, :x.shape[1]]
-        mask = [ctx.needs_input_grad[0] and not native_dx,
+        mask = [ctx.needs_input_grad[0] and gx is None,
                 ctx.needs_input_grad[1] and not native_dw, False]
         if any(mask):
             r = torch.ops.aten.convolution_backward(
@@ -602,7 +630,7 @@ class _ConvImplicit(torch.autograd.Function):
                 gw = r[1]
         if has_bias and ctx.needs_input_grad[2]:
             gb = gy.sum((0, 2, 3))
-        return gx, gw, gb, None, None, None, None
+        return gx, gw, gb, None, None, None, None, None
 
 
 def _pad4(t: torch.Tensor) -> torch.Tensor:
@@ -615,14 +643,18 @@ def _pad4(t: torch.Tensor) -> torch.Tensor:
     return torch.cat([t, z], 1).contiguous(memory_format=torch.channels_last)
 
 
-def _implicit_ok(m: nn.Conv2d) -> bool:
+def _implicit_shape_ok(m: nn.Conv2d) -> bool:
     kh, kw = m.kernel_size
     return (m.groups == 1 and tuple(m.dilation) == (1, 1) and m.padding_mode == 'zeros'
             and kh == kw and kh > 1 and isinstance(m.padding, tuple)
-            and m.padding[0] == m.padding[1] and m.stride[0] == m.stride[1]
-            # the 3-channel stem runs (4-channel padded) but slower than
-            # MIOpen's: bench 1932 vs 1942-1950 img/s with it switched
-            and m.in_channels % 4 == 0)
+            and m.padding[0] == m.padding[1] and m.stride[0] == m.stride[1])
+
+
+def _implicit_ok(m: nn.Conv2d) -> bool:
+    # the 3-channel stem runs (4-channel padded) but slower than MIOpen's:
+    # bench 1932 vs 1942-1950 img/s with it switched (it becomes a
+    # StemConv2d: MIOpen forward, native weight gradient)
+    return _implicit_shape_ok(m) and m.in_channels % 4 == 0
 
 
 class ImplicitGemmConv2d(nn.Conv2d):
@@ -657,13 +689,39 @@ class ImplicitGemmConv2d(nn.Conv2d):
         return out
 
 
+class StemConv2d(nn.Conv2d):
+    """A convolution whose input channels are not a multiple of 4 (ResNet's
+    3-channel stem): MIOpen's forward (faster there than the padded native
+    one), and under ``KFAC_CONV_DETERMINISTIC`` the fp32 channels_last weight
+    gradient on the native split-K kernel (``_ConvImplicit`` with
+    ``miopen_fwd``) instead of MIOpen's global-split solver, whose atomics
+    make it nondeterministic; the two cost the same
+    (``tools/conv3x3_probe.py``, profiles/r6/).  Same module, parameters and
+    state-dict keys as ``nn.Conv2d``."""
+
+    def _conv_forward(  # type: ignore[override]
+        self,
+        input: torch.Tensor,
+        weight: torch.Tensor,
+        bias: torch.Tensor | None,
+    ) -> torch.Tensor:
+        lib = _gemm3_lib(input, weight, math=conv_kxk_math())
+        if (lib is None or not _conv_deterministic()
+                or torch.is_autocast_enabled(input.device.type)
+                or not input.is_contiguous(memory_format=torch.channels_last)):
+            return super()._conv_forward(input, weight, bias)
+        return _ConvImplicit.apply(input, weight, bias, self.stride[0], self.padding[0], lib,
+                                   None, True)
+
+
 def use_implicit_gemm_conv(model: nn.Module) -> int:
     """Switch every eligible non-1x1 ``nn.Conv2d`` of ``model`` (in place)
-    to ``ImplicitGemmConv2d``.  Returns the number switched."""
+    to ``ImplicitGemmConv2d`` (to ``StemConv2d`` when its input channels are
+    not a multiple of 4).  Returns the number switched."""
     n = 0
     for m in model.modules():
-        if type(m) is nn.Conv2d and _implicit_ok(m):
-            m.__class__ = ImplicitGemmConv2d
+        if type(m) is nn.Conv2d and _implicit_shape_ok(m):
+            m.__class__ = ImplicitGemmConv2d if _implicit_ok(m) else StemConv2d
             n += 1
     return n
 

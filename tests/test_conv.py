@@ -275,6 +275,90 @@ def test_implicit_gemm_conv_wgrad_falls_back_past_kernel_limit(cuda, monkeypatch
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('shape,stride,k,stem', [((32, 128, 56, 56, 128), 2, 3, False),
+                                                 ((32, 512, 14, 14, 512), 2, 3, False),
+                                                 ((3, 12, 9, 11, 40), 2, 3, False),
+                                                 ((2, 8, 10, 10, 40), 3, 5, False),
+                                                 ((16, 64, 56, 56, 64), 1, 3, False),
+                                                 ((32, 3, 224, 224, 64), 2, 7, True)])
+def test_deterministic_conv_backward(cuda, shape, stride, k, stem, monkeypatch) -> None:
+    """``KFAC_CONV_DETERMINISTIC=1`` (the default): a strided input gradient
+    is ``dy . W`` on gemm3 plus the native fixed-order col2im, a 64-channel
+    weight gradient and the 3-channel stem's (``StemConv2d``: MIOpen
+    forward) run on the native split-K kernel.  Gradients match float64 to
+    fp32-class accuracy, the native kernels run, MIOpen's backward does not,
+    and two backward passes are bit-identical."""
+    from distributed_kfac_pytorch_amd.ops import _native
+    from distributed_kfac_pytorch_amd.ops import conv as cops
+
+    lib = _native.native()
+    assert lib is not None, _native.load_error()
+    calls: list = []
+
+    class Spy:
+        def __getattr__(self, name):  # type: ignore[no-untyped-def]
+            return getattr(lib, name)
+
+        def col2im_nhwc(self, *a):  # type: ignore[no-untyped-def]
+            calls.append('col2im')
+            return lib.col2im_nhwc(*a)
+
+        def gemm3_conv_wgrad(self, *a):  # type: ignore[no-untyped-def]
+            calls.append('wgrad')
+            return lib.gemm3_conv_wgrad(*a)
+
+    real_cb = torch.ops.aten.convolution_backward
+
+    class Aten:
+        def __getattr__(self, name):  # type: ignore[no-untyped-def]
+            return getattr(torch.ops.aten, name)
+
+        def convolution_backward(self, *a):  # type: ignore[no-untyped-def]
+            calls.append('miopen')
+            return real_cb(*a)
+
+    monkeypatch.setattr(_native, 'native', lambda: Spy())
+    monkeypatch.setattr(cops.torch.ops, 'aten', Aten(), raising=False)
+    monkeypatch.setenv('KFAC_CONV_KXK_MATH', 'bf16x3')
+    monkeypatch.setenv('KFAC_CONV_DETERMINISTIC', '1')
+    n, c, h, w, co = shape
+    torch.manual_seed(0)
+    conv = nn.Conv2d(c, co, k, stride=stride, padding=k // 2, bias=False).to(cuda)
+    conv = conv.to(memory_format=torch.channels_last)
+    assert cops.use_implicit_gemm_conv(conv) == 1
+    assert type(conv) is (cops.StemConv2d if stem else cops.ImplicitGemmConv2d)
+    x = torch.randn(n, c, h, w, device=cuda).contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(not stem)
+    y = conv(x)
+    g = torch.randn_like(y)
+    grads = []
+    for _ in range(2):
+        calls.clear()
+        conv.weight.grad = None
+        x.grad = None
+        y = conv(x)
+        y.backward(g)
+        grads.append((None if stem else x.grad.clone(), conv.weight.grad.clone()))
+        assert 'miopen' not in calls, calls
+        assert 'wgrad' in calls, calls
+        assert ('col2im' in calls) == (stride > 1 and not stem), calls
+    assert stem or torch.equal(grads[0][0], grads[1][0])
+    assert torch.equal(grads[0][1], grads[1][1])
+    xd = x.detach().double().requires_grad_(not stem)
+    wd = conv.weight.detach().double().requires_grad_(True)
+    yd = torch.nn.functional.conv2d(xd, wd, None, stride=stride, padding=k // 2)
+    yd.backward(g.double())
+
+    def rel(a: torch.Tensor, b: torch.Tensor) -> float:
+        return float((a.double() - b).norm() / b.norm())
+
+    assert rel(y, yd) < 2e-5, rel(y, yd)
+    assert rel(conv.weight.grad, wd.grad) < 2e-5, rel(conv.weight.grad, wd.grad)
+    if not stem:
+        assert rel(x.grad, xd.grad) < 2e-5, rel(x.grad, xd.grad)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize('shape,s', [((32, 256, 56, 56), 2), ((3, 12, 7, 9), 2), ((2, 8, 10, 10), 3)])
 def test_subsample_native_exact(cuda, shape, s) -> None:
     """The strided 1x1 convolutions' subsample and its adjoint on the native

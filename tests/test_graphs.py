@@ -8,6 +8,7 @@ import torch
 
 import distributed_kfac_pytorch_amd as kfac
 from distributed_kfac_pytorch_amd.graphs import GraphedTrainStep
+from distributed_kfac_pytorch_amd.graphs import verify_ratio
 from distributed_kfac_pytorch_amd.graphs import verify_tolerance
 
 
@@ -69,6 +70,20 @@ def test_verify_tolerance() -> None:
     big = verify_tolerance(torch.tensor([0.0, 0.6], dtype=torch.float64))
     assert float(big[0]) == pytest.approx(0.251)
     assert torch.isnan(verify_tolerance(torch.tensor([0.0, float('nan')]))).all()
+
+
+def test_verify_ratio_strict() -> None:
+    """A bit-reproducible eager step (all noise zero) makes the check
+    strict: any nonzero replay distance fails, zero passes; otherwise the
+    distance is measured against the tolerance and non-finite fails."""
+    tol = verify_tolerance(torch.zeros(3, dtype=torch.float64))
+    d = torch.tensor([0.0, 1e-7, 0.0], dtype=torch.float64)
+    assert float(verify_ratio(d, tol, False).max()) < 1.0
+    strict = verify_ratio(d, tol, True)
+    assert strict[0] == 0 and strict[2] == 0 and torch.isinf(strict[1])
+    assert float(verify_ratio(torch.zeros(3, dtype=torch.float64), tol, True).max()) == 0.0
+    assert torch.isinf(verify_ratio(torch.tensor([float('nan')]), tol[:1], False)).all()
+    assert torch.isinf(verify_ratio(torch.tensor([float('nan')]), tol[:1], True)).all()
 
 
 def test_step_kinds() -> None:
