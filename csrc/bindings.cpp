@@ -87,8 +87,8 @@ void subsample_bwd(const float* g, float* gx, int N, int H, int W, int C, int sh
 void subsample_bwd_acc(const float* g, float* gx, int N, int H, int W, int C, int sh, int sw,
                    hipStream_t s);
 int gemm3_conv_splits(int N, int H, int W, int C, int Cout, int kh, int kw, int stride, int pad);
-void col2im_nhwc(const float* cols, float* gx, int B, int H, int W, int C, int OH, int OW,
-                 int kh, int kw, int sh, int sw, int ph, int pw, hipStream_t s);
+void col2im_nhwc(int dtype, const void* cols, void* gx, int B, int H, int W, int C, int OH,
+                 int OW, int kh, int kw, int sh, int sw, int ph, int pw, hipStream_t s);
 int gemm3_wgrad_splits(int pixels, int Cout, int kcols);
 void gemm3_conv_wgrad(const float* x, const float* dy, float* dw, int N, int H, int W, int C,
                       int Cout, int kh, int kw, int stride, int pad, int splits, hipStream_t s);
@@ -1298,27 +1298,29 @@ void subsample_bwd_acc(const at::Tensor& gy, const at::Tensor& gx, int64_t sh, i
                           (int)C, (int)sh, (int)sw, cur_stream());
 }
 
-// gx[B, C, H, W] (channels_last) = col2im(cols): the adjoint of the NHWC
-// im2col, cols the contiguous fp32 [B * OH * OW, kh * kw * C] in (ky, kx, c)
-// column order (csrc/im2col.hip col2im_nhwc; fixed-order sums)
+// gx[B, C, H, W] (channels_last, cols' dtype) = col2im(cols): the adjoint of
+// the NHWC im2col, cols the contiguous fp32 or bf16 [B * OH * OW, kh * kw * C]
+// in (ky, kx, c) column order (csrc/im2col.hip col2im_nhwc; fixed-order fp32
+// sums)
 at::Tensor col2im_nhwc(const at::Tensor& cols, int64_t B, int64_t C, int64_t H, int64_t W,
                        int64_t kh, int64_t kw, int64_t stride, int64_t pad) {
   check_cuda(cols, "col2im cols");
-  TORCH_CHECK(C % 4 == 0 && kh >= 1 && kw >= 1 && stride >= 1 && pad >= 0,
-              "col2im_nhwc: C % 4 == 0, positive geometry");
+  const bool bf = cols.scalar_type() == at::kBFloat16;
+  TORCH_CHECK((bf ? C % 8 : C % 4) == 0 && kh >= 1 && kw >= 1 && stride >= 1 && pad >= 0,
+              "col2im_nhwc: C % 4 == 0 (fp32) / C % 8 == 0 (bf16), positive geometry");
   const int64_t OH = (H + 2 * pad - kh) / stride + 1, OW = (W + 2 * pad - kw) / stride + 1;
-  TORCH_CHECK(OH >= 1 && OW >= 1 && cols.scalar_type() == at::kFloat && cols.dim() == 2 &&
+  TORCH_CHECK(OH >= 1 && OW >= 1 && (bf || cols.scalar_type() == at::kFloat) && cols.dim() == 2 &&
                   cols.is_contiguous() && cols.size(0) == B * OH * OW &&
                   cols.size(1) == kh * kw * C &&
                   (reinterpret_cast<uintptr_t>(cols.data_ptr()) & 15) == 0,
-              "col2im_nhwc: cols must be a 16-byte aligned contiguous fp32 [B*OH*OW, kh*kw*C]");
+              "col2im_nhwc: cols must be a 16-byte aligned contiguous fp32 / bf16 [B*OH*OW, kh*kw*C]");
   TORCH_CHECK(B * H * W * C < ((int64_t)1 << 31) * 4 && B * H * W < ((int64_t)1 << 31),
               "col2im_nhwc: too large");
   auto gx = at::empty({B, C, H, W}, cols.options().memory_format(at::MemoryFormat::ChannelsLast));
   c10::hip::HIPGuardMasqueradingAsCUDA g(cols.device());
-  kfac::col2im_nhwc(cols.data_ptr<float>(), gx.data_ptr<float>(), (int)B, (int)H, (int)W, (int)C,
-                    (int)OH, (int)OW, (int)kh, (int)kw, (int)stride, (int)stride, (int)pad,
-                    (int)pad, cur_stream());
+  kfac::col2im_nhwc(bf ? kfac::kBF16 : kfac::kF32, cols.data_ptr(), gx.data_ptr(), (int)B, (int)H,
+                    (int)W, (int)C, (int)OH, (int)OW, (int)kh, (int)kw, (int)stride, (int)stride,
+                    (int)pad, (int)pad, cur_stream());
   return gx;
 }
 

@@ -149,6 +149,49 @@ col2im_nhwc_kernel(const float4* __restrict__ cols, float4* __restrict__ gx, int
   }
 }
 
+// the bf16 variant (the bf16 autocast step's 3x3 input gradients, cols from a
+// bf16 GEMM): 8 channels (16 bytes) per thread, summed in fp32 in the same
+// fixed tap order, rounded once to bf16
+__global__ void __launch_bounds__(256)
+col2im_nhwc_bf16_kernel(const uint4* __restrict__ cols, uint4* __restrict__ gx, int64_t total8,
+                        int C8, int H, int W, int OH, int OW, int kh, int kw, int sh, int sw,
+                        int ph, int pw) {
+  const int64_t KC8 = (int64_t)kh * kw * C8;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total8;
+       i += (int64_t)gridDim.x * 256) {
+    const int64_t pix = i / C8;
+    const int c = (int)(i - pix * C8);
+    const int x = (int)(pix % W);
+    const int64_t q = pix / W;
+    const int y = (int)(q % H);
+    const int64_t b = q / H;
+    float a[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[e] = 0.f;
+    for (int ky = 0; ky < kh; ++ky) {
+      const int t = y + ph - ky;
+      if (t < 0 || t % sh != 0 || t / sh >= OH) continue;
+      const int64_t rowy = (b * OH + t / sh) * OW;
+      for (int kx = 0; kx < kw; ++kx) {
+        const int u = x + pw - kx;
+        if (u < 0 || u % sw != 0 || u / sw >= OW) continue;
+        const uint4 v = cols[(rowy + u / sw) * KC8 + (int64_t)(ky * kw + kx) * C8 + c];
+        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          a[2 * e] += bf16_bits_to_f32((uint16_t)(w4[e] & 0xffffu));
+          a[2 * e + 1] += bf16_bits_to_f32((uint16_t)(w4[e] >> 16));
+        }
+      }
+    }
+    uint32_t o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      o[e] = (uint32_t)f32_to_bf16_bits(a[2 * e]) | ((uint32_t)f32_to_bf16_bits(a[2 * e + 1]) << 16);
+    gx[i] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
 inline unsigned grid_for(int64_t n) {
   int64_t g = ceil_div(n, 256);
   if (g > 8192) g = 8192;
@@ -221,8 +264,15 @@ void im2col_nchw(int dtype, const void* x, int64_t B, int64_t C, int64_t H,
 #undef KFAC_NCHW
 }
 
-void col2im_nhwc(const float* cols, float* gx, int B, int H, int W, int C, int OH, int OW,
-                 int kh, int kw, int sh, int sw, int ph, int pw, hipStream_t s) {
+void col2im_nhwc(int dtype, const void* cols, void* gx, int B, int H, int W, int C, int OH,
+                 int OW, int kh, int kw, int sh, int sw, int ph, int pw, hipStream_t s) {
+  if (dtype == kBF16) {
+    const int64_t total8 = (int64_t)B * H * W * (C / 8);
+    if (total8 == 0) return;
+    col2im_nhwc_bf16_kernel<<<grid_for(total8), 256, 0, s>>>(
+        (const uint4*)cols, (uint4*)gx, total8, C / 8, H, W, OH, OW, kh, kw, sh, sw, ph, pw);
+    return;
+  }
   const int64_t total4 = (int64_t)B * H * W * (C / 4);
   if (total4 == 0) return;
   col2im_nhwc_kernel<<<grid_for(total4), 256, 0, s>>>(

@@ -201,6 +201,16 @@ def _conv_deterministic() -> bool:
     return getenv('KFAC_CONV_DETERMINISTIC', '1') == '1'
 
 
+def _conv_deterministic_lowp() -> bool:
+    """``KFAC_CONV_DETERMINISTIC_BF16`` (default 0, opt-in): under bf16
+    autocast the ``ImplicitGemmConv2d`` / ``StemConv2d`` run as bf16 GEMMs
+    (``_ConvLowpDet``: im2col forward, ``dy . W`` + the native bf16 col2im,
+    ``dy^T . patches``) instead of MIOpen's bf16 solvers, whose global-split
+    variants accumulate with atomics.  Not the default: it costs the bf16
+    step ~2.5 ms (profiles/r6/deterministic_bf16/)."""
+    return getenv('KFAC_CONV_DETERMINISTIC_BF16', '0') == '1'
+
+
 def _splitk_few_tiles() -> bool:
     return getenv('KFAC_CONV1X1_SPLITK', '0') == '1'
 
@@ -633,6 +643,76 @@ class _ConvImplicit(torch.autograd.Function):
         return gx, gw, gb, None, None, None, None, None
 
 
+class _ConvLowpDet(torch.autograd.Function):
+    """bf16 ``y = conv2d(x, w, b, stride, pad)`` (autocast off inside) as
+    bf16 GEMMs with fp32 accumulation, bit-reproducible end to end: forward
+    ``im2col(x) . W^T`` (the channels_last weight read as [Cout, kh*kw*C];
+    MIOpen's tuned bf16 forward takes global-split solvers with atomics for
+    the 512-channel 7x7-output convolutions), input gradient ``cols = dy .
+    W`` then the native fixed-order col2im (C % 8 == 0; MIOpen otherwise),
+    weight gradient ``dy^T . patches`` from the forward's saved patches."""
+
+    @staticmethod
+    def forward(  # type: ignore[override]
+        ctx, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None, stride: int, pad: int,
+        lib,  # type: ignore[no-untyped-def]
+    ) -> torch.Tensor:
+        n, c, h, wd = x.shape
+        cout, _, kh, kw = w.shape
+        ho = (h + 2 * pad - kh) // stride + 1
+        wo = (wd + 2 * pad - kw) // stride + 1
+        patches = torch.empty(n * ho * wo, kh * kw * c, dtype=x.dtype, device=x.device)
+        lib.im2col(x, patches, kh, kw, stride, stride, pad, pad, True)
+        w2 = w.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1).reshape(cout, -1)
+        y2 = torch.mm(patches, w2.t()) if b is None else torch.addmm(b, patches, w2.t())
+        ctx.save_for_backward(x, w, patches)
+        ctx.conf = (stride, pad, b is not None, lib)
+        return y2.view(n, ho, wo, cout).permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, gy: torch.Tensor) -> tuple:  # type: ignore[override]
+        x, w, patches = ctx.saved_tensors
+        stride, pad, has_bias, lib = ctx.conf
+        gy = gy.contiguous(memory_format=torch.channels_last)
+        n, c, h, wd = x.shape
+        cout, _, kh, kw = w.shape
+        gy2 = gy.permute(0, 2, 3, 1).reshape(-1, cout)
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            if c % 8 == 0:
+                w2 = w.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1)
+                cols = torch.mm(gy2, w2.reshape(cout, -1))
+                gx = lib.col2im_nhwc(cols, n, c, h, wd, kh, kw, stride, pad)
+            else:
+                gx = torch.ops.aten.convolution_backward(
+                    gy, x, w, None, [stride, stride], [pad, pad], [1, 1], False, [0, 0], 1,
+                    [True, False, False])[0]
+        if ctx.needs_input_grad[1]:
+            gw = torch.mm(gy2.t(), patches).view(cout, kh, kw, c).permute(0, 3, 1, 2)
+        if has_bias and ctx.needs_input_grad[2]:
+            gb = gy.float().sum((0, 2, 3)).to(gy.dtype)
+        return gx, gw, gb, None, None, None
+
+
+def _lowp_det_conv(m: nn.Conv2d, input: torch.Tensor, weight: torch.Tensor,
+                   bias: torch.Tensor | None) -> torch.Tensor | None:
+    """``_ConvLowpDet`` for a bf16-autocast convolution when
+    ``KFAC_CONV_DETERMINISTIC_BF16`` applies, else None."""
+    dev = input.device.type
+    if (not input.is_cuda or not torch.is_autocast_enabled(dev)
+            or torch.get_autocast_dtype(dev) != torch.bfloat16 or not _conv_deterministic_lowp()):
+        return None
+    lib = _nat.native()
+    if lib is None:
+        return None
+    dt = torch.bfloat16
+    x = input.to(dt).contiguous(memory_format=torch.channels_last)
+    w = weight.to(dt)
+    b = bias.to(dt) if bias is not None else None
+    with torch.autocast(dev, enabled=False):
+        return _ConvLowpDet.apply(x, w, b, m.stride[0], m.padding[0], lib)
+
+
 def _pad4(t: torch.Tensor) -> torch.Tensor:
     """Zero-pad dim 1 (channels) of an NCHW-shaped tensor to a multiple of 4
     (the 3-channel stem: one pixel's channels = one float4), channels_last."""
@@ -678,6 +758,9 @@ class ImplicitGemmConv2d(nn.Conv2d):
         weight: torch.Tensor,
         bias: torch.Tensor | None,
     ) -> torch.Tensor:
+        y = _lowp_det_conv(self, input, weight, bias)
+        if y is not None:
+            return y
         lib = _gemm3_lib(input, weight, math=conv_kxk_math())
         if (lib is None or torch.is_autocast_enabled(input.device.type)
                 or not input.is_contiguous(memory_format=torch.channels_last)):
@@ -705,6 +788,9 @@ class StemConv2d(nn.Conv2d):
         weight: torch.Tensor,
         bias: torch.Tensor | None,
     ) -> torch.Tensor:
+        y = _lowp_det_conv(self, input, weight, bias)
+        if y is not None:
+            return y
         lib = _gemm3_lib(input, weight, math=conv_kxk_math())
         if (lib is None or not _conv_deterministic()
                 or torch.is_autocast_enabled(input.device.type)

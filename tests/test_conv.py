@@ -359,6 +359,85 @@ def test_deterministic_conv_backward(cuda, shape, stride, k, stem, monkeypatch) 
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('shape,stride,k,stem', [((32, 64, 56, 56, 64), 1, 3, False),
+                                                 ((32, 128, 56, 56, 128), 2, 3, False),
+                                                 ((32, 512, 7, 7, 512), 1, 3, False),
+                                                 ((3, 16, 9, 11, 40), 2, 3, False),
+                                                 ((8, 3, 224, 224, 64), 2, 7, True)])
+def test_deterministic_conv_backward_bf16(cuda, shape, stride, k, stem, monkeypatch) -> None:
+    """``KFAC_CONV_DETERMINISTIC_BF16=1`` (opt-in): under bf16 autocast the
+    3x3 convolutions and the stem run as bf16 GEMMs -- forward ``im2col(x) .
+    W^T``, input gradient ``dy . W`` + the native bf16 col2im, weight gradient
+    ``dy^T . patches`` -- with no MIOpen backward call.  Two passes are
+    bit-identical and output and gradients match float64 of the same bf16
+    operands to bf16 accuracy."""
+    from distributed_kfac_pytorch_amd.ops import _native
+    from distributed_kfac_pytorch_amd.ops import conv as cops
+
+    lib = _native.native()
+    assert lib is not None, _native.load_error()
+    calls: list = []
+
+    class Spy:
+        def __getattr__(self, name):  # type: ignore[no-untyped-def]
+            return getattr(lib, name)
+
+        def col2im_nhwc(self, *a):  # type: ignore[no-untyped-def]
+            calls.append('col2im')
+            return lib.col2im_nhwc(*a)
+
+    real_cb = torch.ops.aten.convolution_backward
+
+    class Aten:
+        def __getattr__(self, name):  # type: ignore[no-untyped-def]
+            return getattr(torch.ops.aten, name)
+
+        def convolution_backward(self, *a):  # type: ignore[no-untyped-def]
+            calls.append('miopen')
+            return real_cb(*a)
+
+    monkeypatch.setattr(_native, 'native', lambda: Spy())
+    monkeypatch.setattr(cops.torch.ops, 'aten', Aten(), raising=False)
+    monkeypatch.setenv('KFAC_CONV_DETERMINISTIC_BF16', '1')
+    n, c, h, w, co = shape
+    torch.manual_seed(0)
+    conv = nn.Conv2d(c, co, k, stride=stride, padding=k // 2, bias=False).to(cuda)
+    conv = conv.to(memory_format=torch.channels_last)
+    assert cops.use_implicit_gemm_conv(conv) == 1
+    x = torch.randn(n, c, h, w, device=cuda).contiguous(memory_format=torch.channels_last)
+    x = x.to(torch.bfloat16).requires_grad_(not stem)
+    with torch.autocast('cuda', dtype=torch.bfloat16):
+        y = conv(x)
+    assert y.dtype == torch.bfloat16
+    g = torch.randn_like(y)
+    grads = []
+    for _ in range(2):
+        calls.clear()
+        conv.weight.grad = None
+        x.grad = None
+        with torch.autocast('cuda', dtype=torch.bfloat16):
+            y = conv(x)
+        y.backward(g)
+        grads.append((None if stem else x.grad.clone(), conv.weight.grad.clone(), y.detach()))
+        assert 'miopen' not in calls, calls
+        assert ('col2im' in calls) == (not stem), calls
+    assert stem or torch.equal(grads[0][0], grads[1][0])
+    assert torch.equal(grads[0][1], grads[1][1]) and torch.equal(grads[0][2], grads[1][2])
+    xd = x.detach().double().requires_grad_(not stem)
+    wd = conv.weight.detach().to(torch.bfloat16).double().requires_grad_(True)
+    yd = torch.nn.functional.conv2d(xd, wd, None, stride=stride, padding=k // 2)
+    yd.backward(g.double())
+
+    def rel(a: torch.Tensor, b: torch.Tensor) -> float:
+        return float((a.detach().double() - b).norm() / b.norm())
+
+    assert rel(y, yd) < 1e-2, rel(y, yd)
+    assert rel(conv.weight.grad, wd.grad) < 1e-2, rel(conv.weight.grad, wd.grad)
+    if not stem:
+        assert rel(x.grad, xd.grad) < 1e-2, rel(x.grad, xd.grad)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize('shape,s', [((32, 256, 56, 56), 2), ((3, 12, 7, 9), 2), ((2, 8, 10, 10), 3)])
 def test_subsample_native_exact(cuda, shape, s) -> None:
     """The strided 1x1 convolutions' subsample and its adjoint on the native

@@ -111,6 +111,9 @@ def main() -> None:
     ap.add_argument('--fp32', action='store_true', help="the bench's fp32 step (no autocast)")
     ap.add_argument('--kxk', choices=('gemm', 'miopen'), default='gemm')
     ap.add_argument('--cudnn-det', type=int, default=1)
+    ap.add_argument('--fwd-check', action='store_true',
+                    help='step 0: report the first module (forward order) whose output '
+                         'differs between the twins')
     args = ap.parse_args()
     torch.backends.cudnn.deterministic = bool(args.cudnn_det)
     if args.det_algos:
@@ -134,8 +137,24 @@ def main() -> None:
             m['raw'].clear()
             m['x'].copy_(xb)
             m['y'].copy_(yb)
+        outs: dict = {'A': [], 'B': []}
+        hooks = []
+        if args.fwd_check and i == 0:
+            for tag, m in (('A', A), ('B', B)):
+                for name, mod in m['model'].named_modules():
+                    if name and not list(mod.children()):
+                        hooks.append(mod.register_forward_hook(
+                            lambda mod_, a_, o_, tag=tag, name=name: outs[tag].append(
+                                (name, o_.detach().clone()))))
         A['run']()
         B['run']()
+        for h in hooks:
+            h.remove()
+        if outs['A']:
+            first = next(((na, rel(oa, ob)) for (na, oa), (_, ob) in zip(outs['A'], outs['B'])
+                          if not torch.equal(oa, ob)), None)
+            print(json.dumps({'fwd_modules': len(outs['A']), 'first_fwd_mismatch': first}),
+                  flush=True)
         torch.cuda.synchronize()
         rec = {'step': i}
         if 'g' in A['raw'] and 'g' in B['raw']:
