@@ -629,17 +629,24 @@ def main() -> None:
         # fp32 model math outside MIOpen: the 1x1 convolutions' forward and
         # input-gradient GEMMs (ops/conv.py conv1x1_math; ~5e-6 relative,
         # TF32 -- the reference's fp32 convolution default on NVIDIA Ampere --
-        # is ~1e-3); 3x3 / 7x7 convolutions are MIOpen fp32, weight
-        # gradients hipBLASLt fp32
+        # is ~1e-3); the 3x3 convolutions and the stem's weight gradient on
+        # the native implicit GEMM, the stem's forward MIOpen fp32
+        from distributed_kfac_pytorch_amd.ops.conv import _conv_deterministic
         from distributed_kfac_pytorch_amd.ops.conv import conv1x1_math
         from distributed_kfac_pytorch_amd.ops.conv import conv_kxk_math
         kxk = conv_kxk_math() if args.conv_kxk == 'gemm' else 'fp32'
+        det = args.conv_kxk == 'gemm' and _conv_deterministic()
         line['model_math'] = {
             'conv1x1_fwd_dgrad': conv1x1_math() if args.dtype == 'fp32' else args.dtype,
             'conv1x1_wgrad': (conv1x1_math() if args.dtype == 'fp32' else args.dtype) +
                              ' from 256x128 weights up, fp32 below',
             'conv3x3_fwd_dgrad_stride1_wgrad_ge128ch': kxk if args.dtype == 'fp32' else args.dtype,
-            'conv3x3_strided_dgrad_64ch_wgrad_stem': 'fp32 (MIOpen)'}
+            # KFAC_CONV_DETERMINISTIC: strided input gradients as dy . W
+            # (gemm3) + fixed-order col2im, 64-channel / stem weight
+            # gradients native; the stem forward stays MIOpen fp32
+            'conv3x3_strided_dgrad_64ch_wgrad_stem': (
+                f'{kxk} (native, deterministic); stem forward fp32 (MIOpen)' if det
+                else 'fp32 (MIOpen)') if args.dtype == 'fp32' else args.dtype}
     line['host_issue_ms'] = res['host_issue_ms']
     hi = res['host_issue_ms']
     if not args.no_kfac and all(k in hi for k in ('plain', 'inverse')):
