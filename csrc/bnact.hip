@@ -27,9 +27,7 @@ namespace kfac {
 namespace {
 
 constexpr int BN_T = 256;
-constexpr int BN_FIN_CH = 32;  // channels per finalize block
-constexpr int BN_FIN_L = 16;   // lanes splitting the partial blocks
-constexpr int BN_FIN_T = BN_FIN_CH * BN_FIN_L;
+constexpr int BN_FIN_T = 512;  // finalize block: CH channels x BN_FIN_T / CH lanes
 
 typedef unsigned short us8 __attribute__((ext_vector_type(8)));
 
@@ -208,21 +206,28 @@ __global__ void __launch_bounds__(BN_T) bn_partial_kernel(
   }
 }
 
-// fp64 reduction of the partials: 32 channels x 16 lanes per block.
+// fp64 reduction of the partials: CH channels x (BN_FIN_T / CH) lanes per
+// block.  CH = 32 when there are few partial blocks; with many (a
+// convolution epilogue's partials: one per 64 output rows, 1568 for a
+// 56x56 layer at batch 32) fewer channels and more lanes per block, so each
+// lane walks fewer latency-bound loads (fin_ch_for).  The order is fixed for
+// a given (nblk, C): deterministic.
+template <int CH>
 __device__ __forceinline__ void reduce_parts(const float* __restrict__ part, int nblk, int C,
                                              int c, double& a, double& b) {
-  __shared__ double ra[BN_FIN_L][BN_FIN_CH], rb[BN_FIN_L][BN_FIN_CH];
-  const int lane = threadIdx.x / BN_FIN_CH, cl = threadIdx.x % BN_FIN_CH;
+  constexpr int L = BN_FIN_T / CH;
+  __shared__ double ra[L][CH], rb[L][CH];
+  const int lane = threadIdx.x / CH, cl = threadIdx.x % CH;
   double sa = 0.0, sb = 0.0;
   if (c < C) {
     // 4 independent loads in flight per step (the finalize is latency bound)
     int blk = lane;
-    for (; blk + 3 * BN_FIN_L < nblk; blk += 4 * BN_FIN_L) {
+    for (; blk + 3 * L < nblk; blk += 4 * L) {
       float va[4], vb[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        va[u] = part[((int64_t)(blk + u * BN_FIN_L) * 2) * C + c];
-        vb[u] = part[((int64_t)(blk + u * BN_FIN_L) * 2 + 1) * C + c];
+        va[u] = part[((int64_t)(blk + u * L) * 2) * C + c];
+        vb[u] = part[((int64_t)(blk + u * L) * 2 + 1) * C + c];
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -230,7 +235,7 @@ __device__ __forceinline__ void reduce_parts(const float* __restrict__ part, int
         sb += (double)vb[u];
       }
     }
-    for (; blk < nblk; blk += BN_FIN_L) {
+    for (; blk < nblk; blk += L) {
       sa += (double)part[((int64_t)blk * 2) * C + c];
       sb += (double)part[((int64_t)blk * 2 + 1) * C + c];
     }
@@ -240,24 +245,26 @@ __device__ __forceinline__ void reduce_parts(const float* __restrict__ part, int
   __syncthreads();
   a = 0.0;
   b = 0.0;
-#pragma unroll
-  for (int q = 0; q < BN_FIN_L; ++q) {
-    a += ra[q][cl];
-    b += rb[q][cl];
+  if (threadIdx.x < CH) {
+    for (int q = 0; q < L; ++q) {
+      a += ra[q][cl];
+      b += rb[q][cl];
+    }
   }
 }
 
 // stats[4][C]: mean, invstd, scale, shift
+template <int CH>
 __global__ void __launch_bounds__(BN_FIN_T) bn_fwd_finalize_kernel(
     const float* __restrict__ part, int nblk, int64_t M, int C,
     const float* __restrict__ weight, const float* __restrict__ bias,
     float* __restrict__ running_mean, float* __restrict__ running_var,
     int64_t* __restrict__ num_batches, float momentum, float eps,
     float* __restrict__ stats) {
-  const int c = blockIdx.x * BN_FIN_CH + threadIdx.x % BN_FIN_CH;
+  const int c = blockIdx.x * CH + threadIdx.x % CH;
   double s, q;
-  reduce_parts(part, nblk, C, c, s, q);
-  if (threadIdx.x >= BN_FIN_CH || c >= C) return;
+  reduce_parts<CH>(part, nblk, C, c, s, q);
+  if (threadIdx.x >= CH || c >= C) return;
   const double mean = s / (double)M;
   double var = q / (double)M - mean * mean;
   if (var < 0.0) var = 0.0;
@@ -337,14 +344,15 @@ __global__ void __launch_bounds__(BN_T) bn_fwd_apply_kernel(
 }
 
 // coef[3][C]: k1, k2, k3 with dx = k1*dz + k2 + k3*(x - mean)
+template <int CH>
 __global__ void __launch_bounds__(BN_FIN_T) bn_bwd_finalize_kernel(
     const float* __restrict__ part, int nblk, int64_t M, int C,
     const float* __restrict__ weight, const float* __restrict__ stats,
     float* __restrict__ dweight, float* __restrict__ dbias, float* __restrict__ coef) {
-  const int c = blockIdx.x * BN_FIN_CH + threadIdx.x % BN_FIN_CH;
+  const int c = blockIdx.x * CH + threadIdx.x % CH;
   double sdz, sdzx;
-  reduce_parts(part, nblk, C, c, sdz, sdzx);
-  if (threadIdx.x >= BN_FIN_CH || c >= C) return;
+  reduce_parts<CH>(part, nblk, C, c, sdz, sdzx);
+  if (threadIdx.x >= CH || c >= C) return;
   const double invstd = stats[C + c];
   const double w = weight ? weight[c] : 1.0;
   if (dweight) dweight[c] = (float)(sdzx * invstd);
@@ -804,6 +812,50 @@ int bn_max_c() { return 8 * BN_T; }
 
 namespace {
 
+// channels per finalize block: enough lanes that each walks <= ~16 of the
+// nblk partial rows (KFAC_BN_FIN_CH=32 pins the old 32 x 16 layout)
+int fin_ch_for(int nblk) {
+  static const int pin = [] {
+    const char* e = std::getenv("KFAC_BN_FIN_CH");
+    return e != nullptr ? std::atoi(e) : 0;
+  }();
+  if (pin == 4 || pin == 8 || pin == 16 || pin == 32) return pin;
+  int lanes = 16;
+  while (lanes < BN_FIN_T / 4 && lanes * 16 < nblk) lanes *= 2;
+  return BN_FIN_T / lanes;
+}
+
+void launch_fwd_finalize(const float* part, int nblk, int64_t M, int C, const float* weight,
+                         const float* bias, float* running_mean, float* running_var,
+                         int64_t* num_batches, float momentum, float eps, float* stats,
+                         hipStream_t s) {
+  const int ch = fin_ch_for(nblk);
+#define KFAC_FWD_FIN(CHV)                                                                     \
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel<CHV>, dim3((unsigned)ceil_div(C, CHV)),            \
+                     dim3(BN_FIN_T), 0, s, part, nblk, M, C, weight, bias, running_mean,       \
+                     running_var, num_batches, momentum, eps, stats)
+  if (ch == 4) KFAC_FWD_FIN(4);
+  else if (ch == 8) KFAC_FWD_FIN(8);
+  else if (ch == 16) KFAC_FWD_FIN(16);
+  else KFAC_FWD_FIN(32);
+#undef KFAC_FWD_FIN
+}
+
+void launch_bwd_finalize(const float* part, int nblk, int64_t M, int C, const float* weight,
+                         const float* stats, float* dweight, float* dbias, float* coef,
+                         hipStream_t s) {
+  const int ch = fin_ch_for(nblk);
+#define KFAC_BWD_FIN(CHV)                                                                     \
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel<CHV>, dim3((unsigned)ceil_div(C, CHV)),            \
+                     dim3(BN_FIN_T), 0, s, part, nblk, M, C, weight, stats, dweight, dbias,    \
+                     coef)
+  if (ch == 4) KFAC_BWD_FIN(4);
+  else if (ch == 8) KFAC_BWD_FIN(8);
+  else if (ch == 16) KFAC_BWD_FIN(16);
+  else KFAC_BWD_FIN(32);
+#undef KFAC_BWD_FIN
+}
+
 template <typename E>
 void bn_forward_t(const E* x, const E* res, const float* weight, const float* bias,
                   float* running_mean, float* running_var, int64_t* num_batches, float momentum,
@@ -822,9 +874,8 @@ void bn_forward_t(const E* x, const E* res, const float* weight, const float* bi
                          running_var, num_batches, momentum, eps, relu, stats, y);
       return;
     }
-    hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((unsigned)ceil_div(C, BN_FIN_CH)),
-                       dim3(BN_FIN_T), 0, s, ext_part, ext_p, M, C, weight, bias, running_mean,
-                       running_var, num_batches, momentum, eps, stats);
+    launch_fwd_finalize(ext_part, ext_p, M, C, weight, bias, running_mean, running_var,
+                        num_batches, momentum, eps, stats, s);
     hipLaunchKernelGGL(bn_fwd_apply_kernel<E>, dim3(apply_grid(M, C)), dim3(BN_T), 0, s, x, res,
                        stats, relu, M, C, y);
     return;
@@ -849,9 +900,8 @@ void bn_forward_t(const E* x, const E* res, const float* weight, const float* bi
   const size_t shm = (size_t)2 * rpi * C * sizeof(float);
   hipLaunchKernelGGL((bn_partial_kernel<E, 0>), dim3(nblk), dim3(BN_T), shm, s, x, nullptr,
                      nullptr, nullptr, 0, M, C, rpb, part);
-  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((unsigned)ceil_div(C, BN_FIN_CH)),
-                     dim3(BN_FIN_T), 0, s, part, nblk, M, C, weight, bias, running_mean,
-                     running_var, num_batches, momentum, eps, stats);
+  launch_fwd_finalize(part, nblk, M, C, weight, bias, running_mean, running_var, num_batches,
+                      momentum, eps, stats, s);
   hipLaunchKernelGGL(bn_fwd_apply_kernel<E>, dim3(apply_grid(M, C)), dim3(BN_T), 0, s, x, res,
                      stats, relu, M, C, y);
 }
@@ -889,8 +939,7 @@ void bn_backward_t(const E* x, const E* dy, const E* y, const float* weight, con
   const size_t shm = (size_t)2 * rpi * C * sizeof(float);
   hipLaunchKernelGGL((bn_partial_kernel<E, 1>), dim3(nblk), dim3(BN_T), shm, s, x, dy, y, stats,
                      relu, M, C, rpb, part);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((unsigned)ceil_div(C, BN_FIN_CH)),
-                     dim3(BN_FIN_T), 0, s, part, nblk, M, C, weight, stats, dweight, dbias, coef);
+  launch_bwd_finalize(part, nblk, M, C, weight, stats, dweight, dbias, coef, s);
   hipLaunchKernelGGL(bn_bwd_apply_kernel<E>, dim3(apply_grid(M, C)), dim3(BN_T), 0, s, x, dy, y,
                      stats, coef, relu, M, C, dx, dres);
 }
