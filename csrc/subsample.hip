@@ -9,6 +9,8 @@
 // reading the gradient only at the kept pixels.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace kfac {
 
 namespace {
@@ -141,11 +143,70 @@ __global__ void __launch_bounds__(256) sum_splits_kernel(const float4* __restric
   }
 }
 
+// Few outputs, many splits (a small weight gradient split over many pixel
+// blocks): G lanes per output float4 each sum every G-th partial, then the
+// G lane sums are added in lane order through LDS -- fixed order for a
+// given (S, T), so deterministic.  Thread t owns output e = t % E (E =
+// 256 / G consecutive outputs: coalesced) and lane g = t / E.
+template <int G>
+__global__ void __launch_bounds__(256) sum_splits_grouped_kernel(const float4* __restrict__ part,
+                                                                 float4* __restrict__ out, int S,
+                                                                 int64_t T4) {
+  constexpr int E = 256 / G;
+  __shared__ float4 red[G][E];
+  const int e = threadIdx.x % E, g = threadIdx.x / E;
+  const int64_t i = (int64_t)blockIdx.x * E + e;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i < T4) {
+    int s = g;
+    for (; s + 3 * G < S; s += 4 * G) {
+      const float4 b0 = part[(int64_t)s * T4 + i];
+      const float4 b1 = part[(int64_t)(s + G) * T4 + i];
+      const float4 b2 = part[(int64_t)(s + 2 * G) * T4 + i];
+      const float4 b3 = part[(int64_t)(s + 3 * G) * T4 + i];
+      a.x += b0.x; a.y += b0.y; a.z += b0.z; a.w += b0.w;
+      a.x += b1.x; a.y += b1.y; a.z += b1.z; a.w += b1.w;
+      a.x += b2.x; a.y += b2.y; a.z += b2.z; a.w += b2.w;
+      a.x += b3.x; a.y += b3.y; a.z += b3.z; a.w += b3.w;
+    }
+    for (; s < S; s += G) {
+      const float4 b = part[(int64_t)s * T4 + i];
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+  }
+  red[g][e] = a;
+  __syncthreads();
+  if (g == 0 && i < T4) {
+#pragma unroll 4
+    for (int q = 1; q < G; ++q) {
+      const float4 b = red[q][e];
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    out[i] = a;
+  }
+}
+
 }  // namespace
 
 void sum_splits(const float* part, float* out, int S, int64_t T, hipStream_t s) {
   const int64_t T4 = T / 4;
   if (T4 == 0 || S <= 0) return;
+  // lanes per output: enough threads to cover ~64K with at least 4
+  // partials per lane
+  static const int gmax = [] {
+    const char* e = std::getenv("KFAC_SUM_SPLITS_GROUP");
+    return e != nullptr ? std::atoi(e) : 16;
+  }();
+  int G = 1;
+  while (G < gmax && T4 * G < 65536 && 4 * (2 * G) <= S) G *= 2;
+#define KFAC_SSG(GV)                                                                    \
+  sum_splits_grouped_kernel<GV><<<(unsigned)ceil_div(T4, 256 / GV), 256, 0, s>>>(       \
+      (const float4*)part, (float4*)out, S, T4)
+  if (G >= 16) { KFAC_SSG(16); return; }
+  if (G == 8) { KFAC_SSG(8); return; }
+  if (G == 4) { KFAC_SSG(4); return; }
+  if (G == 2) { KFAC_SSG(2); return; }
+#undef KFAC_SSG
   int64_t b = ceil_div(T4, 256);
   if (b > 4096) b = 4096;
   sum_splits_kernel<<<(unsigned)b, 256, 0, s>>>((const float4*)part, (float4*)out, S, T4);

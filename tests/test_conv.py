@@ -460,10 +460,12 @@ def test_subsample_native_exact(cuda, shape, s) -> None:
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('shape', [(7, 256, 64), (256, 64, 256), (3, 5, 7), (1, 8, 4)])
+@pytest.mark.parametrize('shape', [(7, 256, 64), (256, 64, 256), (3, 5, 7), (1, 8, 4),
+                                   (64, 64, 576), (37, 16, 36), (128, 4, 8)])
 def test_sum_splits_matches_torch(cuda, shape) -> None:
     """The split-K partial sum kernel (csrc/subsample.hip ``sum_splits``,
-    fixed order) equals ``part.sum(0)`` to fp32 rounding, with the torch
+    fixed order; lane-grouped when few outputs meet many splits) equals
+    ``part.sum(0)`` to fp32 rounding and repeats bit for bit, with the torch
     fallback for element counts that are not a multiple of 4."""
     from distributed_kfac_pytorch_amd.ops import _native
 
@@ -476,4 +478,4 @@ def test_sum_splits_matches_torch(cuda, shape) -> None:
     assert float((got.double() - ref).abs().max() / ref.abs().max().clamp_min(1e-30)) < 1e-5
     out = torch.empty(shape[1:], device=cuda)
     assert lib.sum_splits(part, out).data_ptr() == out.data_ptr()
-    torch.testing.assert_close(out, got)
+    assert torch.equal(out, got)  # fixed summation order
