@@ -458,7 +458,7 @@ class _Conv1x1Gemm(torch.autograd.Function):
         # 56-58 at 512 x 256 / 1024 x 512); hipBLASLt's slabs keep the small
         # 64-channel weights (37 vs 48 us): profiles/r5/conv1x1_gemm3_probe.jsonl
         if (lib is not None and _wgrad_1x1() == 'native'
-                and gy.shape[1] * x.shape[1] >= 32768):
+                and gy.shape[1] * x.shape[1] >= int(getenv('KFAC_CONV1X1_WGRAD_MIN', '32768'))):
             gw = _wgrad_native(lib, gy, x)
         elif ctx.needs_input_grad[1]:
             m = gy.shape[0]
