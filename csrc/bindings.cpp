@@ -302,6 +302,32 @@ void syrk(const at::Tensor& x, at::Tensor& C, bool bias, double alpha,
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   int sp = splits > 0 ? (int)splits : (int)kfac::syrk_workspace_splits(N, D);
   at::Tensor ws = syrk_ws(C, D, sp);
+  // fp32 input on the bf16x3 path with several column tiles: every element
+  // is otherwise split to bf16 hi / lo once per column tile that reads it
+  // (VALU-bound: 45-50 TFLOP/s at D = 1024-2048 vs 110-180 for the
+  // pre-split patch SYRKs, profiles/r6/syrk_dense_planes/).  Split it once
+  // into contiguous planes and run the planes kernel as a 1x1 "convolution"
+  // over a 1x1 image per row, when the input has >= 2M elements (below it
+  // the extra pass costs more than it saves: 1568 x 512 went 28 -> 30 us).
+  // KFAC_SYRK_DENSE_PLANES_MIN_D: smallest D (default 257, three or more
+  // tiles); 0 disables.
+  static const int64_t planes_min_d = [] {
+    const char* e = std::getenv("KFAC_SYRK_DENSE_PLANES_MIN_D");
+    return e != nullptr ? (int64_t)std::atoll(e) : (int64_t)257;
+  }();
+  const int64_t elems = N * K;
+  if (x.scalar_type() == at::kFloat && !fp32_exact && planes_min_d > 0 && D >= planes_min_d &&
+      K % 8 == 0 && ldx % 4 == 0 && (reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0 &&
+      N < (1LL << 24) && elems >= (1LL << 21) && elems < (1LL << 29)) {
+    at::Tensor planes = at::empty({2 * elems}, x.options().dtype(at::kBFloat16));
+    kfac::syrk_split_planes(x.data_ptr<float>(), N, 1, 1, (int)K, ldx, K, K,
+                            reinterpret_cast<uint16_t*>(planes.data_ptr()), cur_stream());
+    kfac::ConvGeom gp{K, K, K, 1, 1, (int32_t)K, 1, 1, 1, 0, 0, 1, 1, elems, 0};
+    kfac::syrk(kfac::kF32, planes.data_ptr(), N, K, /*ldx=*/K, bias, C.data_ptr<float>(), D,
+               ldc, (float)alpha, (float)beta, sp, cur_stream(), &gp,
+               ws.defined() ? ws.data_ptr<float>() : nullptr, syrk_ascale(ascale, C), false);
+    return;
+  }
   kfac::syrk(dtype_tag(x), x.data_ptr(), N, K, ldx, bias,
              C.data_ptr<float>(), D, ldc, (float)alpha, (float)beta,
              sp, cur_stream(), nullptr, ws.defined() ? ws.data_ptr<float>() : nullptr,

@@ -503,6 +503,40 @@ def test_syrk_fp32_input_modes(cuda, exact):
     assert torch.equal(out, out.t())
 
 
+@pytest.mark.parametrize('n,k,width,bias,splits', [
+    (3000, 1024, 1024, True, 0),   # dense fp32, D >= 257, >= 2M elements: planes
+    (4500, 512, 520, False, 3),    # strided rows, forced split-K
+    (1100, 2048, 2048, True, 1),   # single split
+    (1000, 512, 512, True, 0),     # below 2M elements: the in-loop split
+])
+def test_syrk_dense_planes_fp32(cuda, n, k, width, bias, splits):
+    """Dense fp32 SYRK inputs with D >= KFAC_SYRK_DENSE_PLANES_MIN_D (257)
+    and >= 2M elements are split once into bf16 hi / lo planes and run on
+    the planes kernel:
+    fp32-class against fp64, exactly symmetric, bit-identical on repeat, and
+    the packed-triangle output equals the dense one's upper triangle."""
+    torch.manual_seed(n + k)
+    lib = _native.native()
+    x = (2 * torch.randn(n, width, device=cuda))[:, :k]
+    d = k + int(bias)
+    c0 = torch.randn(d, d, device=cuda)
+    c0 = (c0 + c0.t()) / 2
+    alpha, beta = 0.5 / n, 0.9
+    outs = []
+    for _ in range(2):
+        out = c0.clone()
+        lib.syrk(x, out, bias, alpha, beta, splits)
+        outs.append(out)
+    assert torch.equal(outs[0], outs[1])
+    assert torch.equal(outs[0], outs[0].t())
+    ref = beta * c0.double() + alpha * _ref_cov(x, bias)
+    rel = (outs[0].double() - ref).abs().max().item() / ref.abs().max().item()
+    assert rel < 1e-5, rel
+    packed = comm_pack.triu_pack(c0)
+    lib.syrk(x, packed, bias, alpha, beta, splits)
+    torch.testing.assert_close(packed, comm_pack.triu_pack(outs[0]), rtol=1e-6, atol=1e-6)
+
+
 def test_eigh_many_repairs_nonfinite_results(cuda, monkeypatch):
     """A solver result with NaN (e.g. a divide-and-conquer failure that
     rocSOLVER reports only on the device) is detected and re-solved."""
