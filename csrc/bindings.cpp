@@ -87,6 +87,10 @@ void subsample_bwd(const float* g, float* gx, int N, int H, int W, int C, int sh
 void subsample_bwd_acc(const float* g, float* gx, int N, int H, int W, int C, int sh, int sw,
                    hipStream_t s);
 int gemm3_conv_splits(int N, int H, int W, int C, int Cout, int kh, int kw, int stride, int pad);
+void maxpool_nhwc_fwd(int dtype, const void* x, void* y, uint8_t* code, int N, int H, int W,
+                      int C, int OH, int OW, int k, int s, int p, hipStream_t st);
+void maxpool_nhwc_bwd(int dtype, const void* gy, const uint8_t* code, void* gx, int N, int H,
+                      int W, int C, int OH, int OW, int k, int s, int p, hipStream_t st);
 void col2im_nhwc(int dtype, const void* cols, void* gx, int B, int H, int W, int C, int OH,
                  int OW, int kh, int kw, int sh, int sw, int ph, int pw, hipStream_t s);
 int gemm3_wgrad_splits(int pixels, int Cout, int kcols);
@@ -1350,6 +1354,54 @@ at::Tensor col2im_nhwc(const at::Tensor& cols, int64_t B, int64_t C, int64_t H, 
   return gx;
 }
 
+// max_pool2d of a channels_last fp32 (C % 4 == 0) / bf16 (C % 8 == 0)
+// tensor (square kernel k, stride s, padding p, dilation 1, floor mode):
+// returns (y, code) with code the uint8 [N, OH, OW, C] window position of
+// each maximum (csrc/pool.hip)
+static void check_pool_input(const at::Tensor& t, const char* what) {
+  check_cuda(t, what);
+  const bool bf = t.scalar_type() == at::kBFloat16;
+  TORCH_CHECK((bf || t.scalar_type() == at::kFloat) && t.dim() == 4 &&
+                  t.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  t.size(1) % (bf ? 8 : 4) == 0 &&
+                  (reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0,
+              what, ": 16-byte aligned channels_last fp32 (C % 4 == 0) or bf16 (C % 8 == 0)");
+}
+
+std::vector<at::Tensor> maxpool_nhwc_fwd(const at::Tensor& x, int64_t k, int64_t s, int64_t p) {
+  check_pool_input(x, "maxpool input");
+  TORCH_CHECK(k >= 1 && k <= 15 && s >= 1 && p >= 0 && 2 * p <= k, "maxpool: geometry");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int64_t OH = (H + 2 * p - k) / s + 1, OW = (W + 2 * p - k) / s + 1;
+  TORCH_CHECK(OH >= 1 && OW >= 1 && N * H * W * C < ((int64_t)1 << 40), "maxpool: shape");
+  auto y = at::empty({N, C, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto code = at::empty({N, OH, OW, C}, x.options().dtype(at::kByte));
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  kfac::maxpool_nhwc_fwd(dtype_tag(x), x.data_ptr(), y.data_ptr(), code.data_ptr<uint8_t>(),
+                         (int)N, (int)H, (int)W, (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)p,
+                         cur_stream());
+  return {y, code};
+}
+
+at::Tensor maxpool_nhwc_bwd(const at::Tensor& gy, const at::Tensor& code, int64_t H, int64_t W,
+                            int64_t k, int64_t s, int64_t p) {
+  check_pool_input(gy, "maxpool gradient");
+  const int64_t N = gy.size(0), C = gy.size(1), OH = gy.size(2), OW = gy.size(3);
+  TORCH_CHECK(k >= 1 && k <= 15 && s >= 1 && p >= 0 && 2 * p <= k &&
+                  OH == (H + 2 * p - k) / s + 1 && OW == (W + 2 * p - k) / s + 1,
+              "maxpool_bwd: geometry");
+  TORCH_CHECK(code.scalar_type() == at::kByte && code.is_contiguous() && code.dim() == 4 &&
+                  code.size(0) == N && code.size(1) == OH && code.size(2) == OW &&
+                  code.size(3) == C && code.device() == gy.device(),
+              "maxpool_bwd: code must be the forward's uint8 [N, OH, OW, C]");
+  auto gx = at::empty({N, C, H, W}, gy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  c10::hip::HIPGuardMasqueradingAsCUDA g(gy.device());
+  kfac::maxpool_nhwc_bwd(dtype_tag(gy), gy.data_ptr(), code.data_ptr<uint8_t>(), gx.data_ptr(),
+                         (int)N, (int)H, (int)W, (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)p,
+                         cur_stream());
+  return gx;
+}
+
 void gemm3_grouped(const at::Tensor& table, int64_t nlayers, int64_t total_tiles,
                    bool a_kc, bool b_kc) {
   check_cuda(table, "table");
@@ -1627,6 +1679,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm3_grouped", &gemm3_grouped);
   m.def("subsample_fwd", &subsample_fwd, py::arg("x"), py::arg("sh"), py::arg("sw"));
   m.def("sum_splits", &sum_splits, py::arg("part"), py::arg("out") = py::none());
+  m.def("maxpool_nhwc_fwd", &maxpool_nhwc_fwd, py::arg("x"), py::arg("k"), py::arg("s"),
+        py::arg("p"));
+  m.def("maxpool_nhwc_bwd", &maxpool_nhwc_bwd, py::arg("gy"), py::arg("code"), py::arg("H"),
+        py::arg("W"), py::arg("k"), py::arg("s"), py::arg("p"));
   m.def("col2im_nhwc", &col2im_nhwc, py::arg("cols"), py::arg("B"), py::arg("C"), py::arg("H"),
         py::arg("W"), py::arg("kh"), py::arg("kw"), py::arg("stride"), py::arg("pad"));
   m.def("subsample_bwd_acc", &subsample_bwd_acc, py::arg("gy"), py::arg("gx"), py::arg("sh"),

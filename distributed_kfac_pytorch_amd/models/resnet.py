@@ -24,6 +24,7 @@ from distributed_kfac_pytorch_amd.ops.conv import ResidualGradSlot
 from distributed_kfac_pytorch_amd.ops.conv import StridedConv1x1
 from distributed_kfac_pytorch_amd.ops.conv import _fuse_residual_grad
 from distributed_kfac_pytorch_amd.ops.conv import residual_tap
+from distributed_kfac_pytorch_amd.ops.pool import MaxPool2dNHWC
 
 __all__ = [
     'Bottleneck',
@@ -163,7 +164,8 @@ class ResNet(nn.Module):
         self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
         self.bn1 = BatchNormAct2d(64)
         self.relu = nn.ReLU(inplace=True)
-        self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
+        # native NHWC kernels on the GPU (ops/pool.py), nn.MaxPool2d elsewhere
+        self.maxpool = MaxPool2dNHWC(kernel_size=3, stride=2, padding=1)
         self.layer1 = self._make_layer(block, 64, layers[0])
         self.layer2 = self._make_layer(block, 128, layers[1], stride=2)
         self.layer3 = self._make_layer(block, 256, layers[2], stride=2)
