@@ -471,7 +471,13 @@ class _Conv1x1Gemm(torch.autograd.Function):
                     part = torch.bmm(a, b, out_dtype=torch.float32)
                 else:
                     part = torch.bmm(a, b)
-                gw = part.sum(0, dtype=torch.promote_types(w.dtype, torch.float32)).to(w.dtype)
+                lib = _nat.native() if part.is_cuda and w.dtype == torch.float32 else None
+                if lib is not None:
+                    # fixed-order slab sum (csrc/subsample.hip sum_splits):
+                    # one pass instead of torch's dim-0 reduction
+                    gw = lib.sum_splits(part)
+                else:
+                    gw = part.sum(0, dtype=torch.promote_types(w.dtype, torch.float32)).to(w.dtype)
             else:
                 gw = gy.t() @ x
         gb = gy.sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
