@@ -27,6 +27,7 @@
 #include "common.h"
 #include "descs.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace kfac {
@@ -958,7 +959,19 @@ int64_t syrk_workspace_splits(int64_t N, int64_t D) {
   // unless the triangle has so few tiles that 64 splits cannot fill the
   // chip (the 147-wide A factor of ResNet's 7x7 stem: 3 tiles x 64 splits
   // = 192 blocks for 401k rows)
-  const int64_t cap = tiles * 64 >= target_blocks / 2 ? 64 : ceil_div(target_blocks, tiles);
+  // KFAC_SYRK_ONE_TILE_SPLITS: the cap for a one-tile triangle (D <= 128:
+  // the 64-channel G factors, 100k-400k rows), whose blocks are otherwise
+  // a latency-bound chain of ~200 k-tiles each
+  static const int64_t one_tile_cap = [] {
+    const char* e = std::getenv("KFAC_SYRK_ONE_TILE_SPLITS");
+    const long v = e != nullptr ? std::atol(e) : 0;
+    return (int64_t)(v > 0 ? v : 64);
+  }();
+  int64_t cap = tiles * 64 >= target_blocks / 2 ? 64 : ceil_div(target_blocks, tiles);
+  if (tiles == 1 && one_tile_cap > cap) {
+    cap = one_tile_cap;
+    splits = std::min<int64_t>(one_tile_cap, std::min(max_by_rows, max_by_ws));
+  }
   if (splits > cap) splits = cap;
   if (splits < 2) splits = 1;
   return splits;
