@@ -313,11 +313,11 @@ void syrk(const at::Tensor& x, at::Tensor& C, bool bias, double alpha,
   // into contiguous planes and run the planes kernel as a 1x1 "convolution"
   // over a 1x1 image per row, when the input has >= 2M elements (below it
   // the extra pass costs more than it saves: 1568 x 512 went 28 -> 30 us).
-  // KFAC_SYRK_DENSE_PLANES_MIN_D: smallest D (default 257, three or more
-  // tiles); 0 disables.
+  // KFAC_SYRK_DENSE_PLANES_MIN_D: smallest D (default 129, two or more
+  // tiles: 100352 x 256 went 203 -> 157 us); 0 disables.
   static const int64_t planes_min_d = [] {
     const char* e = std::getenv("KFAC_SYRK_DENSE_PLANES_MIN_D");
-    return e != nullptr ? (int64_t)std::atoll(e) : (int64_t)257;
+    return e != nullptr ? (int64_t)std::atoll(e) : (int64_t)129;
   }();
   const int64_t elems = N * K;
   if (x.scalar_type() == at::kFloat && !fp32_exact && planes_min_d > 0 && D >= planes_min_d &&

@@ -504,13 +504,14 @@ def test_syrk_fp32_input_modes(cuda, exact):
 
 
 @pytest.mark.parametrize('n,k,width,bias,splits', [
-    (3000, 1024, 1024, True, 0),   # dense fp32, D >= 257, >= 2M elements: planes
+    (3000, 1024, 1024, True, 0),   # dense fp32, D >= 129, >= 2M elements: planes
     (4500, 512, 520, False, 3),    # strided rows, forced split-K
     (1100, 2048, 2048, True, 1),   # single split
     (1000, 512, 512, True, 0),     # below 2M elements: the in-loop split
+    (9000, 256, 256, False, 0),    # two tiles
 ])
 def test_syrk_dense_planes_fp32(cuda, n, k, width, bias, splits):
-    """Dense fp32 SYRK inputs with D >= KFAC_SYRK_DENSE_PLANES_MIN_D (257)
+    """Dense fp32 SYRK inputs with D >= KFAC_SYRK_DENSE_PLANES_MIN_D (129)
     and >= 2M elements are split once into bf16 hi / lo planes and run on
     the planes kernel:
     fp32-class against fp64, exactly symmetric, bit-identical on repeat, and
