@@ -188,10 +188,10 @@ def test_implicit_gemm_conv_matches_float64(cuda, shape, stride, k, monkeypatch)
     """fp32 ``ImplicitGemmConv2d`` (3x3 pad 1, and the 7x7 stride-2 stem
     with its 3 channels padded to 4): forward on the native implicit GEMM
     (split-K on small images), stride-1 input gradient as the native
-    convolution of dy with the flipped kernel, weight gradient native from
-    128 channels (and for the stem), MIOpen otherwise -- output and both
-    gradients match float64 to fp32-class accuracy, and the native kernel
-    runs."""
+    convolution of dy with the flipped kernel, strided input gradient as dy .
+    W + col2im and every weight gradient native (KFAC_CONV_DETERMINISTIC,
+    the default) -- output and both gradients match float64 to fp32-class
+    accuracy, and the native kernel runs."""
     from distributed_kfac_pytorch_amd.ops import _native
     from distributed_kfac_pytorch_amd.ops.conv import ImplicitGemmConv2d
 
