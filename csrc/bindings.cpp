@@ -86,6 +86,7 @@ void subsample_bwd(const float* g, float* gx, int N, int H, int W, int C, int sh
                    hipStream_t s);
 void subsample_bwd_acc(const float* g, float* gx, int N, int H, int W, int C, int sh, int sw,
                    hipStream_t s);
+void pad_channels4(const float* x, float* y, int64_t pixels, int C, hipStream_t s);
 int gemm3_conv_splits(int N, int H, int W, int C, int Cout, int kh, int kw, int stride, int pad);
 void maxpool_nhwc_fwd(int dtype, const void* x, void* y, uint8_t* code, int N, int H, int W,
                       int C, int OH, int OW, int k, int s, int p, hipStream_t st);
@@ -1315,6 +1316,21 @@ at::Tensor subsample_bwd(const at::Tensor& gy, int64_t H, int64_t W, int64_t sh,
   return gx;
 }
 
+// [N, C, H, W] channels_last fp32 -> [N, ceil4(C), H, W] channels_last,
+// the extra channels zero (csrc/subsample.hip pad_channels4)
+at::Tensor pad_channels4(const at::Tensor& x) {
+  check_cuda(x, "pad_channels4 input");
+  TORCH_CHECK(x.scalar_type() == at::kFloat && x.dim() == 4 &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "pad_channels4: channels_last fp32 [N, C, H, W]");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int64_t C4 = (C + 3) / 4 * 4;
+  auto y = at::empty({N, C4, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  kfac::pad_channels4(x.data_ptr<float>(), y.data_ptr<float>(), N * H * W, (int)C, cur_stream());
+  return y;
+}
+
 // gx += adjoint(gy), in place: gx is the other branch's full-size gradient
 void subsample_bwd_acc(const at::Tensor& gy, const at::Tensor& gx, int64_t sh, int64_t sw) {
   check_nhwc4(gy, "subsample gradient");
@@ -1685,6 +1701,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("W"), py::arg("k"), py::arg("s"), py::arg("p"));
   m.def("col2im_nhwc", &col2im_nhwc, py::arg("cols"), py::arg("B"), py::arg("C"), py::arg("H"),
         py::arg("W"), py::arg("kh"), py::arg("kw"), py::arg("stride"), py::arg("pad"));
+  m.def("pad_channels4", &pad_channels4, py::arg("x"));
   m.def("subsample_bwd_acc", &subsample_bwd_acc, py::arg("gy"), py::arg("gx"), py::arg("sh"),
         py::arg("sw"));
   m.def("subsample_bwd", &subsample_bwd, py::arg("gy"), py::arg("h"), py::arg("w"),

@@ -72,6 +72,24 @@ __global__ void __launch_bounds__(256) subsample_bwd_acc_kernel(
   }
 }
 
+// y[p][0..C4) = x[p][0..C) zero-padded to a multiple of 4 channels, NHWC:
+// one float4 of y per thread (the 3-channel stem input for the native
+// weight gradient: one pass instead of a zero fill plus a cat)
+__global__ void __launch_bounds__(256) pad_channels4_kernel(const float* __restrict__ x,
+                                                            float4* __restrict__ y, int64_t total4,
+                                                            int C, int C4) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total4;
+       i += (int64_t)gridDim.x * 256) {
+    const int64_t pix = i / (C4 / 4);
+    const int c0 = (int)(i - pix * (C4 / 4)) * 4;
+    const float* px = x + pix * C;
+    float v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = c0 + e < C ? px[c0 + e] : 0.f;
+    y[i] = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
 int grid_for(int64_t total4) {
   const int64_t b = ceil_div(total4, 256);
   return (int)(b < 8192 ? (b > 0 ? b : 1) : 8192);
@@ -95,6 +113,13 @@ void subsample_bwd(const float* g, float* gx, int N, int H, int W, int C, int sh
   if (total4 == 0) return;
   subsample_bwd_kernel<<<grid_for(total4), 256, 0, s>>>(
       (const float4*)g, (float4*)gx, total4, C / 4, H, W, Ho, Wo, sh, sw);
+}
+
+void pad_channels4(const float* x, float* y, int64_t pixels, int C, hipStream_t s) {
+  const int C4 = (C + 3) / 4 * 4;
+  const int64_t total4 = pixels * (C4 / 4);
+  if (total4 == 0) return;
+  pad_channels4_kernel<<<grid_for(total4), 256, 0, s>>>(x, (float4*)y, total4, C, C4);
 }
 
 void subsample_bwd_acc(const float* g, float* gx, int N, int H, int W, int C, int sh, int sw,

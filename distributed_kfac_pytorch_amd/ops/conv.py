@@ -725,6 +725,11 @@ def _pad4(t: torch.Tensor) -> torch.Tensor:
     c = t.shape[1]
     if c % 4 == 0:
         return t
+    if (t.is_cuda and t.dtype == torch.float32
+            and t.is_contiguous(memory_format=torch.channels_last)):
+        lib = _nat.native()
+        if lib is not None:
+            return lib.pad_channels4(t)  # one pass, no zero fill + cat
     z = t.new_zeros(t.shape[0], 4 - c % 4, *t.shape[2:])
     return torch.cat([t, z], 1).contiguous(memory_format=torch.channels_last)
 

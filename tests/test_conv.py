@@ -438,6 +438,26 @@ def test_deterministic_conv_backward_bf16(cuda, shape, stride, k, stem, monkeypa
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('shape', [(32, 3, 224, 224), (2, 5, 7, 9), (64, 3, 7, 7), (1, 1, 3, 3)])
+def test_pad_channels4_native_exact(cuda, shape) -> None:
+    """``pad_channels4`` (csrc/subsample.hip): the channels_last input
+    zero-padded to a multiple of 4 channels in one pass, equal to torch's
+    cat with zeros, channels_last."""
+    from distributed_kfac_pytorch_amd.ops import _native
+    from distributed_kfac_pytorch_amd.ops.conv import _pad4
+
+    lib = _native.native()
+    assert lib is not None, _native.load_error()
+    x = torch.randn(*shape, device=cuda).contiguous(memory_format=torch.channels_last)
+    c = shape[1]
+    ref = torch.cat([x, x.new_zeros(shape[0], (4 - c % 4) % 4, *shape[2:])], 1)
+    got = lib.pad_channels4(x)
+    assert torch.equal(got, ref)
+    assert got.is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(_pad4(x), ref)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize('shape,s', [((32, 256, 56, 56), 2), ((3, 12, 7, 9), 2), ((2, 8, 10, 10), 3)])
 def test_subsample_native_exact(cuda, shape, s) -> None:
     """The strided 1x1 convolutions' subsample and its adjoint on the native
